@@ -1,0 +1,140 @@
+/*
+ * pptk_rx.h -- C-ABI of the MI355X batch receive transform.
+ *
+ * One call turns a batch of Ethernet frames into one 64-byte record per
+ * frame: IPv4 header checksum, TCP/UDP (v4/v6) checksum, fixed-format
+ * L2/L3/L4 field extraction and a SipHash-2-4 flow hash of the 5-tuple.
+ *
+ * Where it plugs in: between ldp_in_nextpkts() and ldp_in_deallocate_some()
+ * of an LDP rx loop (reference ldp/ldprecv.c:60-70, ldp/ldprecvmt.c:54-64,
+ * ldp/ldpfwdmt.c:72-89).  The reference has no batch entry point: its rx
+ * loops call the per-packet primitives below, one packet at a time:
+ *   ip_hdr_cksum_calc      iphdr/ipcksum.c:39-49
+ *   tcp_cksum_calc         iphdr/ipcksum.c:51-68
+ *   tcp6_cksum_calc        iphdr/ipcksum.c:74-115
+ *   udp_cksum_calc         iphdr/ipcksum.c:117-134
+ *   udp6_cksum_calc        iphdr/ipcksum.c:140-181
+ *   ipv6_const_proto_hdr_2 iphdr/iphdr.h:804-860
+ *   siphash_buf            misc/siphash.h:214-229
+ *   ip_permitted hashing   iphash/iphash.c:157-162 (v4), :108-120 (v6)
+ * pptk_rx_batch() replaces that per-packet loop; its record carries exactly
+ * the values those functions return for the same frame.
+ *
+ * Plain C types only: no HIP, torch or RCCL types appear in signatures.
+ * Every function returns 0 or a negative errno (-EINVAL, -ENOMEM, -EIO for
+ * HIP/RCCL failures).  Nothing aborts on packet content: per-packet problems
+ * are reported in pptk_rx_rec.flags.
+ */
+#ifndef PPTK_RX_H
+#define PPTK_RX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ldp_packet.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-packet record (64 bytes, one per frame, written at the frame's
+ * index).  Multi-byte integers are host (little-endian) order unless noted. */
+struct pptk_rx_rec {
+  uint64_t flow_hash;  /*  0 siphash_buf(key, tuple, 40); 0 if !PARSED      */
+  uint8_t src[16];     /*  8 network-order address; IPv4 uses bytes 0..3    */
+  uint8_t dst[16];     /* 24 idem                                           */
+  uint16_t sport;      /* 40 host order (tcp_src_port / udp_src_port)       */
+  uint16_t dport;      /* 42                                                */
+  uint16_t ip_cksum;   /* 44 ip_hdr_cksum_calc(ip, ihl); 0 == valid; 0 v6   */
+  uint16_t l4_cksum;   /* 46 tcp/udp(6)_cksum_calc(...); 0 == valid         */
+  uint16_t l4_off;     /* 48 frame offset of the L4 header                  */
+  uint16_t l4_len;     /* 50 L4 length = ip_total_len - ihl (v6: tlen - off)*/
+  uint8_t l3_off;      /* 52 14, or 18 behind an 802.1Q tag                 */
+  uint8_t proto;       /* 53 ip_proto / final IPv6 next header              */
+  uint16_t flags;      /* 54 PPTK_RX_F_*                                    */
+  uint32_t src_bucket; /* 56 ip_permitted/ipv6_permitted bucket, 0 if off   */
+  uint16_t ethertype;  /* 60 (inner) ethertype, host order                  */
+  uint8_t ip_version;  /* 62 version nibble of the L3 header (0 if none)    */
+  uint8_t reserved;    /* 63 always 0                                       */
+};
+
+#define PPTK_RX_F_PARSED 0x0001u      /* IPv4/IPv6 header parsed            */
+#define PPTK_RX_F_IP_OK 0x0002u       /* ip_cksum == 0 (always for IPv6)    */
+#define PPTK_RX_F_L4_OK 0x0004u       /* L4 present and l4_cksum == 0       */
+#define PPTK_RX_F_L4 0x0008u          /* TCP/UDP header present             */
+#define PPTK_RX_F_IPV6 0x0010u        /* L3 is IPv6                         */
+#define PPTK_RX_F_VLAN 0x0020u        /* one 802.1Q tag was skipped         */
+#define PPTK_RX_F_FRAGMENT 0x0040u    /* IPv4 MF/offset or IPv6 frag header */
+#define PPTK_RX_F_UDP_ZERO 0x0080u    /* UDP checksum field transmitted 0   */
+#define PPTK_RX_F_MALFORMED 0x0100u   /* lengths/IHL/ext chain inconsistent */
+#define PPTK_RX_F_V6_EXT 0x0200u      /* IPv6 extension headers walked      */
+
+/* ---- context ------------------------------------------------------------ */
+struct pptk_rx_ctx;
+
+struct pptk_rx_opts {
+  int device;           /* HIP device ordinal                              */
+  uint8_t key[16];      /* SipHash key (hash_seed in the reference)        */
+  uint8_t iphash_bits4; /* ip_permitted prefix bits, 1..32; 0 = no bucket  */
+  uint8_t iphash_bits6; /* ipv6_permitted prefix bits, 1..128; 0 = off     */
+  uint16_t pad0;
+  uint32_t iphash_size; /* struct ip_hash.hash_size (power of two)         */
+  uint32_t max_batch;   /* largest num passed to pptk_rx_batch             */
+  uint32_t max_frame;   /* largest frame accepted by pptk_rx_batch (<=65535)*/
+};
+
+void pptk_rx_opts_default(struct pptk_rx_opts *opts);
+
+int pptk_rx_ctx_create(struct pptk_rx_ctx **ctx, const struct pptk_rx_opts *opts);
+void pptk_rx_ctx_destroy(struct pptk_rx_ctx *ctx);
+
+/* Host in -> host out.  Gathers the borrowed ldp_packet frames into pinned
+ * staging, copies them to HBM, runs the transform and copies the records
+ * back; synchronous: on return recs[0..num) are final and no pointer in pkts
+ * is retained.  ancillary fields are neither read nor written.
+ * Frames longer than opts.max_frame get PPTK_RX_F_MALFORMED only. */
+int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
+                  int num, struct pptk_rx_rec *recs);
+
+/* Device-resident batch (asynchronous on `stream`, a hipStream_t or NULL).
+ * Frame i starts at d_frames + (d_off ? d_off[i] : i * stride) and is
+ * (d_len ? d_len[i] : fixed_len) bytes long.  d_perm (nullable) gives the
+ * processing order (a permutation of 0..n-1, e.g. from
+ * pptk_rx_bin_device); records always land at recs[i] for frame i.
+ * d_hash (nullable) additionally receives flow_hash[i] as a dense u64 array,
+ * the send buffer of the multi-GPU all-gather.
+ * The frame buffer must stay readable up to the next 16-byte boundary past
+ * the last frame (any hipMalloc allocation is). */
+struct pptk_rx_dev_batch {
+  const uint8_t *d_frames;
+  const uint64_t *d_off;  /* nullable: fixed stride                       */
+  const uint16_t *d_len;  /* nullable: fixed_len                          */
+  const uint32_t *d_perm; /* nullable: identity order                     */
+  uint64_t stride;
+  uint32_t fixed_len;
+  uint32_t max_len;       /* upper bound of frame lengths (tuning only)   */
+  uint64_t n;
+  struct pptk_rx_rec *d_recs;
+  uint64_t *d_hash;       /* nullable                                     */
+};
+
+int pptk_rx_batch_device(struct pptk_rx_ctx *ctx,
+                         const struct pptk_rx_dev_batch *b, void *stream);
+
+/* Length binning for mixed-size batches: writes into d_perm a stable
+ * permutation of 0..n-1 ordered by ceil(len/256), so the lanes of one
+ * wavefront sum frames of similar length.  d_scratch must hold
+ * pptk_rx_bin_scratch_bytes(n) bytes.  Asynchronous on `stream`. */
+size_t pptk_rx_bin_scratch_bytes(uint64_t n);
+int pptk_rx_bin_device(struct pptk_rx_ctx *ctx, const uint16_t *d_len,
+                       uint64_t n, uint32_t *d_perm, void *d_scratch,
+                       void *stream);
+
+/* Library / build identification for the loaders. */
+const char *pptk_rx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PPTK_RX_H */

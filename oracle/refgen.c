@@ -1,0 +1,347 @@
+/*
+ * refgen.c -- TEST INFRASTRUCTURE ONLY.  Applies the record composition of
+ * DESIGN.md ("Record semantics") using the REFERENCE's own functions,
+ * compiled unmodified from /root/reference by oracle/Makefile into
+ * oracle/_ref/libpptkref.so.  Used (a) in this container to generate the
+ * golden fixtures under tests/golden/ and to cross-check the C restatement
+ * (rx_oracle.c), and (b) on the GPU box as the "reference" CPU baseline.
+ *
+ * Nothing from the reference is copied here: this file only #includes the
+ * reference headers in place (-I/root/reference/...) and calls:
+ *   ether_type, ip_version, ip_hdr_len, ip_total_len, ip_proto,
+ *   ip_frag_off, ip_more_frags, ip_src, ip_dst, ip_const_payload,
+ *   ipv6_payload_len, ipv6_nexthdr, is_ipv6_nexthdr, ipv6_const_src/dst,
+ *   ipv6_const_proto_hdr_2, tcp/udp_src_port, tcp/udp_dst_port, udp_cksum
+ *                                                  (iphdr/iphdr.h)
+ *   ip_hdr_cksum_calc, tcp_cksum_calc, udp_cksum_calc, tcp6_cksum_calc,
+ *   udp6_cksum_calc, ip_cksum_feed, ip_cksum_postprocess  (iphdr/ipcksum.*)
+ *   siphash_buf, siphash64                         (misc/siphash.h)
+ *   ip_permitted, ipv6_permitted                   (iphash/iphash.c)
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hashseed.h"
+#include "ipcksum.h"
+#include "iphash.h"
+#include "iphdr.h"
+#include "siphash.h"
+
+#include "../include/pptk_rx.h"
+
+struct ref_opts {
+  uint8_t key[16];
+  uint8_t bits4;
+  uint8_t bits6;
+  uint16_t pad;
+  uint32_t hash_size;
+};
+
+/* ---- thin exported wrappers over single reference primitives ---------- */
+uint16_t ref_cksum_buf(const void *buf, size_t sz)
+{
+  struct ip_cksum_ctx ctx = IP_CKSUM_CTX_INITER;
+  ip_cksum_feed(&ctx, buf, sz);
+  return ip_cksum_postprocess(&ctx);
+}
+
+uint16_t ref_ip_hdr_cksum_calc(const void *ip, uint16_t iplen)
+{
+  return ip_hdr_cksum_calc(ip, iplen);
+}
+uint16_t ref_tcp_cksum_calc(const void *ip, uint16_t iplen, const void *l4, uint16_t l4len)
+{
+  return tcp_cksum_calc(ip, iplen, l4, l4len);
+}
+uint16_t ref_udp_cksum_calc(const void *ip, uint16_t iplen, const void *l4, uint16_t l4len)
+{
+  return udp_cksum_calc(ip, iplen, l4, l4len);
+}
+uint16_t ref_tcp6_cksum_calc(const void *ip, uint16_t iplen, const void *l4, uint16_t l4len)
+{
+  return tcp6_cksum_calc(ip, iplen, l4, l4len);
+}
+uint16_t ref_udp6_cksum_calc(const void *ip, uint16_t iplen, const void *l4, uint16_t l4len)
+{
+  return udp6_cksum_calc(ip, iplen, l4, l4len);
+}
+
+uint64_t ref_siphash_buf(const void *key, const void *buf, size_t len)
+{
+  return siphash_buf(key, buf, len);
+}
+
+uint64_t ref_siphash64(const void *key, uint64_t v)
+{
+  return siphash64(key, v);
+}
+
+/* ipv6_const_proto_hdr_2 -> offset of the returned pointer, or -1 (NULL). */
+int ref_ipv6_proto_hdr(const void *ip6, uint8_t *proto, int *frag,
+                       uint16_t *frag_hdr_off)
+{
+  uint16_t fo = 0, pfo = 0;
+  const char *p = ipv6_const_proto_hdr_2(ip6, proto, frag, &fo, &pfo);
+  if (p == NULL)
+    return -1;
+  if (frag_hdr_off)
+    *frag_hdr_off = fo;
+  return (int)(p - (const char *)ip6);
+}
+
+/* ---- ip_permitted / ipv6_permitted used as black boxes: every bucket
+ * starts with one token, the call consumes one, and the bucket whose token
+ * went to zero is the reference's hash value (iphash/iphash.c:162, :120). */
+static uint32_t bucket_probe(int v6, const void *src6, uint32_t src4,
+                             uint8_t bits, uint32_t hash_size)
+{
+  struct ip_hash h;
+  uint32_t i, found = 0xffffffffu;
+  memset(&h, 0, sizeof(h));
+  h.hash_size = hash_size;
+  h.initial_tokens = 1; /* use_tiny() */
+  h.u.entries_tiny = malloc(hash_size * sizeof(*h.u.entries_tiny));
+  for (i = 0; i < hash_size; i++)
+    h.u.entries_tiny[i].tokens = 1;
+  if (v6)
+    ipv6_permitted(src6, bits, &h);
+  else
+    ip_permitted(src4, bits, &h);
+  for (i = 0; i < hash_size; i++)
+    if (h.u.entries_tiny[i].tokens == 0)
+      found = i;
+  free(h.u.entries_tiny);
+  return found;
+}
+
+static void set_seed(const uint8_t key[16])
+{
+  memcpy(hash_seed, key, 16);
+  hash_seed_inited = 1;
+}
+
+uint32_t ref_ip_bucket(const uint8_t key[16], uint32_t src_host, uint8_t bits,
+                       uint32_t hash_size)
+{
+  set_seed(key);
+  return bucket_probe(0, NULL, src_host, bits, hash_size);
+}
+
+uint32_t ref_ipv6_bucket(const uint8_t key[16], const uint8_t src[16],
+                         uint8_t bits, uint32_t hash_size)
+{
+  set_seed(key);
+  return bucket_probe(1, src, 0, bits, hash_size);
+}
+
+/* ---- record composition with reference functions ---------------------- */
+static void to_malformed(struct pptk_rx_rec *r)
+{
+  uint16_t keep = r->flags & (PPTK_RX_F_VLAN | PPTK_RX_F_IPV6);
+  uint16_t et = r->ethertype;
+  uint8_t l3 = r->l3_off, ver = r->ip_version;
+  memset(r, 0, sizeof(*r));
+  r->flags = (uint16_t)(keep | PPTK_RX_F_MALFORMED);
+  r->ethertype = et;
+  r->l3_off = l3;
+  r->ip_version = ver;
+}
+
+void ref_rx_one(const uint8_t *f, uint32_t len, const struct ref_opts *o,
+                struct pptk_rx_rec *r, int with_bucket)
+{
+  const char *ip, *l4 = NULL;
+  uint16_t et, ihl = 0, l4len = 0;
+  uint32_t l3;
+  uint8_t proto = 0;
+  int frag = 0, v6 = 0;
+  unsigned char tuple[40];
+
+  memset(r, 0, sizeof(*r));
+  if (len > 65535u || len < 14) {
+    r->flags = PPTK_RX_F_MALFORMED;
+    return;
+  }
+  et = ether_type(f);
+  l3 = ETHER_HDR_LEN;
+  if (et == 0x8100) {
+    r->flags |= PPTK_RX_F_VLAN;
+    if (len < 18) {
+      r->flags |= PPTK_RX_F_MALFORMED;
+      return;
+    }
+    et = ether_type(f + 4);
+    l3 = ETHER_HDR_LEN + 4;
+  }
+  r->ethertype = et;
+  r->l3_off = (uint8_t)l3;
+  ip = (const char *)f + l3;
+
+  if (et == ETHER_TYPE_IP) {
+    uint16_t tl;
+    if (len < l3 + 20) {
+      to_malformed(r);
+      return;
+    }
+    r->ip_version = ip_version(ip);
+    ihl = ip_hdr_len(ip);
+    tl = ip_total_len(ip);
+    if (r->ip_version != 4 || ihl < 20 || tl < ihl || l3 + tl > len) {
+      to_malformed(r);
+      return;
+    }
+    r->flags |= PPTK_RX_F_PARSED;
+    r->ip_cksum = ip_hdr_cksum_calc(ip, ihl);
+    if (r->ip_cksum == 0)
+      r->flags |= PPTK_RX_F_IP_OK;
+    hdr_set32n(r->src, ip_src(ip));
+    hdr_set32n(r->dst, ip_dst(ip));
+    proto = ip_proto(ip);
+    frag = ip_frag_off(ip) != 0 || ip_more_frags(ip);
+    l4 = ip_const_payload(ip);
+    l4len = (uint16_t)(tl - ihl);
+  } else if (et == ETHER_TYPE_IPV6) {
+    uint32_t tlen;
+    uint16_t fo = 0, pfo = 0;
+    r->flags |= PPTK_RX_F_IPV6;
+    if (len < l3 + 40) {
+      to_malformed(r);
+      return;
+    }
+    r->ip_version = ip_version(ip);
+    tlen = (uint32_t)ipv6_payload_len(ip) + 40u;
+    if (r->ip_version != 6 || l3 + tlen > len) {
+      to_malformed(r);
+      return;
+    }
+    l4 = ipv6_const_proto_hdr_2(ip, &proto, &frag, &fo, &pfo);
+    if (l4 == NULL) {
+      to_malformed(r);
+      return;
+    }
+    v6 = 1;
+    if (is_ipv6_nexthdr(ipv6_nexthdr(ip)))
+      r->flags |= PPTK_RX_F_V6_EXT;
+    r->flags |= PPTK_RX_F_PARSED | PPTK_RX_F_IP_OK;
+    memcpy(r->src, ipv6_const_src(ip), 16);
+    memcpy(r->dst, ipv6_const_dst(ip), 16);
+    l4len = (uint16_t)(tlen - (uint32_t)(l4 - ip));
+  } else {
+    return;
+  }
+
+  if (frag)
+    r->flags |= PPTK_RX_F_FRAGMENT;
+  r->proto = proto;
+  r->l4_off = (uint16_t)(l4 - (const char *)f);
+  r->l4_len = l4len;
+  if (!frag && ((proto == 6 && l4len >= 20) || (proto == 17 && l4len >= 8))) {
+    r->flags |= PPTK_RX_F_L4;
+    if (proto == 6) {
+      r->sport = tcp_src_port(l4);
+      r->dport = tcp_dst_port(l4);
+      r->l4_cksum = v6 ? tcp6_cksum_calc(ip, 40, l4, l4len)
+                       : tcp_cksum_calc(ip, ihl, l4, l4len);
+    } else {
+      r->sport = udp_src_port(l4);
+      r->dport = udp_dst_port(l4);
+      r->l4_cksum = v6 ? udp6_cksum_calc(ip, 40, l4, l4len)
+                       : udp_cksum_calc(ip, ihl, l4, l4len);
+      if (udp_cksum(l4) == 0)
+        r->flags |= PPTK_RX_F_UDP_ZERO;
+    }
+    if (r->l4_cksum == 0)
+      r->flags |= PPTK_RX_F_L4_OK;
+  }
+
+  memcpy(tuple, r->src, 16);
+  memcpy(tuple + 16, r->dst, 16);
+  hdr_set16n(tuple + 32, r->sport);
+  hdr_set16n(tuple + 34, r->dport);
+  tuple[36] = proto;
+  tuple[37] = tuple[38] = tuple[39] = 0;
+  r->flow_hash = siphash_buf(o->key, tuple, sizeof(tuple));
+
+  if (with_bucket) {
+    if (!v6 && o->bits4)
+      r->src_bucket = ref_ip_bucket(o->key, hdr_get32n(r->src), o->bits4, o->hash_size);
+    else if (v6 && o->bits6)
+      r->src_bucket = ref_ipv6_bucket(o->key, r->src, o->bits6, o->hash_size);
+  }
+}
+
+/* ---- threaded batch: the "reference" CPU baseline of bench.py ---------- */
+struct ref_job {
+  const uint8_t *buf;
+  const uint64_t *off;
+  const uint16_t *len;
+  uint64_t stride;
+  uint32_t fixed_len;
+  size_t lo, hi;
+  const struct ref_opts *o;
+  struct pptk_rx_rec *recs;
+  int with_bucket;
+};
+
+static void *ref_worker(void *arg)
+{
+  struct ref_job *j = arg;
+  for (size_t i = j->lo; i < j->hi; i++) {
+    uint64_t off = j->off ? j->off[i] : (uint64_t)i * j->stride;
+    uint32_t len = j->len ? j->len[i] : j->fixed_len;
+    ref_rx_one(j->buf + off, len, j->o, &j->recs[i], j->with_bucket);
+  }
+  return NULL;
+}
+
+int ref_rx_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
+                 uint64_t stride, uint32_t fixed_len, size_t n,
+                 const struct ref_opts *o, struct pptk_rx_rec *recs,
+                 int nthreads, int with_bucket)
+{
+  pthread_t th[256];
+  struct ref_job jobs[256];
+  int t;
+  if (nthreads < 1)
+    nthreads = 1;
+  if (nthreads > 256)
+    nthreads = 256;
+  if (with_bucket)
+    nthreads = 1; /* the black-box bucket probe touches the global seed */
+  for (t = 0; t < nthreads; t++) {
+    jobs[t].buf = buf;
+    jobs[t].off = off;
+    jobs[t].len = len;
+    jobs[t].stride = stride;
+    jobs[t].fixed_len = fixed_len;
+    jobs[t].lo = n * (size_t)t / (size_t)nthreads;
+    jobs[t].hi = n * (size_t)(t + 1) / (size_t)nthreads;
+    jobs[t].o = o;
+    jobs[t].recs = recs;
+    jobs[t].with_bucket = with_bucket;
+  }
+  if (nthreads == 1) {
+    ref_worker(&jobs[0]);
+    return 0;
+  }
+  for (t = 0; t < nthreads; t++)
+    if (pthread_create(&th[t], NULL, ref_worker, &jobs[t]) != 0)
+      return -1;
+  for (t = 0; t < nthreads; t++)
+    pthread_join(th[t], NULL);
+  return 0;
+}
+
+/* ipcksumperf loop shape (iphdr/ipcksumperf.c:21-29). */
+uint32_t ref_cksum_loop(const uint8_t *buf, size_t sz, uint64_t iters)
+{
+  uint32_t x = 0;
+  for (uint64_t i = 0; i < iters; i++) {
+    struct ip_cksum_ctx ctx = IP_CKSUM_CTX_INITER;
+    ip_cksum_feed(&ctx, buf, sz);
+    x ^= ip_cksum_postprocess(&ctx) + (uint32_t)i;
+  }
+  return x;
+}

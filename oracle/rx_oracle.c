@@ -1,0 +1,460 @@
+/*
+ * rx_oracle.c -- TEST INFRASTRUCTURE ONLY.  CPU restatement of the PPTK
+ * per-packet receive transform, used as the parity checker for the HIP
+ * kernels and as the "port" CPU baseline in bench.py.  Nothing in pptk_amd/
+ * links, loads or calls this file; only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg do.
+ *
+ * Parity is pinned: tests/test_oracle.py checks this file against the
+ * reference's own known-answer tests (iphdr/ipcksumtest.c:23-36,58-114,
+ * iphdr/iphdrtest.c:12-54, misc/siphashtest.c:16, the SipHash-2-4 paper
+ * vectors) and against tests/golden/*.npz, whose records were produced by
+ * the reference sources compiled unmodified (oracle/_ref, see
+ * oracle/Makefile and oracle/refgen.c).
+ *
+ * Each function names the reference code it restates (path:line relative to
+ * the reference tree).  The record layout and the composition rules (which
+ * reference function is applied to which bytes) are defined in DESIGN.md
+ * section "Record semantics"; refgen.c applies the same rules with the
+ * reference's own functions.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rx_oracle.h"
+
+/* ---- byte access: misc/hdr.h:7-63.  "h" loads are host order (x86 and the
+ * AMD GPU are both little-endian), "n" loads are big-endian. */
+static uint16_t le16_at(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static uint16_t be16_at(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+static uint64_t le64_at(const uint8_t *p)
+{
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--)
+    v = (v << 8) | p[i];
+  return v;
+}
+static uint16_t swap16(uint16_t v) { return (uint16_t)((v >> 8) | (v << 8)); }
+
+/* ---- one's-complement engine ------------------------------------------ */
+
+/* ip_cksum_feed, iphdr/ipcksum.c:9-37: add each little-endian 16-bit word
+ * into a 32-bit accumulator with no intermediate folding; an odd trailing
+ * byte b is added as htons(b << 8), i.e. as b on a little-endian host
+ * (ip_cksum_add_leftover, iphdr/ipcksum.h:32-35).  The 16-byte unrolling of
+ * the reference does not change the sum. */
+uint32_t orc_sum_feed(uint32_t sum, const uint8_t *buf, size_t sz)
+{
+  size_t i;
+  for (i = 0; i + 1 < sz; i += 2)
+    sum += le16_at(buf + i);
+  if (sz & 1)
+    sum += buf[sz - 1];
+  return sum;
+}
+
+/* ip_cksum_postprocess, iphdr/ipcksum.h:17-25: end-around-carry fold, then
+ * ntohs(~sum). */
+uint16_t orc_finish(uint32_t sum)
+{
+  while (sum >> 16)
+    sum = (sum & 0xffffu) + (sum >> 16);
+  return swap16((uint16_t)~sum);
+}
+
+uint16_t orc_cksum_buf(const uint8_t *buf, size_t sz)
+{
+  return orc_finish(orc_sum_feed(0, buf, sz));
+}
+
+/* ip_hdr_cksum_calc, iphdr/ipcksum.c:39-49 (called with iplen == ihl, so the
+ * abort() branch cannot trigger). */
+uint16_t orc_ip_hdr_cksum(const uint8_t *ip)
+{
+  size_t ihl = (size_t)(ip[0] & 0x0f) * 4;
+  return orc_cksum_buf(ip, ihl);
+}
+
+/* tcp_cksum_calc / udp_cksum_calc, iphdr/ipcksum.c:51-68 and :117-134.
+ * Pseudo-header: source and destination address as their raw network bytes
+ * (htonl(ip_src()) then two host-order 16-bit loads, ipcksum.h:37-42),
+ * htons(proto), htons(l4len); then the segment itself. */
+uint16_t orc_l4_cksum_v4(const uint8_t *ip, const uint8_t *l4, uint16_t l4len,
+                         uint8_t proto)
+{
+  uint32_t s = 0;
+  s = orc_sum_feed(s, ip + 12, 4);
+  s = orc_sum_feed(s, ip + 16, 4);
+  s += swap16(proto);
+  s += swap16(l4len);
+  s = orc_sum_feed(s, l4, l4len);
+  return orc_finish(s);
+}
+
+/* tcp6_cksum_calc / udp6_cksum_calc, iphdr/ipcksum.c:74-115 and :140-181.
+ * RFC 2460 pseudo-header: 16 B source, 16 B destination (both from the
+ * fixed IPv6 header, so with a routing header the *header* destination is
+ * used -- the reference's documented bug, :70-73), the length as a 32-bit
+ * big-endian value and the next header as a 32-bit big-endian value. */
+uint16_t orc_l4_cksum_v6(const uint8_t *ip, const uint8_t *l4, uint16_t l4len,
+                         uint8_t proto)
+{
+  uint8_t be32[4];
+  uint32_t s = 0;
+  s = orc_sum_feed(s, ip + 8, 16);
+  s = orc_sum_feed(s, ip + 24, 16);
+  be32[0] = 0; be32[1] = 0; be32[2] = (uint8_t)(l4len >> 8); be32[3] = (uint8_t)l4len;
+  s = orc_sum_feed(s, be32, 4);
+  be32[2] = 0; be32[3] = proto;
+  s = orc_sum_feed(s, be32, 4);
+  s = orc_sum_feed(s, l4, l4len);
+  return orc_finish(s);
+}
+
+/* ---- IPv6 extension-header walk: ipv6_const_proto_hdr_2,
+ * iphdr/iphdr.h:804-860, with is_ipv6_nexthdr (:717-727), ipv6_extlen
+ * (:702-715) and ipv6_frag_off (:729-733).
+ *
+ * Restated literally, including two reference behaviours a "fixed" walk
+ * would not have:
+ *  - the length of the header at `off` is computed from the *next* header's
+ *    type (nexthdr is reassigned before ipv6_extlen is called, :830-831);
+ *  - offsets are uint16_t.
+ * Returns 0 and sets *l4off (offset from the IPv6 header) on success,
+ * -1 where the reference returns NULL. */
+static int is_v6_ext(uint8_t nh)
+{
+  return nh == 0 || nh == 60 || nh == 43 || nh == 44 || nh == 51;
+}
+
+static uint32_t v6_extlen(uint8_t nh, uint8_t lenfield)
+{
+  if (nh == 44)
+    return 8;
+  if (nh == 51)
+    return (uint32_t)lenfield * 4 + 8;
+  return (uint32_t)lenfield * 8 + 8;
+}
+
+int orc_v6_walk(const uint8_t *ip6, uint8_t *proto, int *fragmented,
+                uint16_t *l4off, int *walked)
+{
+  uint32_t tlen = (uint32_t)be16_at(ip6 + 4) + 40u;
+  uint16_t off = 40;
+  uint8_t nh = ip6[6];
+  int frag = 0, any = 0;
+  while (is_v6_ext(nh)) {
+    uint32_t extlen;
+    any = 1;
+    if (off + 8u > tlen)
+      return -1;
+    if (nh == 44) {
+      frag = 1;
+      if ((be16_at(ip6 + off + 2) & 0xfff8) > 0)
+        break;
+    }
+    nh = ip6[off];
+    extlen = v6_extlen(nh, ip6[off + 1]);
+    if (off + extlen > tlen)
+      return -1;
+    off = (uint16_t)(off + extlen);
+  }
+  *proto = nh;
+  *fragmented = frag;
+  *l4off = off;
+  *walked = any;
+  return 0;
+}
+
+/* ---- SipHash-2-4: misc/siphash.h:11-121 (init/feed_u64/get), :132-172
+ * (feed_remaining) and :214-229 (siphash_buf, the spec-compliant form). */
+#define ROTL64(x, b) (((x) << (b)) | ((x) >> (64 - (b))))
+
+struct orc_sip {
+  uint64_t v0, v1, v2, v3;
+};
+
+static void sip_round(struct orc_sip *s)
+{
+  s->v0 += s->v1; s->v1 = ROTL64(s->v1, 13); s->v1 ^= s->v0; s->v0 = ROTL64(s->v0, 32);
+  s->v2 += s->v3; s->v3 = ROTL64(s->v3, 16); s->v3 ^= s->v2;
+  s->v0 += s->v3; s->v3 = ROTL64(s->v3, 21); s->v3 ^= s->v0;
+  s->v2 += s->v1; s->v1 = ROTL64(s->v1, 17); s->v1 ^= s->v2; s->v2 = ROTL64(s->v2, 32);
+}
+
+static void sip_block(struct orc_sip *s, uint64_t m)
+{
+  s->v3 ^= m;
+  sip_round(s);
+  sip_round(s);
+  s->v0 ^= m;
+}
+
+uint64_t orc_siphash(const uint8_t key[16], const uint8_t *msg, size_t len)
+{
+  struct orc_sip s;
+  uint64_t k0 = le64_at(key), k1 = le64_at(key + 8), last;
+  size_t i, full = len & ~(size_t)7;
+  s.v0 = 0x736f6d6570736575ULL ^ k0;
+  s.v1 = 0x646f72616e646f6dULL ^ k1;
+  s.v2 = 0x6c7967656e657261ULL ^ k0;
+  s.v3 = 0x7465646279746573ULL ^ k1;
+  for (i = 0; i < full; i += 8)
+    sip_block(&s, le64_at(msg + i));
+  last = (uint64_t)len << 56;
+  for (i = 0; i < (len & 7); i++)
+    last |= (uint64_t)msg[full + i] << (8 * i);
+  sip_block(&s, last);
+  s.v2 ^= 0xff;
+  sip_round(&s); sip_round(&s); sip_round(&s); sip_round(&s);
+  return s.v0 ^ s.v1 ^ s.v2 ^ s.v3;
+}
+
+/* siphash64, misc/siphash.h:123-130: one 8-byte block. */
+uint64_t orc_siphash64(const uint8_t key[16], uint64_t val)
+{
+  uint8_t m[8];
+  for (int i = 0; i < 8; i++)
+    m[i] = (uint8_t)(val >> (8 * i));
+  return orc_siphash(key, m, 8);
+}
+
+/* ip_permitted hashing step, iphash/iphash.c:159-162 (bits in 1..32). */
+uint32_t orc_ip_bucket(const uint8_t key[16], uint32_t src_host, uint8_t bits,
+                       uint32_t hash_size)
+{
+  uint32_t mask = (bits >= 32) ? 0xffffffffu : ~((1u << (32 - bits)) - 1u);
+  return (uint32_t)orc_siphash64(key, src_host & mask) & (hash_size - 1u);
+}
+
+/* ipv6_permitted hashing step, iphash/iphash.c:111-120 (bits in 1..128). */
+uint32_t orc_ipv6_bucket(const uint8_t key[16], const uint8_t src[16],
+                         uint8_t bits, uint32_t hash_size)
+{
+  uint8_t net[16];
+  size_t toset = (128u - bits) / 8;
+  unsigned tomask = (128u - bits) % 8;
+  memcpy(net, src, 16);
+  memset(net + 16 - toset, 0, toset);
+  if (toset < 16)
+    net[16 - toset - 1] &= (uint8_t)~((1u << tomask) - 1u);
+  return (uint32_t)orc_siphash(key, net, 16) & (hash_size - 1u);
+}
+
+/* ---- the record: composition of the primitives above (DESIGN.md,
+ * "Record semantics").  Field extraction follows iphdr/iphdr.h accessors:
+ * ether_type :403, ether_const_payload :421, ip_version :435, ip_hdr_len
+ * :876, ip_total_len :943, ip_frag_off/ip_more_frags :1124/:1023, ip_proto
+ * :1171, ip_src/ip_dst :1259-1269, ipv6_payload_len :527, ipv6_nexthdr
+ * :533, ipv6_const_src/dst :569-579, tcp/udp ports :1303-1313/:1393-1403,
+ * udp_cksum :1429. */
+static void malformed(struct pptk_rx_rec *r)
+{
+  uint16_t keep_flags = r->flags & (PPTK_RX_F_VLAN | PPTK_RX_F_IPV6);
+  uint16_t et = r->ethertype;
+  uint8_t l3 = r->l3_off, ver = r->ip_version;
+  memset(r, 0, sizeof(*r));
+  r->flags = (uint16_t)(keep_flags | PPTK_RX_F_MALFORMED);
+  r->ethertype = et;
+  r->l3_off = l3;
+  r->ip_version = ver;
+}
+
+void orc_rx_one(const uint8_t *f, uint32_t len, const struct orc_opts *o,
+                struct pptk_rx_rec *r)
+{
+  uint32_t l3, rs = 0, re = 0;
+  uint16_t et;
+  uint8_t proto = 0;
+  int frag = 0, v6 = 0;
+  const uint8_t *ip;
+  uint8_t tuple[40];
+
+  memset(r, 0, sizeof(*r));
+  if (len > 65535u) {
+    r->flags = PPTK_RX_F_MALFORMED;
+    return;
+  }
+  if (len < 14) {
+    r->flags = PPTK_RX_F_MALFORMED;
+    return;
+  }
+  et = be16_at(f + 12);
+  l3 = 14;
+  if (et == 0x8100) {
+    r->flags |= PPTK_RX_F_VLAN;
+    if (len < 18) {
+      r->flags |= PPTK_RX_F_MALFORMED;
+      return;
+    }
+    et = be16_at(f + 16);
+    l3 = 18;
+  }
+  r->ethertype = et;
+  r->l3_off = (uint8_t)l3;
+  ip = f + l3;
+
+  if (et == 0x0800) {
+    uint32_t ihl, tl;
+    if (len < l3 + 20) {
+      malformed(r);
+      return;
+    }
+    r->ip_version = ip[0] >> 4;
+    ihl = (uint32_t)(ip[0] & 0x0f) * 4;
+    tl = be16_at(ip + 2);
+    if (r->ip_version != 4 || ihl < 20 || tl < ihl || l3 + tl > len) {
+      malformed(r);
+      return;
+    }
+    r->flags |= PPTK_RX_F_PARSED;
+    r->ip_cksum = orc_ip_hdr_cksum(ip);
+    if (r->ip_cksum == 0)
+      r->flags |= PPTK_RX_F_IP_OK;
+    memcpy(r->src, ip + 12, 4);
+    memcpy(r->dst, ip + 16, 4);
+    proto = ip[9];
+    if (be16_at(ip + 6) & 0x3fff)
+      frag = 1;
+    rs = l3 + ihl;
+    re = l3 + tl;
+  } else if (et == 0x86dd) {
+    uint32_t tlen;
+    uint16_t off;
+    int walked;
+    r->flags |= PPTK_RX_F_IPV6;
+    if (len < l3 + 40) {
+      malformed(r);
+      return;
+    }
+    r->ip_version = ip[0] >> 4;
+    tlen = (uint32_t)be16_at(ip + 4) + 40u;
+    if (r->ip_version != 6 || l3 + tlen > len) {
+      malformed(r);
+      return;
+    }
+    if (orc_v6_walk(ip, &proto, &frag, &off, &walked) != 0) {
+      malformed(r);
+      return;
+    }
+    v6 = 1;
+    if (walked)
+      r->flags |= PPTK_RX_F_V6_EXT;
+    r->flags |= PPTK_RX_F_PARSED | PPTK_RX_F_IP_OK; /* ip46_hdr_cksum_calc: 0 */
+    memcpy(r->src, ip + 8, 16);
+    memcpy(r->dst, ip + 24, 16);
+    rs = l3 + off;
+    re = l3 + tlen;
+  } else {
+    return; /* not IP: nothing parsed, nothing hashed */
+  }
+
+  if (frag)
+    r->flags |= PPTK_RX_F_FRAGMENT;
+  r->proto = proto;
+  r->l4_off = (uint16_t)rs;
+  r->l4_len = (uint16_t)(re - rs);
+  if (!frag && ((proto == 6 && re - rs >= 20) || (proto == 17 && re - rs >= 8))) {
+    const uint8_t *l4 = f + rs;
+    uint16_t l4len = (uint16_t)(re - rs);
+    r->flags |= PPTK_RX_F_L4;
+    r->sport = be16_at(l4);
+    r->dport = be16_at(l4 + 2);
+    r->l4_cksum = v6 ? orc_l4_cksum_v6(ip, l4, l4len, proto)
+                     : orc_l4_cksum_v4(ip, l4, l4len, proto);
+    if (r->l4_cksum == 0)
+      r->flags |= PPTK_RX_F_L4_OK;
+    if (proto == 17 && le16_at(l4 + 6) == 0)
+      r->flags |= PPTK_RX_F_UDP_ZERO;
+  }
+
+  /* 5-tuple flow hash: siphash_buf (misc/siphash.h:214-229) over
+   * src[16] | dst[16] | be16 sport | be16 dport | proto | 0 0 0. */
+  memcpy(tuple, r->src, 16);
+  memcpy(tuple + 16, r->dst, 16);
+  tuple[32] = (uint8_t)(r->sport >> 8);
+  tuple[33] = (uint8_t)r->sport;
+  tuple[34] = (uint8_t)(r->dport >> 8);
+  tuple[35] = (uint8_t)r->dport;
+  tuple[36] = proto;
+  tuple[37] = tuple[38] = tuple[39] = 0;
+  r->flow_hash = orc_siphash(o->key, tuple, 40);
+
+  if (!v6 && o->bits4) {
+    uint32_t src_host = ((uint32_t)r->src[0] << 24) | ((uint32_t)r->src[1] << 16) |
+                        ((uint32_t)r->src[2] << 8) | r->src[3];
+    r->src_bucket = orc_ip_bucket(o->key, src_host, o->bits4, o->hash_size);
+  } else if (v6 && o->bits6) {
+    r->src_bucket = orc_ipv6_bucket(o->key, r->src, o->bits6, o->hash_size);
+  }
+}
+
+/* ---- batch driver (pthreads, one contiguous shard per thread) ---------- */
+struct orc_job {
+  const uint8_t *buf;
+  const uint64_t *off;
+  const uint16_t *len;
+  uint64_t stride;
+  uint32_t fixed_len;
+  size_t lo, hi;
+  const struct orc_opts *o;
+  struct pptk_rx_rec *recs;
+};
+
+static void *orc_worker(void *arg)
+{
+  struct orc_job *j = arg;
+  for (size_t i = j->lo; i < j->hi; i++) {
+    uint64_t off = j->off ? j->off[i] : (uint64_t)i * j->stride;
+    uint32_t len = j->len ? j->len[i] : j->fixed_len;
+    orc_rx_one(j->buf + off, len, j->o, &j->recs[i]);
+  }
+  return NULL;
+}
+
+int orc_rx_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
+                 uint64_t stride, uint32_t fixed_len, size_t n,
+                 const struct orc_opts *o, struct pptk_rx_rec *recs,
+                 int nthreads)
+{
+  pthread_t th[256];
+  struct orc_job jobs[256];
+  int t;
+  if (nthreads < 1)
+    nthreads = 1;
+  if (nthreads > 256)
+    nthreads = 256;
+  for (t = 0; t < nthreads; t++) {
+    jobs[t].buf = buf;
+    jobs[t].off = off;
+    jobs[t].len = len;
+    jobs[t].stride = stride;
+    jobs[t].fixed_len = fixed_len;
+    jobs[t].lo = n * (size_t)t / (size_t)nthreads;
+    jobs[t].hi = n * (size_t)(t + 1) / (size_t)nthreads;
+    jobs[t].o = o;
+    jobs[t].recs = recs;
+  }
+  if (nthreads == 1) {
+    orc_worker(&jobs[0]);
+    return 0;
+  }
+  for (t = 0; t < nthreads; t++)
+    if (pthread_create(&th[t], NULL, orc_worker, &jobs[t]) != 0)
+      return -1;
+  for (t = 0; t < nthreads; t++)
+    pthread_join(th[t], NULL);
+  return 0;
+}
+
+/* ipcksumperf semantics (iphdr/ipcksumperf.c:21-29): `iters` checksums of
+ * one buffer; returns the xor of results so the loop cannot be elided. */
+uint32_t orc_cksum_loop(const uint8_t *buf, size_t sz, uint64_t iters)
+{
+  uint32_t x = 0;
+  for (uint64_t i = 0; i < iters; i++)
+    x ^= orc_cksum_buf(buf, sz) + (uint32_t)i;
+  return x;
+}

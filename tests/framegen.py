@@ -1,0 +1,370 @@
+"""Deterministic synthetic Ethernet frames for the rx-transform tests.
+
+Recipes follow SURVEY.md section 8(d) (C64 / C1500 / CMIX) and the
+reference's frame recipe ldp/ldpsend.c:141-168 (Eth + IPv4 DF TTL 64 +
+UDP, checksums filled).  Checksums are filled by a small independent
+Python one's-complement sum, not by the oracle.
+
+Every generator returns ``(buf, off, lens)``: frames packed back to back in
+one uint8 buffer (so frame starts are generally NOT aligned), u64 offsets
+and u16 lengths.
+"""
+import struct
+
+import numpy as np
+
+ETH_IP, ETH_IP6, ETH_VLAN = 0x0800, 0x86DD, 0x8100
+
+
+# ---------------------------------------------------------------- checksums
+def ones_sum(data, start=0):
+    """Sum of big-endian 16-bit words (RFC 1071), odd tail padded."""
+    b = bytes(data)
+    if len(b) & 1:
+        b += b"\0"
+    a = np.frombuffer(b, dtype=">u2").astype(np.uint64)
+    s = int(a.sum()) + start
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def csum(data, start=0):
+    return (~ones_sum(data, start)) & 0xFFFF
+
+
+def eth(etype, vlan=None, dst=b"\x02\0\0\0\0\x01", src=b"\x02\0\0\0\0\x02"):
+    h = dst + src
+    if vlan is not None:
+        h += struct.pack(">HH", ETH_VLAN, vlan & 0x0FFF)
+    return h + struct.pack(">H", etype)
+
+
+def ipv4_hdr(src, dst, proto, payload_len, opts=b"", df=True, mf=False,
+             frag_off=0, ttl=64, ident=0, fix=True):
+    assert len(opts) % 4 == 0
+    ihl = 5 + len(opts) // 4
+    flags = (0x4000 if df else 0) | (0x2000 if mf else 0) | (frag_off & 0x1FFF)
+    h = bytearray(struct.pack(">BBHHHBBH4s4s", 0x40 | ihl, 0, ihl * 4 + payload_len,
+                              ident, flags, ttl, proto, 0, src, dst) + opts)
+    if fix:
+        struct.pack_into(">H", h, 10, csum(h))
+    return bytes(h)
+
+
+def ipv6_hdr(src, dst, nexthdr, payload_len, hlim=64):
+    return struct.pack(">IHBB16s16s", 0x60000000, payload_len, nexthdr, hlim, src, dst)
+
+
+def tcp_hdr(sport, dport, seq=0, ack=0, flags=0x18, win=8192, opts=b""):
+    doff = 5 + len(opts) // 4
+    return struct.pack(">HHIIBBHHH", sport, dport, seq, ack, doff << 4, flags,
+                       win, 0, 0) + opts
+
+
+def udp_hdr(sport, dport, length):
+    return struct.pack(">HHHH", sport, dport, length, 0)
+
+
+def pseudo4(src, dst, proto, l4len):
+    return src + dst + struct.pack(">BBH", 0, proto, l4len)
+
+
+def pseudo6(src, dst, proto, l4len):
+    return src + dst + struct.pack(">II", l4len, proto)
+
+
+def fill_l4(seg, proto, pseudo, udp_zero=False):
+    seg = bytearray(seg)
+    off = 16 if proto == 6 else 6
+    seg[off:off + 2] = b"\0\0"
+    if proto == 17 and udp_zero:
+        return bytes(seg)
+    c = csum(bytes(pseudo) + bytes(seg))
+    if proto == 17 and c == 0:
+        c = 0xFFFF
+    struct.pack_into(">H", seg, off, c)
+    return bytes(seg)
+
+
+# ------------------------------------------------------------ frame builders
+def frame_v4(rng, proto, total, vlan=None, ihl_words=5, corrupt=None,
+             src=None, dst=None, udp_zero=False, mf=False, frag_off=0):
+    """IPv4 frame of exactly `total` bytes (>= minimum)."""
+    l2 = eth(ETH_IP, vlan)
+    opts = bytes(rng.integers(0, 256, (ihl_words - 5) * 4, dtype=np.uint8))
+    l4min = 20 if proto == 6 else 8
+    l4len = total - len(l2) - 20 - len(opts)
+    assert l4len >= l4min, (total, l4len)
+    src = src if src is not None else bytes([10]) + bytes(rng.integers(0, 256, 3, dtype=np.uint8))
+    dst = dst if dst is not None else bytes([192, 168]) + bytes(rng.integers(0, 256, 2, dtype=np.uint8))
+    sp, dp = (int(x) for x in rng.integers(0, 65536, 2))
+    payload = bytes(rng.integers(0, 256, l4len - l4min, dtype=np.uint8))
+    if proto == 6:
+        seg = tcp_hdr(sp, dp, int(rng.integers(0, 2**32)), 0) + payload
+    else:
+        seg = udp_hdr(sp, dp, l4len) + payload
+    seg = fill_l4(seg, proto, pseudo4(src, dst, proto, l4len), udp_zero)
+    ip = ipv4_hdr(src, dst, proto, l4len, opts, mf=mf, frag_off=frag_off,
+                  ident=int(rng.integers(0, 65536)))
+    f = bytearray(l2 + ip + seg)
+    corrupt_frame(f, rng, corrupt, len(l2), len(ip))
+    return bytes(f)
+
+
+def frame_v6(rng, proto, total, vlan=None, ext=None, corrupt=None):
+    """IPv6 frame; ext = list of (type, bytes) extension headers."""
+    l2 = eth(ETH_IP6, vlan)
+    ext = ext or []
+    exth = b""
+    types = [t for t, _ in ext] + [proto]
+    for i, (t, body) in enumerate(ext):
+        exth += bytes([types[i + 1]]) + body[1:]
+    l4min = 20 if proto == 6 else 8
+    l4len = total - len(l2) - 40 - len(exth)
+    assert l4len >= l4min
+    src = bytes([0x20, 0x01, 0x0d, 0xb8]) + bytes(rng.integers(0, 256, 12, dtype=np.uint8))
+    dst = bytes([0xfd]) + bytes(rng.integers(0, 256, 15, dtype=np.uint8))
+    sp, dp = (int(x) for x in rng.integers(0, 65536, 2))
+    payload = bytes(rng.integers(0, 256, l4len - l4min, dtype=np.uint8))
+    seg = (tcp_hdr(sp, dp) if proto == 6 else udp_hdr(sp, dp, l4len)) + payload
+    seg = fill_l4(seg, proto, pseudo6(src, dst, proto, l4len))
+    ip = ipv6_hdr(src, dst, types[0], len(exth) + l4len)
+    f = bytearray(l2 + ip + exth + seg)
+    corrupt_frame(f, rng, corrupt, len(l2), 40 + len(exth))
+    return bytes(f)
+
+
+def hbh(n8=1):
+    """Hop-by-hop / destination-options header of n8*8 bytes (PadN)."""
+    body = bytearray(8 * n8)
+    body[1] = n8 - 1
+    body[2] = 1          # PadN
+    body[3] = 8 * n8 - 4
+    return bytes(body)
+
+
+def corrupt_frame(f, rng, how, l3, l3len):
+    if how is None:
+        return
+    if how == "ip":        # flip a bit of the IPv4 identification field
+        f[l3 + 4] ^= 0x01
+    elif how == "l4":      # flip a payload/L4 byte
+        pos = int(rng.integers(l3 + l3len, len(f)))
+        f[pos] ^= 0xFF if f[pos] != 0xFF else 0x01
+
+
+def pack(frames, align=1):
+    """Pack frames back to back (each start rounded up to `align`)."""
+    offs, lens, pos = [], [], 0
+    for fr in frames:
+        pos = (pos + align - 1) // align * align
+        offs.append(pos)
+        lens.append(len(fr))
+        pos += len(fr)
+    buf = np.zeros(pos + 64, dtype=np.uint8)
+    for o, fr in zip(offs, frames):
+        buf[o:o + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
+    return buf, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint16)
+
+
+def _corrupt_choice(rng, rate=0.01):
+    u = rng.random()
+    return "ip" if u < rate / 2 else ("l4" if u < rate else None)
+
+
+# ----------------------------------------------------------------- configs
+def gen_c64(n, seed=0x5EED + 1):
+    rng = np.random.default_rng(seed)
+    return pack([frame_v4(rng, 17, 64, corrupt=_corrupt_choice(rng)) for _ in range(n)])
+
+
+def gen_c1500(n, seed=0x5EED + 2):
+    rng = np.random.default_rng(seed)
+    return pack([frame_v4(rng, 6, 1500, corrupt=_corrupt_choice(rng)) for _ in range(n)])
+
+
+def gen_cmix(n, seed=0x5EED + 3):
+    """64..1500 B, 70 % IPv4 / 30 % IPv6, 50/50 TCP/UDP, 25 % VLAN, 5 % IPv4
+    with IHL > 5, 2 % IPv6 with one hop-by-hop header."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for _ in range(n):
+        proto = 6 if rng.random() < 0.5 else 17
+        vlan = int(rng.integers(1, 4095)) if rng.random() < 0.25 else None
+        size = int(rng.integers(64, 1501))
+        corrupt = _corrupt_choice(rng)
+        if rng.random() < 0.7:
+            ihl = int(rng.integers(6, 16)) if rng.random() < 0.05 else 5
+            minsz = 14 + (4 if vlan is not None else 0) + ihl * 4 + (20 if proto == 6 else 8)
+            frames.append(frame_v4(rng, proto, max(size, minsz), vlan, ihl, corrupt))
+        else:
+            ext = [(0, hbh(1))] if rng.random() < 0.02 else None
+            minsz = 14 + (4 if vlan is not None else 0) + 40 + (8 if ext else 0) + (20 if proto == 6 else 8)
+            frames.append(frame_v6(rng, proto, max(size, minsz), vlan, ext,
+                                   "l4" if corrupt else None))
+    return pack(frames)
+
+
+# ------------------------------------------------------- reference KAT frames
+# Raw IP packets of iphdr/ipcksumtest.c:14-18 and iphdr/iphdrtest.c:5-8
+# (fixture data, each must verify to 0 / walk as the reference tests assert).
+KAT_IP = {
+    "iptcp6hdr": bytes.fromhex(
+        "6000000000170640" + "00" * 15 + "01" + "00" * 15 + "01"
+        + "00140050000000000000000050022000ba0a0000666f6f"),
+    "ipudp6hdr": bytes.fromhex(
+        "60000000000b1140" + "00" * 15 + "01" + "00" * 15 + "01"
+        + "00350035000b29fd666f6f"),
+    "iphdr": bytes.fromhex("450000140001000040007ce77f0000017f000001"),
+    "iptcphdr": bytes.fromhex(
+        "4500002b0001000040067cca7f0000017f000001"
+        "00140050000000000000000050022000bc090000666f6f"),
+    "ipudphdr": bytes.fromhex(
+        "4500001f0001000040117ccb7f0000017f000001"
+        "00350035000b2bfc666f6f"),
+    "tcp6frag": bytes.fromhex(
+        "60000000001f2c40" + "00" * 15 + "01" + "00" * 15 + "01"
+        + "0600000000000000" + "00140050000000000000000050022000ba0a0000666f6f"),
+    "tcp6hop": bytes.fromhex(
+        "60000000001f0040" + "00" * 15 + "01" + "00" * 15 + "01"
+        + "0600010400000000" + "00140050000000000000000050022000ba0a0000666f6f"),
+    "tcp6subsequentfrag": bytes.fromhex(
+        "60000000001f2c40" + "00" * 15 + "01" + "00" * 15 + "01"
+        + "0600000800000000" + "00140050000000000000000050022000ba0a0000666f6f"),
+}
+
+
+def kat_frames():
+    out = []
+    for name, ip in KAT_IP.items():
+        et = ETH_IP6 if ip[0] >> 4 == 6 else ETH_IP
+        out.append(eth(et) + ip)
+        out.append(eth(et, vlan=7) + ip)
+    return out
+
+
+# ------------------------------------------------------------- edge frames
+def edge_frames(seed=0xED6E):
+    rng = np.random.default_rng(seed)
+    F = []
+    base4 = frame_v4(rng, 6, 100)
+    base6 = frame_v6(rng, 17, 120)
+    F += kat_frames()
+    # runts and truncations of valid frames at every length up to 80
+    for cut in list(range(0, 80)) + [99]:
+        F.append(base4[:cut])
+    for cut in (0, 13, 14, 17, 18, 40, 53, 54, 55, 61, 62, 119):
+        F.append(base6[:cut])
+        F.append(eth(ETH_IP6, 5)[:min(cut, 18)] + base6[14:cut])
+    F.append(eth(ETH_VLAN)[:14] + b"\x00")                       # VLAN runt
+    F.append(b"\x02" * 12 + b"\x81\x00\x00\x05")                 # VLAN, len 16
+    # IHL / total-length / version corner cases
+    for ihl_nib in range(0, 16):
+        f = bytearray(frame_v4(rng, 17, 90))
+        f[14] = 0x40 | ihl_nib
+        F.append(bytes(f))
+    for tl in (0, 19, 20, 27, 28, 29, 39, 40, 41, 75, 76, 77, 1000):
+        f = bytearray(frame_v4(rng, 17, 90))
+        struct.pack_into(">H", f, 16, tl)
+        F.append(bytes(f))
+    for ver in (0, 5, 6, 15):
+        f = bytearray(frame_v4(rng, 6, 90))
+        f[14] = (ver << 4) | 5
+        F.append(bytes(f))
+        g = bytearray(frame_v6(rng, 6, 100))
+        g[14] = (ver << 4) | (g[14] & 0xF)
+        F.append(bytes(g))
+    # Ethernet padding beyond ip_total_len (excluded from the L4 sum)
+    for pad in (1, 2, 3, 6, 17):
+        F.append(frame_v4(rng, 17, 60) + bytes(rng.integers(0, 256, pad, dtype=np.uint8)))
+    # odd and tiny L4 lengths
+    for total in range(42, 80):
+        F.append(frame_v4(rng, 17, total))
+    for total in range(54, 90):
+        F.append(frame_v4(rng, 6, total))
+    for total in range(62, 100):
+        F.append(frame_v6(rng, 17, total))
+        F.append(frame_v6(rng, 6, total + 12))
+    # runt L4 (UDP < 8, TCP < 20) via total length
+    for proto, l4 in ((17, 0), (17, 4), (17, 7), (6, 0), (6, 8), (6, 19)):
+        ip = ipv4_hdr(b"\x0a\0\0\x01", b"\x0a\0\0\x02", proto, l4)
+        F.append(eth(ETH_IP) + ip + bytes(rng.integers(0, 256, l4, dtype=np.uint8)))
+    # UDP transmitted checksum zero (v4) and one that sums to 0xffff
+    F.append(frame_v4(rng, 17, 80, udp_zero=True))
+    F.append(frame_v4(rng, 17, 64, udp_zero=True, vlan=100))
+    # fragments: MF, offset, both, DF only
+    F.append(frame_v4(rng, 6, 200, mf=True))
+    F.append(frame_v4(rng, 17, 200, frag_off=185))
+    F.append(frame_v4(rng, 17, 200, mf=True, frag_off=3))
+    # IHL up to 15 with options
+    for ihl in range(5, 16):
+        F.append(frame_v4(rng, 6, 200, ihl_words=ihl))
+        F.append(frame_v4(rng, 17, 120, vlan=9, ihl_words=ihl))
+    # IPv6 extension chains
+    for chain in ([(0, hbh(1))], [(0, hbh(2))], [(60, hbh(1))], [(43, hbh(1))],
+                  [(0, hbh(1)), (60, hbh(3))], [(60, hbh(1)), (43, hbh(2)), (60, hbh(1))],
+                  [(51, bytes([0, 1]) + bytes(6))], [(51, bytes([0, 4]) + bytes(22))],
+                  [(44, bytes(8))], [(0, hbh(1)), (44, bytes(8))],
+                  [(0, hbh(3)), (44, bytes(8))],           # extlen-from-next-header quirk
+                  [(44, bytes([0, 0, 0, 8]) + bytes(4))],   # subsequent fragment
+                  [(44, bytes([0, 0, 0, 1]) + bytes(4))],   # first fragment, M=1
+                  [(60, hbh(1))] * 6,
+                  [(60, hbh(1))] * 20):
+        for proto in (6, 17):
+            try:
+                F.append(frame_v6(rng, proto, 64 + 8 * sum(len(b) // 8 for _, b in chain) + 80, ext=chain))
+            except AssertionError:
+                pass
+    # IPv6 chain overrunning the payload length -> NULL in the reference
+    g = bytearray(frame_v6(rng, 6, 120, ext=[(0, hbh(1))]))
+    g[14 + 40 + 1] = 30
+    F.append(bytes(g))
+    g = bytearray(frame_v6(rng, 6, 120, ext=[(60, hbh(1))]))
+    struct.pack_into(">H", g, 18, 7)                             # plen 7 < 8
+    F.append(bytes(g[:14 + 47]))
+    # non-IP ethertypes, QinQ
+    F.append(eth(0x0806) + bytes(28))
+    F.append(eth(0x88A8) + bytes(46))
+    F.append(eth(0x0800, vlan=1)[:12] + b"\x81\x00\x00\x01\x86\xdd" + bytes(60))
+    # jumbo frames
+    F.append(frame_v4(rng, 6, 9014))
+    F.append(frame_v4(rng, 17, 9018, vlan=3))
+    F.append(frame_v6(rng, 6, 9000))
+    F.append(frame_v6(rng, 17, 65535))
+    F.append(frame_v4(rng, 6, 65535))
+    return F
+
+
+def gen_edge(seed=0xED6E):
+    return pack(edge_frames(seed))
+
+
+def gen_fuzz(n, seed=0xF022):
+    """Valid frames of every kind with random header mutations/truncations."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for i in range(n):
+        kind = int(rng.integers(0, 4))
+        if kind == 0:
+            ihl = int(rng.integers(5, 16)) if rng.random() < 0.3 else 5
+            f = frame_v4(rng, 6 if rng.random() < 0.5 else 17,
+                         max(int(rng.integers(64, 400)), 18 + 4 * ihl + 20),
+                         vlan=5 if rng.random() < 0.3 else None, ihl_words=ihl)
+        elif kind == 1:
+            ext = [(int(rng.choice([0, 43, 44, 51, 60])), hbh(1))] if rng.random() < 0.5 else None
+            f = frame_v6(rng, 6 if rng.random() < 0.5 else 17, int(rng.integers(100, 400)),
+                         vlan=5 if rng.random() < 0.3 else None, ext=ext)
+        elif kind == 2:
+            f = frame_v4(rng, 17, int(rng.integers(42, 200)))
+        else:
+            f = frame_v6(rng, 17, int(rng.integers(80, 200)),
+                         ext=[(int(rng.choice([0, 44, 60])), hbh(int(rng.integers(1, 3))))])
+        f = bytearray(f)
+        for _ in range(int(rng.integers(1, 4))):
+            pos = int(rng.integers(0, min(len(f), 96)))
+            f[pos] = int(rng.integers(0, 256))
+        if rng.random() < 0.2:
+            f = f[:int(rng.integers(0, len(f) + 1))]
+        frames.append(bytes(f))
+    return pack(frames)
