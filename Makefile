@@ -1,0 +1,48 @@
+# Build of libpptkrx.so (product) and the oracle (test infrastructure).
+#   make            -> pptk_amd/libpptkrx.so + oracle/liboracle.so (+ oracle/_ref)
+# gfx950 only; hipcc cross-compiles without a GPU.
+HIPCC ?= /opt/rocm/bin/hipcc
+CC ?= gcc
+ARCH ?= gfx950
+OBJDIR := build/obj
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
+CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wextra -Iinclude
+
+LIB := pptk_amd/libpptkrx.so
+HIP_SRCS := pptk_amd/csrc/rx_kernel.hip pptk_amd/csrc/rx_bin.hip pptk_amd/csrc/rx_capi.hip
+C_SRCS := pptk_amd/csrc/host/ipcksum.c pptk_amd/csrc/host/hashseed.c
+HDRS := $(wildcard include/*.h) pptk_amd/csrc/rx_internal.h
+HIP_OBJS := $(patsubst pptk_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
+C_OBJS := $(patsubst pptk_amd/csrc/host/%.c,$(OBJDIR)/host/%.o,$(C_SRCS))
+
+all: $(LIB) oracle
+
+$(OBJDIR)/%.o: pptk_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/host/%.o: pptk_amd/csrc/host/%.c $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS) $(C_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: $(HIP_SRCS)
+	@mkdir -p build/asm
+	cd build/asm && $(HIPCC) $(HIPFLAGS) -I../../include -c ../../pptk_amd/csrc/rx_kernel.hip -save-temps -o rx_kernel.o -Rpass-analysis=kernel-resource-usage 2> resource.txt; true
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean asm
+
+# bench/test tooling: synthetic frames generated in HBM
+tools/libpptksynth.so: tools/synth.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
+
+all: tools/libpptksynth.so

@@ -1,0 +1,319 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident throughput of the MI355X rx transform.
+
+One "step" = one launch of the rx transform (checksum verify + header
+parse + SipHash flow hash, pptk_rx_batch_device) over one batch of
+synthetic frames already resident in HBM.  Primary workload: C1500
+(16 M x 1500 B IPv4/TCP per GPU, BASELINE.json configs[2], on which the
+70 %-of-HBM target is stated); C64 (configs[1]) and CMIX (configs[3]) are
+reported in "secondary".  With N > 1 GPUs every rank processes its own
+16 M-frame shard (weak scaling) and the per-frame flow hashes of each batch
+are all-gathered over RCCL, overlapped with the next batch's kernel.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement".
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpkts/s device-resident (cksum+parse+SipHash), 64B & 1500B; % HBM roofline"
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KEY = bytes(range(1, 17))
+N_PER_GPU = 16 * 1024 * 1024
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(ngpus):
+    import torch
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if ws > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    return ws, rank, dev
+
+
+def barrier(ws, dev):
+    import torch
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, ws, dev):
+    if ws == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, ws, dev):
+    if ws == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check):
+    """Generate shard `rank` of config `cfg`, time `steps` launches."""
+    import torch
+    from pptk_amd.shard import allgather_flow_hash
+    from tools.synth import make_batch
+    b = make_batch(cfg, n, dev, first=rank * n)
+    torch.cuda.synchronize(dev)
+    recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
+    perm = None
+    kw = {}
+    if "off" in b:
+        kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
+        perm = ctx.bin_device(b["lens"], n)        # length binning (part of setup)
+    else:
+        kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
+    gout = None
+    if gather and ws > 1:
+        gout = torch.empty(n * ws, dtype=torch.int64, device=dev)
+
+    work = [None]
+
+    def step(k):
+        h = hbuf[k & 1]
+        ctx.batch_device(b["frames"], n, perm=perm, recs=recs, hash_out=h, **kw)
+        if gout is not None:
+            if work[0] is not None:
+                work[0].wait()                  # previous gather done before reuse
+            _, work[0] = allgather_flow_hash(h, gout, async_op=True)
+
+    for k in range(warmup):
+        step(k)
+    if work[0] is not None:
+        work[0].wait()
+        work[0] = None
+    barrier(ws, dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record()
+        step(k)
+        ev[k][1].record()
+    if work[0] is not None:
+        work[0].wait()
+    barrier(ws, dev)
+    wall = time.perf_counter() - t0
+    wall = max_over_ranks(wall, ws, dev)
+    # kernel-only duration: the rx launch is the only work between the
+    # events when there is no gather; with a gather the event pair brackets
+    # the launch plus the (async) collective enqueue
+    kms = [a.elapsed_time(z) for a, z in ev]
+    kernel_ms = float(np.median(kms))
+    res = {
+        "n": n, "bytes": b["bytes"], "wall_s": wall,
+        "ms_per_step": wall / steps * 1e3, "kernel_ms": kernel_ms,
+        "mpkts": n * ws * steps / wall / 1e6,
+    }
+    # size-independent parity on the full batch: every frame parsed, and the
+    # checksum verdicts equal what the generator planted
+    if check:
+        from pptk_amd.records import F_IP_OK, F_L4_OK, F_PARSED
+        r = recs.view(torch.int16)[:, 27].to(torch.int32) & 0xFFFF   # flags @54
+        exp = b["expect"].to(torch.int32)
+        ok_parsed = bool(((r & F_PARSED) != 0).all().item())
+        ip_ok = ((r & F_IP_OK) != 0).to(torch.int32)
+        l4_ok = ((r & F_L4_OK) != 0).to(torch.int32)
+        ok_ip = bool((ip_ok == (exp & 1)).all().item())
+        ok_l4 = bool((l4_ok == ((exp >> 1) & 1)).all().item())
+        res["full_batch_check"] = {"parsed": ok_parsed, "ip_verdicts": ok_ip,
+                                   "l4_verdicts": ok_l4,
+                                   "corrupted": int((exp != 3).sum().item())}
+        res["oracle_sample"] = oracle_sample(b, recs, n, dev)
+    res["_batch"] = b
+    res["_recs"] = recs
+    return res
+
+
+def oracle_sample(b, recs, n, dev, k=4096):
+    """Bit-exact check of k random frames against the CPU oracle."""
+    import torch
+    from oracle.oracle import Oracle, make_opts
+    from pptk_amd.records import diff_records
+    rng = np.random.default_rng(1234)
+    idx = np.sort(rng.choice(n, size=min(k, n), replace=False))
+    if "off" in b:
+        off = b["off"].cpu().numpy()[idx].astype(np.uint64)
+        lens = (b["lens"].cpu().numpy().view(np.uint16))[idx]
+    else:
+        off = idx.astype(np.uint64) * b["stride"]
+        lens = np.full(len(idx), b["fixed_len"], dtype=np.uint16)
+    frames = b["frames"]
+    chunks, offs, pos = [], [], 0
+    for o, l in zip(off, lens):
+        chunks.append(frames[int(o):int(o) + int(l)].cpu().numpy())
+        offs.append(pos)
+        pos += int(l)
+    buf = np.concatenate(chunks + [np.zeros(64, np.uint8)])
+    want = Oracle().rx_batch(buf, np.array(offs, np.uint64), lens,
+                             opts=make_opts(KEY), nthreads=8)
+    got = recs[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    d = diff_records(got, want)
+    return {"frames": int(len(idx)), "mismatches": 0 if not d else int(d.split()[0])}
+
+
+def cpu_baseline(b, seconds=10.0, sample=262144):
+    """PPTK's CPU path on this host's cores over a sample of the same C1500
+    batch: the reference's own functions when oracle/_ref was built, else
+    the C restatement."""
+    from oracle.oracle import REF_SO, Oracle, Reference, make_opts
+    n = min(sample, b["n"])
+    host = b["frames"][: n * b["stride"]].cpu().numpy()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    kind = "reference" if os.path.exists(REF_SO) else "port"
+    lib = Reference() if kind == "reference" else Oracle()
+    opts = make_opts(KEY)
+    kw = {"with_bucket": False} if kind == "reference" else {}
+
+    def timed(nth):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            lib.rx_batch(host, None, None, stride=b["stride"], fixed_len=b["fixed_len"],
+                         n=n, opts=opts, nthreads=nth, **kw)
+            done += n
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return done / el / 1e6, el
+
+    mt, el_mt = timed(threads)
+    st, el_st = timed(1) if seconds >= 1 else (None, 0)
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(mt, 3), "unit": "Mpkts/s", "cores": threads, "kind": kind,
+            "sample": f"{n} distinct C1500 frames (1500 B IPv4/TCP) from the same batch, "
+                      f"full path (IPv4 hdr cksum + TCP cksum + parse + 40 B SipHash), "
+                      f"repeated for {el_mt:.1f} s on {threads} threads",
+            "single_thread_mpkts": None if st is None else round(st, 3),
+            "cpu_model": cpu}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=N_PER_GPU, help="frames per GPU")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--only", default=None, help="run just this config (profiling)")
+    args = ap.parse_args()
+
+    import torch
+    from pptk_amd.rx import RxContext
+    ws, rank, dev = dist_setup(args.gpus)
+    ctx = RxContext(dev.index, KEY)
+    n = args.frames
+    check = not args.no_check
+
+    primary_cfg = args.only or "c1500"
+    prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, True, check)
+    log(f"[rank {rank}] {primary_cfg}: {prim['mpkts']:.1f} Mpkts/s, kernel {prim['kernel_ms']:.3f} ms")
+    nog = None
+    if ws > 1:
+        nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False)
+
+    bytes_per_launch = prim["bytes"]
+    achieved = bytes_per_launch / (prim["kernel_ms"] * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "kernel_ms": round(prim["kernel_ms"], 4)}
+
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu and primary_cfg == "c1500":
+        cpu = cpu_baseline(prim["_batch"], seconds=args.cpu_seconds)
+        log(f"cpu baseline: {cpu}")
+    full_check = prim.get("full_batch_check")
+    sample_check = prim.get("oracle_sample")
+    del prim["_batch"], prim["_recs"]
+    torch.cuda.empty_cache()
+
+    secondary = {}
+    if not args.no_secondary and args.only is None:
+        for cfg in ("c64", "cmix"):
+            r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check)
+            ach = r["bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
+            secondary[cfg] = {"value": round(r["mpkts"], 1), "unit": "Mpkts/s",
+                              "kernel_ms": round(r["kernel_ms"], 4),
+                              "frames_per_gpu": n, "frame_bytes": r["bytes"],
+                              "roofline": {"bound": "hbm", "achieved": round(ach, 1),
+                                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                           "frac": round(ach / HBM_PEAK_GBS, 4)},
+                              "full_batch_check": r.get("full_batch_check"),
+                              "oracle_sample": r.get("oracle_sample")}
+            del r["_batch"], r["_recs"]
+            torch.cuda.empty_cache()
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(prim["mpkts"], 1),
+            "unit": "Mpkts/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(prim["ms_per_step"], 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"{primary_cfg.upper()}: {n} frames per GPU"
+                                   + (" x 1500 B IPv4/TCP" if primary_cfg == "c1500" else ""),
+                       "frames_per_gpu": n, "global_frames": n * ws,
+                       "parallelism": f"shard{ws}" + ("+allgather(flow_hash)" if ws > 1 else ""),
+                       "key": "01..10"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "value_no_gather": None if nog is None else round(nog["mpkts"], 1),
+            "parity": {"full_batch": full_check, "oracle_sample": sample_check},
+            "secondary": secondary,
+        }
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+// rx_bin.hip -- stable counting sort of frame indices by length class, so
+// that the T lanes of every team in a wavefront round sum frames of similar
+// length (mixed-size batches, SURVEY.md 8(d) CMIX).  Three small launches:
+//   1. per-block histograms over a contiguous index range (bin-major matrix)
+//   2. one-block exclusive scan of the matrix
+//   3. per-block stable scatter of indices (wave ballots give the rank)
+// Reads 2 x 2 bytes and writes 4 bytes per frame: <1 % of the frame bytes
+// the transform itself reads.
+#include "rx_internal.h"
+
+namespace pptk {
+
+namespace {
+
+constexpr int NB = 16;        // length classes: len >> 8, clamped (256-byte steps)
+constexpr int BT = 256;       // threads per block
+constexpr int NWARP = BT / 64;
+
+__device__ __forceinline__ int bin_of(uint32_t len) {
+  const int b = (int)(len >> 8);
+  return b < NB - 1 ? b : NB - 1;
+}
+
+__global__ __launch_bounds__(BT) void bin_count(const uint16_t *len, uint64_t n,
+                                                uint64_t per_block, uint32_t *counts) {
+  __shared__ uint32_t h[NB];
+  if (threadIdx.x < NB) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t lo = blockIdx.x * per_block;
+  const uint64_t hi = min(lo + per_block, n);
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += BT)
+    atomicAdd(&h[bin_of(len[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x < NB) counts[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan of m = NB * nblocks counters, one block
+__global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m) {
+  __shared__ uint32_t part[1024];
+  const uint32_t per = (m + 1023) / 1024;
+  const uint32_t lo = threadIdx.x * per;
+  const uint32_t hi = min(lo + per, m);
+  uint32_t s = 0;
+  for (uint32_t k = lo; k < hi; ++k) s += counts[k];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - s;  // exclusive prefix of this thread's range
+  for (uint32_t k = lo; k < hi; ++k) {
+    const uint32_t c = counts[k];
+    counts[k] = run;
+    run += c;
+  }
+}
+
+__global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t n,
+                                                  uint64_t per_block, const uint32_t *offs,
+                                                  uint32_t *perm) {
+  __shared__ uint32_t cursor[NB];
+  __shared__ uint32_t wcnt[NWARP][NB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x < NB) cursor[threadIdx.x] = offs[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const uint64_t lo = blockIdx.x * per_block;
+  const uint64_t hi = min(lo + per_block, n);
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (uint64_t c0 = lo; c0 < hi; c0 += BT) {
+    const uint64_t i = c0 + threadIdx.x;
+    const bool ok = i < hi;
+    const int b = ok ? bin_of(len[i]) : -1;
+    uint32_t rank = 0;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const uint64_t mk = __ballot(b == k);
+      if (b == k) rank = __popcll(mk & lt_mask);
+      if (lane == 0) wcnt[wv][k] = __popcll(mk);
+    }
+    __syncthreads();
+    if (ok) {
+      uint32_t before = cursor[b];
+      for (int w2 = 0; w2 < wv; ++w2) before += wcnt[w2][b];
+      perm[before + rank] = (uint32_t)i;
+    }
+    __syncthreads();
+    if (threadIdx.x < NB) {
+      uint32_t add = 0;
+      for (int w2 = 0; w2 < NWARP; ++w2) add += wcnt[w2][threadIdx.x];
+      cursor[threadIdx.x] += add;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+size_t bin_scratch_bytes(uint64_t n, int grid) {
+  (void)n;
+  return (size_t)NB * (size_t)grid * sizeof(uint32_t);
+}
+
+hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm, void *scratch,
+                      hipStream_t s, int grid) {
+  if (n == 0) return hipSuccess;
+  const uint64_t per_block = ((n + grid - 1) / grid + BT - 1) / BT * BT;
+  const int g = (int)((n + per_block - 1) / per_block);
+  uint32_t *counts = (uint32_t *)scratch;
+  hipLaunchKernelGGL(bin_count, dim3(g), dim3(BT), 0, s, len, n, per_block, counts);
+  hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, s, counts, (uint32_t)(NB * g));
+  hipLaunchKernelGGL(bin_scatter, dim3(g), dim3(BT), 0, s, len, n, per_block,
+                     (const uint32_t *)counts, perm);
+  return hipGetLastError();
+}
+
+}  // namespace pptk

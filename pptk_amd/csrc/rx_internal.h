@@ -1,0 +1,40 @@
+// rx_internal.h -- shared between the kernels and the C-ABI shim.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pptk_rx.h"
+
+namespace pptk {
+
+// Kernel arguments (by value; a handful of SGPRs).
+struct RxKArgs {
+  const uint8_t *frames;
+  const uint64_t *off;   // nullable -> fixed stride
+  const uint16_t *len;   // nullable -> fixed_len
+  const uint32_t *perm;  // nullable -> identity
+  uint64_t stride;
+  uint64_t n;
+  pptk_rx_rec *recs;
+  uint64_t *hash;        // nullable
+  uint64_t k0, k1;       // SipHash key words (LE loads of key[0..7], key[8..15])
+  uint64_t mask6_0, mask6_1;  // ipv6_permitted prefix mask over the 16 address bytes
+  uint32_t mask4;        // ip_permitted prefix mask (host order)
+  uint32_t hash_mask;    // iphash_size - 1
+  uint32_t fixed_len;
+  uint32_t bucket4, bucket6;  // 1 = compute src_bucket for that family
+};
+
+// Kernel variants: T lanes per frame in the streaming checksum phase, S
+// 16-byte chunks per lane kept in registers (frames up to 16*T*S - 15
+// bytes are summed without a tail loop).
+enum RxVariant { RX_T4S1 = 0, RX_T4S2, RX_T16S2, RX_T16S6, RX_T64S2, RX_NVARIANTS };
+
+hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
+int rx_variant_blocks_per_cu(int variant);
+
+hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm,
+                      void *scratch, hipStream_t s, int grid);
+size_t bin_scratch_bytes(uint64_t n, int grid);
+
+}  // namespace pptk

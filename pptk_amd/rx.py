@@ -1,0 +1,172 @@
+"""ctypes front-end of libpptkrx.so (include/pptk_rx.h) for tests and bench.
+
+The product is the C-ABI library; this module only marshals torch/numpy
+buffers into it.  There is no Python or CPU fallback: if the library is
+missing, importing this module raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .records import REC_DTYPE
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpptkrx.so")
+
+
+class RxOpts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("key", ctypes.c_uint8 * 16),
+                ("iphash_bits4", ctypes.c_uint8), ("iphash_bits6", ctypes.c_uint8),
+                ("pad0", ctypes.c_uint16), ("iphash_size", ctypes.c_uint32),
+                ("max_batch", ctypes.c_uint32), ("max_frame", ctypes.c_uint32)]
+
+
+class RxDevBatch(ctypes.Structure):
+    _fields_ = [("d_frames", ctypes.c_void_p), ("d_off", ctypes.c_void_p),
+                ("d_len", ctypes.c_void_p), ("d_perm", ctypes.c_void_p),
+                ("stride", ctypes.c_uint64), ("fixed_len", ctypes.c_uint32),
+                ("max_len", ctypes.c_uint32), ("n", ctypes.c_uint64),
+                ("d_recs", ctypes.c_void_p), ("d_hash", ctypes.c_void_p)]
+
+
+class LdpPacket(ctypes.Structure):
+    """struct ldp_packet (include/ldp_packet.h; reference ldp/ldp.h:98-108)."""
+    _fields_ = [("data", ctypes.c_void_p), ("sz", ctypes.c_uint32),
+                ("ancillary64", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(LdpPacket) == 24
+assert ctypes.sizeof(RxOpts) == 36
+
+EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
+           "pptk_rx_batch", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
+           "pptk_rx_bin_device", "pptk_rx_version",
+           # kept per-packet APIs (ipcksum.h, hashseed.h)
+           "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
+           "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
+
+_lib = None
+
+
+def lib():
+    """Load libpptkrx.so once; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make` or __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        L.pptk_rx_opts_default.argtypes = [ctypes.POINTER(RxOpts)]
+        L.pptk_rx_opts_default.restype = None
+        L.pptk_rx_ctx_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(RxOpts)]
+        L.pptk_rx_ctx_create.restype = ctypes.c_int
+        L.pptk_rx_ctx_destroy.argtypes = [vp]
+        L.pptk_rx_ctx_destroy.restype = None
+        L.pptk_rx_batch.argtypes = [vp, vp, ctypes.c_int, vp]
+        L.pptk_rx_batch.restype = ctypes.c_int
+        L.pptk_rx_batch_device.argtypes = [vp, ctypes.POINTER(RxDevBatch), vp]
+        L.pptk_rx_batch_device.restype = ctypes.c_int
+        L.pptk_rx_bin_scratch_bytes.argtypes = [ctypes.c_uint64]
+        L.pptk_rx_bin_scratch_bytes.restype = ctypes.c_size_t
+        L.pptk_rx_bin_device.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp]
+        L.pptk_rx_bin_device.restype = ctypes.c_int
+        L.pptk_rx_version.restype = ctypes.c_char_p
+        L.ip_hdr_cksum_calc.argtypes = [vp, ctypes.c_uint16]
+        L.ip_hdr_cksum_calc.restype = ctypes.c_uint16
+        for f in ("tcp_cksum_calc", "udp_cksum_calc", "tcp6_cksum_calc", "udp6_cksum_calc"):
+            getattr(L, f).argtypes = [vp, ctypes.c_uint16, vp, ctypes.c_uint16]
+            getattr(L, f).restype = ctypes.c_uint16
+        L.ip_cksum_feed.argtypes = [ctypes.POINTER(ctypes.c_uint32), vp, ctypes.c_size_t]
+        L.ip_cksum_feed.restype = None
+        _lib = L
+    return _lib
+
+
+def _dp(t):
+    """Device pointer of a torch tensor (or None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class RxContext:
+    """One pptk_rx_ctx (one per rx thread in a C application)."""
+
+    def __init__(self, device=0, key=bytes(16), iphash_bits4=0, iphash_bits6=0,
+                 iphash_size=1, max_batch=8192, max_frame=9216):
+        L = lib()
+        o = RxOpts()
+        L.pptk_rx_opts_default(ctypes.byref(o))
+        o.device = device
+        for i, b in enumerate(bytes(key)):
+            o.key[i] = b
+        o.iphash_bits4, o.iphash_bits6, o.iphash_size = iphash_bits4, iphash_bits6, iphash_size
+        o.max_batch, o.max_frame = max_batch, max_frame
+        self._ctx = ctypes.c_void_p()
+        rc = L.pptk_rx_ctx_create(ctypes.byref(self._ctx), ctypes.byref(o))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_ctx_create failed ({rc})")
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            lib().pptk_rx_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch_device(self, frames, n, off=None, lens=None, stride=0, fixed_len=0,
+                     perm=None, recs=None, hash_out=None, max_len=0, stream=None):
+        """Asynchronous device batch on `stream` (torch stream or None = current).
+        frames/off/lens/perm/recs/hash_out are torch CUDA tensors."""
+        import torch
+        if recs is None:
+            recs = torch.empty((n, 64), dtype=torch.uint8, device=frames.device)
+        b = RxDevBatch(frames.data_ptr(), None if off is None else off.data_ptr(),
+                       None if lens is None else lens.data_ptr(),
+                       None if perm is None else perm.data_ptr(), stride, fixed_len,
+                       max_len, n, recs.data_ptr(),
+                       None if hash_out is None else hash_out.data_ptr())
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = lib().pptk_rx_batch_device(self._ctx, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_batch_device failed ({rc})")
+        return recs
+
+    def bin_device(self, lens, n, stream=None):
+        """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""
+        import torch
+        perm = torch.empty(n, dtype=torch.int32, device=lens.device)
+        scratch = torch.empty(lib().pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
+                              device=lens.device)
+        s = stream if stream is not None else torch.cuda.current_stream(lens.device)
+        rc = lib().pptk_rx_bin_device(self._ctx, _dp(lens), n, _dp(perm), _dp(scratch),
+                                      ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_bin_device failed ({rc})")
+        return perm
+
+    def batch_host(self, pkts):
+        """pptk_rx_batch over a ctypes array of LdpPacket; returns records."""
+        n = len(pkts)
+        recs = np.zeros(n, dtype=REC_DTYPE)
+        rc = lib().pptk_rx_batch(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n,
+                                 ctypes.c_void_p(recs.ctypes.data))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_batch failed ({rc})")
+        return recs
+
+
+def ldp_packets(buf, off, lens):
+    """Build an LdpPacket array pointing into numpy buffer `buf` (kept alive
+    by the caller), as ldp_in_nextpkts() would hand out."""
+    n = len(off)
+    arr = (LdpPacket * n)()
+    base = buf.ctypes.data
+    for i in range(n):
+        arr[i].data = base + int(off[i])
+        arr[i].sz = int(lens[i])
+        arr[i].ancillary64 = i
+    return arr

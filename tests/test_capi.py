@@ -1,0 +1,135 @@
+"""The C-ABI library: loads, exports every function include/*.h declares,
+and its kept per-packet host APIs give the reference's answers.  No GPU
+compute here (CPU suite)."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import framegen
+from conftest import ROOT, load_golden
+
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def _declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(INCLUDE, "*.h")):
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        txt = re.sub(r"//[^\n]*", "", txt)
+        txt = re.sub(r"#ifdef __cplusplus.*?#endif", "", txt, flags=re.S)
+        txt = re.sub(r"#[^\n]*", "", txt)
+        depth, cur, stmts = 0, [], []
+        for ch in txt:                       # statements at brace depth 0
+            if ch == "{":
+                depth += 1
+                if depth == 1:
+                    stmts.append("".join(cur))
+                    cur = []
+            elif ch == "}":
+                depth -= 1
+            elif depth == 0:
+                if ch == ";":
+                    stmts.append("".join(cur))
+                    cur = []
+                else:
+                    cur.append(ch)
+        for stmt in stmts:
+            stmt = " ".join(stmt.split())
+            m = re.match(r"^((?:const )?(?:struct )?\w[\w \*]*?)\b(\w+) ?\(([^()]*)\)$", stmt)
+            if not m or "static" in m.group(1) or "typedef" in m.group(1):
+                continue
+            names.add(m.group(2))
+    return names
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from pptk_amd import rx
+    return rx.lib()
+
+
+def test_library_exports_every_declared_function(lib):
+    declared = _declared_functions()
+    assert {"pptk_rx_batch", "pptk_rx_batch_device", "ip_cksum_feed",
+            "tcp6_cksum_calc", "hash_seed_init"} <= declared
+    missing = [f for f in sorted(declared) if not hasattr(lib, f)]
+    assert not missing, missing
+    for var in ("hash_seed", "hash_seed_inited"):
+        assert ctypes.c_int.in_dll(lib, var) is not None
+
+
+def test_exports_list_matches(lib):
+    from pptk_amd import rx
+    assert set(rx.EXPORTS) <= _declared_functions()
+
+
+def test_host_ip_cksum_feed_matches_oracle(lib, oracle_lib):
+    rng = np.random.default_rng(11)
+    for n in list(range(0, 80)) + [255, 1024, 1499, 1500, 9000, 65535]:
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        s = ctypes.c_uint32(0)
+        lib.ip_cksum_feed(ctypes.byref(s), data, n)
+        post = s.value
+        while post >> 16:
+            post = (post & 0xFFFF) + (post >> 16)
+        got = ((~post & 0xFFFF) >> 8) | (((~post) & 0xFF) << 8)
+        assert got == oracle_lib.cksum(data), n
+    # all-zero input: 0xffff in both
+    s = ctypes.c_uint32(0)
+    lib.ip_cksum_feed(ctypes.byref(s), bytes(100), 100)
+    assert s.value == 0
+
+
+@pytest.mark.parametrize("name", ["edge", "cmix", "fuzz"])
+def test_host_l4_cksums_match_golden(lib, name):
+    """tcp/udp(6)_cksum_calc from libpptkrx.so reproduce the golden l4_cksum
+    of every frame that has an L4 header."""
+    from pptk_amd.records import F_IPV6, F_L4, as_records
+    z = load_golden(name)
+    recs = as_records(z["recs"])
+    buf = z["buf"]
+    n_checked = 0
+    for i in np.nonzero(recs["flags"] & F_L4)[0]:
+        r = recs[i]
+        o = int(z["off"][i])
+        f = buf[o:o + int(z["len"][i])].tobytes()
+        ip = f[r["l3_off"]:]
+        l4 = f[r["l4_off"]:]
+        v6 = bool(r["flags"] & F_IPV6)
+        fn = {(6, False): lib.tcp_cksum_calc, (17, False): lib.udp_cksum_calc,
+              (6, True): lib.tcp6_cksum_calc, (17, True): lib.udp6_cksum_calc}[(int(r["proto"]), v6)]
+        iplen = 40 if v6 else (ip[0] & 15) * 4
+        assert fn(ip, iplen, l4, int(r["l4_len"])) == r["l4_cksum"], i
+        if not v6:
+            assert lib.ip_hdr_cksum_calc(ip, iplen) == r["ip_cksum"]
+        n_checked += 1
+    assert n_checked > 100
+
+
+def test_c_dropin_program(tmp_path):
+    """Compile a C client with plain gcc against include/ + libpptkrx.so."""
+    exe = str(tmp_path / "capi_dropin")
+    libdir = os.path.join(ROOT, "pptk_amd")
+    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Werror",
+                           "-I", INCLUDE, os.path.join(ROOT, "tests", "c", "capi_dropin.c"),
+                           "-L", libdir, "-lpptkrx", f"-Wl,-rpath,{libdir}", "-o", exe])
+    import torch
+    args = [exe] + ([] if torch.cuda.is_available() else ["nogpu"])
+    out = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "capi_dropin ok" in out.stdout
+
+
+def test_record_layout_matches_header():
+    from pptk_amd.records import REC_DTYPE
+    txt = open(os.path.join(INCLUDE, "pptk_rx.h")).read()
+    for name in REC_DTYPE.names:
+        off = REC_DTYPE.fields[name][1]
+        m = re.search(rf"\b{name}(\[\d+\])?;\s*/\*\s*(\d+)", txt)
+        assert m and int(m.group(2)) == off, name

@@ -1,0 +1,144 @@
+"""Parity of the HIP rx transform (through the C-ABI) with the golden
+fixtures produced by the reference's own functions (tests/golden/), bit for
+bit, in every addressing mode and kernel variant.  Needs an MI355X."""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_SETS, load_golden
+from pptk_amd.records import F_PARSED, as_records, diff_records
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def _ctx(z, bucket=True):
+    from pptk_amd.rx import RxContext
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    if not bucket:
+        b4 = b6 = 0
+    return RxContext(0, z["key"].tobytes(), b4, b6, hs)
+
+
+def _upload(buf, dev, shift=0):
+    big = torch.zeros(buf.size + shift + 64, dtype=torch.uint8, device=dev)
+    big[shift:shift + buf.size] = torch.from_numpy(buf).to(dev)
+    return big, big[shift:]
+
+
+def _run(ctx, z, dev, shift=0, perm=False, hash_out=False, max_len=None,
+         stride=None):
+    buf, off, lens = z["buf"], z["off"], z["len"]
+    n = len(off)
+    _keep, frames = _upload(buf, dev, shift)
+    lens_t = torch.from_numpy(lens.view(np.int16)).to(dev)
+    kw = {}
+    if stride is None:
+        kw["off"] = torch.from_numpy(off.view(np.int64)).to(dev)
+        kw["lens"] = lens_t
+        kw["max_len"] = int(lens.max()) if max_len is None else max_len
+    else:
+        assert np.all(off == np.arange(n, dtype=np.uint64) * stride)
+        kw["stride"] = stride
+        kw["fixed_len"] = int(lens[0])
+    p = ctx.bin_device(lens_t, n) if perm else None
+    h = torch.full((n,), -1, dtype=torch.int64, device=dev) if hash_out else None
+    recs = ctx.batch_device(frames, n, perm=p, hash_out=h, **kw)
+    torch.cuda.synchronize()
+    out = recs.cpu().numpy().reshape(-1)
+    if hash_out:
+        return out, h.cpu().numpy().view(np.uint64), (None if p is None else p.cpu().numpy())
+    return out
+
+
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+@pytest.mark.parametrize("shift", [0, 1, 6, 15])
+def test_offsets_mode(name, shift, dev):
+    z = load_golden(name)
+    ctx = _ctx(z)
+    got = _run(ctx, z, dev, shift=shift)
+    d = diff_records(got, z["recs"])
+    assert not d, d
+
+
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+@pytest.mark.parametrize("max_len", [1, 40, 100, 400, 1500, 65535])
+def test_every_variant(name, max_len, dev):
+    """max_len is a tuning hint: a wrong hint selects another kernel variant
+    (T4S1 ... T64S2) but must never change a result."""
+    z = load_golden(name)
+    got = _run(_ctx(z), z, dev, shift=3, max_len=max_len)
+    d = diff_records(got, z["recs"])
+    assert not d, d
+
+
+@pytest.mark.parametrize("name,stride", [("c64", 64), ("c1500", 1500)])
+@pytest.mark.parametrize("shift", [0, 4, 5, 13])
+def test_fixed_stride(name, stride, shift, dev):
+    z = load_golden(name)
+    got = _run(_ctx(z), z, dev, shift=shift, stride=stride)
+    d = diff_records(got, z["recs"])
+    assert not d, d
+
+
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_binned_order_and_hash_out(name, dev):
+    z = load_golden(name)
+    got, h, perm = _run(_ctx(z), z, dev, perm=True, hash_out=True)
+    d = diff_records(got, z["recs"])
+    assert not d, d
+    want = as_records(z["recs"])
+    assert np.array_equal(h, np.where(want["flags"] & F_PARSED, want["flow_hash"], 0))
+    # the permutation is a stable sort of indices by length class
+    n = len(z["off"])
+    assert np.array_equal(np.sort(perm), np.arange(n))
+    cls = np.minimum(z["len"].astype(np.int64) >> 8, 15)
+    assert np.array_equal(perm, np.argsort(cls, kind="stable"))
+
+
+@pytest.mark.parametrize("name", ["edge", "cmix"])
+def test_bucket_disabled(name, dev):
+    z = load_golden(name)
+    got = _run(_ctx(z, bucket=False), z, dev)
+    want = as_records(z["recs"]).copy()
+    want["src_bucket"] = 0
+    d = diff_records(got, want)
+    assert not d, d
+
+
+@pytest.mark.parametrize("name", ["edge", "fuzz", "cmix"])
+def test_host_batch_ldp_packets(name, dev):
+    """pptk_rx_batch: borrowed host frames (ldp_packet[]) in, records out."""
+    from pptk_amd.rx import ldp_packets
+    z = load_golden(name)
+    ctx = _ctx(z)
+    buf = np.ascontiguousarray(z["buf"])
+    pkts = ldp_packets(buf, z["off"], z["len"])
+    ancillary_before = [p.ancillary64 for p in pkts]
+    got = ctx.batch_host(pkts)
+    d = diff_records(got, z["recs"])
+    assert not d, d
+    assert [p.ancillary64 for p in pkts] == ancillary_before
+
+
+def test_empty_and_single(dev):
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    frames = torch.zeros(64, dtype=torch.uint8, device=dev)
+    recs = torch.zeros((1, 64), dtype=torch.uint8, device=dev)
+    ctx.batch_device(frames, 0, stride=64, fixed_len=64, recs=recs)  # n = 0: no-op
+    torch.cuda.synchronize()
+    assert int(recs.sum()) == 0
+    for i in range(0, len(z["off"]), 37):
+        one = {"buf": z["buf"][int(z["off"][i]):int(z["off"][i]) + int(z["len"][i])].copy(),
+               "off": np.zeros(1, np.uint64), "len": z["len"][i:i + 1].copy(),
+               "key": z["key"], "iphash": z["iphash"]}
+        got = _run(ctx, one, dev)
+        d = diff_records(got, z["recs"][i:i + 1])
+        assert not d, f"frame {i}: {d}"
