@@ -31,6 +31,12 @@ $(LIB): $(HIP_OBJS) $(C_OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# A/B builds of the product library with extra defines, e.g.
+#   make abvariant NAME=full DEFS=-DPPTK_RX_FULL_UNROLL
+abvariant:
+	$(MAKE) OBJDIR=build/ab_$(NAME)/obj LIB=build/ab_$(NAME)/libpptkrx.so \
+	  HIPFLAGS="$(HIPFLAGS) $(DEFS)" build/ab_$(NAME)/libpptkrx.so
+
 asm: $(HIP_SRCS)
 	@mkdir -p build/asm
 	cd build/asm && $(HIPCC) $(HIPFLAGS) -I../../include -c ../../pptk_amd/csrc/rx_kernel.hip -save-temps -o rx_kernel.o -Rpass-analysis=kernel-resource-usage 2> resource.txt; true
@@ -46,3 +52,8 @@ tools/libpptksynth.so: tools/synth.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
 all: tools/libpptksynth.so
+
+tools/libmembench.so: tools/membench.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
+
+all: tools/libmembench.so

@@ -30,6 +30,7 @@ METRIC = "Mpkts/s device-resident (cksum+parse+SipHash), 64B & 1500B; % HBM roof
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KEY = bytes(range(1, 17))
 N_PER_GPU = 16 * 1024 * 1024
+SETTLE_S = 1.5                  # seconds of untimed launches before warmup
 
 
 def log(*a):
@@ -86,7 +87,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check):
     b = make_batch(cfg, n, dev, first=rank * n)
     torch.cuda.synchronize(dev)
     recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-    hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
+    hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)] if (gather and ws > 1) else None
     perm = None
     kw = {}
     if "off" in b:
@@ -101,13 +102,26 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check):
     work = [None]
 
     def step(k):
-        h = hbuf[k & 1]
+        # the dense flow-hash array only feeds the all-gather (N > 1); at
+        # N = 1 the records (which carry flow_hash) are the whole output
+        h = hbuf[k & 1] if gout is not None else None
         ctx.batch_device(b["frames"], n, perm=perm, recs=recs, hash_out=h, **kw)
         if gout is not None:
             if work[0] is not None:
                 work[0].wait()                  # previous gather done before reuse
             _, work[0] = allgather_flow_hash(h, gout, async_op=True)
 
+    # settle: clocks ramp up over the first few hundred ms of sustained
+    # load (the kernel trace shows the first launches 4-5 % slower, and a
+    # cold first process up to 20 %); run until `settle` seconds have passed
+    # before the W warmup steps, so the K timed steps see steady state
+    t_settle = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t_settle < SETTLE_S:
+        step(k)
+        k += 1
+        if k % 16 == 0:
+            torch.cuda.synchronize(dev)
     for k in range(warmup):
         step(k)
     if work[0] is not None:
@@ -225,6 +239,21 @@ def cpu_baseline(b, seconds=10.0, sample=262144):
             "cpu_model": cpu}
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+
+
+def pmc_traffic(cfg):
+    """HBM bytes per launch of this config from the committed rocprofv3 PMC
+    passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected; see
+    tools/pmc_summary.py); (None, None) when no summary exists."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            e = json.load(f)[cfg]
+        return int(e["traffic_bytes"]), os.path.relpath(PMC_SUMMARY, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -236,7 +265,13 @@ def main():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--only", default=None, help="run just this config (profiling)")
+    ap.add_argument("--no-membench", action="store_true",
+                    help="skip the in-process HBM read/copy ceiling probe")
+    ap.add_argument("--settle", type=float, default=SETTLE_S,
+                    help="seconds of untimed launches before the warmup steps")
     args = ap.parse_args()
+    global SETTLE_S
+    SETTLE_S = args.settle
 
     import torch
     from pptk_amd.rx import RxContext
@@ -252,10 +287,18 @@ def main():
     if ws > 1:
         nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False)
 
+    box = None
+    if not args.no_membench:
+        from tools.membench import measure
+        box = measure(prim["_batch"]["frames"])
+        log(f"[rank {rank}] box HBM: {box}")
+
     bytes_per_launch = prim["bytes"]
     achieved = bytes_per_launch / (prim["kernel_ms"] * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(primary_cfg)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": tsrc,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_ms": round(prim["kernel_ms"], 4)}
 
@@ -306,6 +349,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "value_no_gather": None if nog is None else round(nog["mpkts"], 1),
+            "box_hbm": box,
             "parity": {"full_batch": full_check, "oracle_sample": sample_check},
             "secondary": secondary,
         }

@@ -130,6 +130,23 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *ctx, const uint16_t *d_len,
                        uint64_t n, uint32_t *d_perm, void *d_scratch,
                        void *stream);
 
+/* Tuning: force kernel variant `variant` (0 .. pptk_rx_variant_count()-1)
+ * and/or memory-policy flags for every later batch of this context; -1
+ * restores the automatic choice (variant by frame length and alignment).
+ * flags: PPTK_RX_TUNE_NT_LOADS (non-temporal frame loads),
+ * PPTK_RX_TUNE_NO_STAGING (store records per lane, not via LDS),
+ * PPTK_RX_TUNE_NT_STORES (non-temporal record stores),
+ * PPTK_RX_TUNE_SC1_STORES (write-through record stores).
+ * Variants and flags change speed only: results are identical for every
+ * setting on every input.  (Flag bits 0x8 and 0x10 are diagnostics that skip
+ * record stores / the per-frame phase: never set them outside profiling.) */
+#define PPTK_RX_TUNE_NT_LOADS 0x1
+#define PPTK_RX_TUNE_NO_STAGING 0x2
+#define PPTK_RX_TUNE_NT_STORES 0x20
+#define PPTK_RX_TUNE_SC1_STORES 0x40
+int pptk_rx_set_tuning(struct pptk_rx_ctx *ctx, int variant, int flags);
+int pptk_rx_variant_count(void);
+
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);
 

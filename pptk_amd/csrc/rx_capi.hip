@@ -29,6 +29,8 @@ struct pptk_rx_ctx {
   RxKArgs tmpl{};      // key/iphash part of the kernel arguments
   int ncu = 256;
   int bpc[RX_NVARIANTS] = {};
+  int forced_variant = -1;
+  int forced_flags = -1;
   // host-batch staging (pptk_rx_batch)
   hipStream_t stream = nullptr;
   size_t cap_pkts = 0, cap_bytes = 0;
@@ -162,7 +164,14 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
     mmax = (uint32_t)((p % gg) + 16 - gg);
   }
   uint32_t maxlen = b->d_len ? (b->max_len ? b->max_len : 65535u) : b->fixed_len;
-  const int variant = pick_variant(maxlen + mmax);
+  int variant = pick_variant(maxlen + mmax);
+  static int force = -2;   // PPTK_RX_VARIANT: A/B override (results never change)
+  if (force == -2) {
+    const char *e = getenv("PPTK_RX_VARIANT");
+    force = e ? atoi(e) : -1;
+  }
+  if (force >= 0 && force < RX_NVARIANTS) variant = force;
+  if (c->forced_variant >= 0) variant = c->forced_variant;
 
   RxKArgs a = c->tmpl;
   a.frames = b->d_frames;
@@ -175,6 +184,18 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   a.recs = b->d_recs;
   a.hash = b->d_hash;
 
+  // Memory policy (PPTK_RX_TUNE_*).  Default: non-temporal frame loads and
+  // record stores for the streaming variants (frames are read once, records
+  // written once: measured 4.47 -> 4.25 ms on C1500 in one process, see
+  // DESIGN.md "Measurement log"), plain for the small-frame variants (nt
+  // measured slower on C64).  PPTK_RX_TUNE overrides for A/B runs.
+  static int tune = -2;
+  if (tune == -2) {
+    const char *e = getenv("PPTK_RX_TUNE");
+    tune = e ? atoi(e) : -1;
+  }
+  a.tune = tune >= 0 ? (uint32_t)tune : (variant >= RX_T16S2 ? 33u : 0u);
+  if (c->forced_flags >= 0) a.tune = (uint32_t)c->forced_flags;
   const uint64_t ntiles = (b->n + 63) / 64;
   const uint64_t want_blocks = (ntiles + 3) / 4;
   static int grid_mult = -1;
@@ -186,6 +207,15 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   const int grid = (int)std::min<uint64_t>(want_blocks, cap);
   return hip_err(launch_rx(variant, a, grid, (hipStream_t)stream));
 }
+
+int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
+  if (!c || variant < -1 || variant >= RX_NVARIANTS || flags < -1 || flags > 255) return -EINVAL;
+  c->forced_variant = variant;
+  c->forced_flags = flags;
+  return 0;
+}
+
+int pptk_rx_variant_count(void) { return RX_NVARIANTS; }
 
 size_t pptk_rx_bin_scratch_bytes(uint64_t n) { return bin_scratch_bytes(n, 2048); }
 

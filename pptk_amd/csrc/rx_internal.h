@@ -23,12 +23,18 @@ struct RxKArgs {
   uint32_t hash_mask;    // iphash_size - 1
   uint32_t fixed_len;
   uint32_t bucket4, bucket6;  // 1 = compute src_bucket for that family
+  uint32_t tune;         // A/B knobs (PPTK_RX_TUNE): bit0 nt frame loads, bit1 no LDS record staging
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S
 // 16-byte chunks per lane kept in registers (frames up to 16*T*S - 15
 // bytes are summed without a tail loop).
-enum RxVariant { RX_T4S1 = 0, RX_T4S2, RX_T16S2, RX_T16S6, RX_T64S2, RX_NVARIANTS };
+enum RxVariant {
+  RX_T4S1 = 0, RX_T4S2, RX_T16S2, RX_T16S6, RX_T32S3, RX_T64S2,
+  RX_T16S7L, RX_T32S4L,   // chunk grid on 128-byte lines
+  RX_T32S3D7, RX_T16S6D1, // prefetch-depth experiments
+  RX_NVARIANTS
+};
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
 int rx_variant_blocks_per_cu(int variant);

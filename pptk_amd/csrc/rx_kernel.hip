@@ -63,8 +63,18 @@ __device__ __forceinline__ uint32_t finish16(uint32_t s) {
   return bswap16(~fold16(s) & 0xffffu);
 }
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) {
-  return (x << b) | (x >> (64 - b));
+// 64-bit rotate left by 0 < b < 32 as two v_alignbit_b32 (full-rate 32-bit
+// funnel shifts); b == 32 is a register swap.
+template <int B>
+__device__ __forceinline__ uint64_t rotl64(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if constexpr (B == 32) {
+    return (uint64_t)hi | ((uint64_t)lo << 32);
+  } else {
+    const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - B);
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - B);
+    return (uint64_t)nlo | ((uint64_t)nhi << 32);
+  }
 }
 
 struct Sip {
@@ -73,10 +83,10 @@ struct Sip {
       : v0(0x736f6d6570736575ULL ^ k0), v1(0x646f72616e646f6dULL ^ k1),
         v2(0x6c7967656e657261ULL ^ k0), v3(0x7465646279746573ULL ^ k1) {}
   __device__ __forceinline__ void round() {
-    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = rotl64(v0, 32);
-    v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;
-    v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;
-    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);
+    v0 += v1; v1 = rotl64<13>(v1); v1 ^= v0; v0 = rotl64<32>(v0);
+    v2 += v3; v3 = rotl64<16>(v3); v3 ^= v2;
+    v0 += v3; v3 = rotl64<21>(v3); v3 ^= v0;
+    v2 += v1; v1 = rotl64<17>(v1); v1 ^= v2; v2 = rotl64<32>(v2);
   }
   // siphash_feed_u64 (misc/siphash.h:42-68), cROUNDS = 2
   __device__ __forceinline__ void block(uint64_t m) {
@@ -130,7 +140,7 @@ __device__ __forceinline__ bool is_v6_ext(uint32_t nh) {
   return nh == 0 || nh == 60 || nh == 43 || nh == 44 || nh == 51;
 }
 
-__device__ Parse parse_frame(const FrameView &v, uint32_t len) {
+__device__ __forceinline__ Parse parse_frame(const FrameView &v, uint32_t len) {
   Parse p = {0, 0, 0, 0, 0, 0, 0};
   if (len < 14 || len > 65535) {
     p.flags = PPTK_RX_F_MALFORMED;
@@ -221,8 +231,14 @@ __device__ Parse parse_frame(const FrameView &v, uint32_t len) {
   return p;
 }
 
-// Sum the bytes of one aligned 16-byte chunk that fall inside the frame
-// region [rs, re); `o` is the chunk's frame-relative offset (may be < 0).
+// Byte-keep mask for bytes [lo, hi) of a dword (0 <= lo, hi <= 4).
+__device__ __forceinline__ uint32_t bmask(int lo, int hi) {
+  return (uint32_t)(((1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull));
+}
+
+// Sum (absolute-address pairing) the bytes of one aligned 16-byte chunk that
+// fall inside the frame region [rs, re); `o` is the chunk's frame-relative
+// offset (may be < 0).
 __device__ __forceinline__ uint32_t sum_chunk(u32x4 c, int o, int rs, int re, uint32_t acc) {
   if (o >= rs && o + 16 <= re) {
     acc = dot16(c.x, acc);
@@ -233,13 +249,62 @@ __device__ __forceinline__ uint32_t sum_chunk(u32x4 c, int o, int rs, int re, ui
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const int od = o + 4 * d;
-      const int lo = min(max(rs - od, 0), 4);
-      const int hi = min(max(re - od, 0), 4);
-      const uint32_t mk = (uint32_t)(((1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull));
-      acc = dot16(c[d] & mk, acc);
+      acc = dot16(c[d] & bmask(min(max(rs - od, 0), 4), min(max(re - od, 0), 4)), acc);
     }
   }
   return acc;
+}
+
+// Team-round chunk sum: whole chunks from the team's first chunk on (no head
+// masking), only bytes past the frame end masked.  `o` = frame offset.
+__device__ __forceinline__ uint32_t sum_chunk_from(u32x4 c, int o, int start, int len,
+                                                   uint32_t acc) {
+  uint32_t t;
+  if (o + 16 <= len) {
+    t = dot16(c.x, 0);
+    t = dot16(c.y, t);
+    t = dot16(c.z, t);
+    t = dot16(c.w, t);
+  } else {
+    t = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      t = dot16(c[d] & bmask(0, min(max(len - (o + 4 * d), 0), 4)), t);
+  }
+  return o >= start ? acc + t : acc;
+}
+
+// First chunk boundary (frame offset) at or after byte 18 of a frame whose
+// start sits at `m` inside its chunk: the team rounds sum [team_start, len);
+// 18 <= team_start <= 33 < 34 <= every L4 start, so the owning lane only
+// subtracts the few bytes [team_start, rs).
+__device__ __forceinline__ int team_start_of(int m) {
+  return (((m + 18 + 15) >> 4) << 4) - m;
+}
+
+// Absolute-pairing sum of frame bytes [a, b): image dwords first, bytes past
+// the image from global memory (rare: long IPv6 chains, Ethernet padding
+// beyond the parked 128 bytes).
+__device__ uint32_t sum_abs(const FrameView &v, int a, int b) {
+  uint32_t s = 0;
+  const int hi_img = min(b, v.lim);
+  if (a < hi_img) {
+    const int lo_o = v.m + a, hi_o = v.m + hi_img;
+    for (int d = lo_o & ~3; d < hi_o; d += 4) {
+      const uint32_t w = *(const uint32_t *)(v.img + d);
+      s = dot16(w & bmask(min(max(lo_o - d, 0), 4), min(max(hi_o - d, 0), 4)), s);
+    }
+  }
+  for (int k = max(a, v.lim); k < b; ++k)
+    s += (uint32_t)v.g[k] << (((v.m + k) & 1) * 8);
+  return s;
+}
+
+// Frame chunk load; frames are read once, so optionally non-temporal.
+template <bool NT>
+__device__ __forceinline__ u32x4 ldc(const u32x4 *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
 }
 
 template <int T>
@@ -250,10 +315,93 @@ __device__ __forceinline__ uint32_t team_sum(uint32_t x) {
   return x;
 }
 
+// Per-lane descriptor of the lane's frame in a tile.
+struct Desc {
+  uint64_t base;
+  uint32_t len, idx;
+};
+
+// Descriptors come either from arithmetic (FIXED: frame i at i * stride,
+// fixed_len bytes, identity order -- no memory traffic, nothing to wait for)
+// or from the d_perm / d_off / d_len arrays (GATHER).
+template <bool GATHER>
+__device__ __forceinline__ uint32_t desc_idx(const RxKArgs &a, uint64_t tile, int lane) {
+  const uint64_t i = tile * WAVE + lane;
+  if (i >= a.n) return 0xffffffffu;
+  if constexpr (GATHER) return a.perm ? a.perm[i] : (uint32_t)i;
+  else return (uint32_t)i;
+}
+
+template <bool GATHER>
+__device__ __forceinline__ Desc desc_fill(const RxKArgs &a, uint32_t idx) {
+  Desc d = {0, 0, 0xffffffffu};
+  if (idx != 0xffffffffu) {
+    d.idx = idx;
+    if constexpr (GATHER) {
+      d.base = a.off ? a.off[idx] : (uint64_t)idx * a.stride;
+      d.len = a.len ? (uint32_t)a.len[idx] : a.fixed_len;
+    } else {
+      d.base = (uint64_t)idx * a.stride;
+      d.len = a.fixed_len;
+    }
+  }
+  return d;
+}
+
+template <bool GATHER>
+__device__ __forceinline__ Desc load_desc(const RxKArgs &a, uint64_t tile, int lane) {
+  return desc_fill<GATHER>(a, desc_idx<GATHER>(a, tile, lane));
+}
+
+// One round's staged chunks for a team: S chunks per lane + the frame.
+template <int S>
+struct Buf {
+  u32x4 v[S];
+  uint64_t pb;
+  uint32_t pl;
+};
+
+// AL = log2 of the chunk-grid alignment: 4 -> chunks on 16-byte boundaries
+// of the frame buffer, 7 -> on 128-byte (cache line) boundaries, so a team's
+// 16*T contiguous bytes are whole lines (no line split between two loads).
+template <int T, int S, int AL, bool NT>
+__device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, int r, int g,
+                                             int j) {
+  Buf<S> b;
+  const int q = g * T + r;
+  b.pb = __shfl(d.base, q);
+  b.pl = __shfl(d.len, q);
+  const int m = (int)(b.pb & ((1u << AL) - 1));
+  const u32x4 *c0 = (const u32x4 *)(a.frames + (b.pb - (uint64_t)m));
+  const int nch = (m + (int)b.pl + 15) >> 4;
+  const int clast = nch > 0 ? nch - 1 : 0;
+  // Unconditional loads (chunks past the frame re-read its last chunk):
+  // branch-free loads let the compiler count vmcnt precisely, so the D
+  // rounds in flight are not drained at every use.
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int c = s * T + j;
+    b.v[s] = ldc<NT>(c0 + min(c, clast));   // bytes past the frame are masked at use
+  }
+  return b;
+}
+
+// Waves per SIMD the register allocator must leave room for: the streaming
+// variants keep D = 3 rounds of S chunks in registers (D * S * 4 VGPRs) and
+// need 2 waves/SIMD; the small-frame variants 4.
 template <int T, int S>
-__global__ __launch_bounds__(WAVE * WPB) void rx_kernel(RxKArgs a) {
+constexpr int min_waves_per_simd() { return S * T >= 32 ? 2 : 4; }
+
+// D = rounds in flight; (D + 1) must divide T so that the prefetch ring is
+// back in its starting registers at the tile boundary (no moves of in-flight
+// load destinations, which would force vmcnt waits).
+template <int T, int S, int D, int AL, bool NT, bool GATHER>
+__global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_kernel(RxKArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * IMG_STRIDE];
   constexpr int IMGC = (S * T < IMG_CHUNKS) ? S * T : IMG_CHUNKS;  // chunks parked
+  constexpr uint32_t ALM = (1u << AL) - 1;
+  static_assert(T % (D + 1) == 0, "prefetch ring must wrap at the tile boundary");
+  constexpr bool UNROLL = T <= 32;   // tail chunks summed in the lane phase
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const int g = lane / T, j = lane % T;
@@ -261,227 +409,281 @@ __global__ __launch_bounds__(WAVE * WPB) void rx_kernel(RxKArgs a) {
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
   const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
 
-  for (uint64_t tile = (uint64_t)blockIdx.x * WPB + wv; tile < ntiles; tile += nwaves) {
-    // ---- the lane's own frame
-    const uint64_t i = tile * WAVE + lane;
-    const bool valid = i < a.n;
-    const uint32_t idx = valid ? (a.perm ? a.perm[i] : (uint32_t)i) : 0u;
-    const uint64_t base = valid ? (a.off ? a.off[idx] : (uint64_t)idx * a.stride) : 0ull;
-    const uint32_t flen = valid ? (a.len ? (uint32_t)a.len[idx] : a.fixed_len) : 0u;
-
-    uint32_t my_sum = 0, my_p0 = 0, my_p1 = 0, my_p2 = 0;
-
-    // ---- streaming rounds: team g sums frame g*T + r
-    u32x4 cur[S];
-    uint64_t cb;
-    uint32_t cl;
-    {
-      const int q = g * T;
-      cb = __shfl(base, q);
-      cl = __shfl(flen, q);
-      const int m = (int)(cb & 15);
-      const u32x4 *c0 = (const u32x4 *)(a.frames + (cb - (uint64_t)m));
-      const int nch = (m + (int)cl + 15) >> 4;
+  uint64_t tile = (uint64_t)blockIdx.x * WPB + wv;
+  Desc dc = load_desc<GATHER>(a, tile, lane);
+  Desc dn = load_desc<GATHER>(a, tile + nwaves, lane);
+  // prologue: the first D rounds of the first tile, in slots 0 .. D-1
+  Buf<S> b[D + 1];
+  // (issued strictly in slot order: the loop-header wait is computed from
+  // the older of the entry and back-edge states, and a reordered prologue
+  // would turn it into a full drain)
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int c = s * T + j;
-        cur[s] = c < nch ? c0[c] : (u32x4){0, 0, 0, 0};
-      }
-    }
+  for (int k = 0; k < D; ++k) {
+    b[k] = load_round<T, S, AL, NT>(a, dc, k, g, j);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  while (tile < ntiles) {
+    uint32_t my_sum = 0;
+    // Descriptors of tile + 2 nwaves, in two stages so that no wait on them
+    // ever has to drain the chunk loads in flight: the index load (perm) is
+    // issued before this tile's rounds, the dependent offset/length loads
+    // after them; both complete long before they are needed.
+    const uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * nwaves, lane);
+    // ---- streaming rounds: team g sums frame g*T + r over [team_start, len).
+    // Fixed-slot ring of D + 1 rounds: round r lives in slot r % (D + 1); the
+    // loop is unrolled by D + 1 so every slot index is a constant and no
+    // register of an in-flight load is ever copied.
+#ifdef PPTK_RX_FULL_UNROLL
+#pragma unroll(T <= 16 ? T : 1)
+#else
 #pragma unroll 1
-    for (int r = 0; r < T; ++r) {
-      const int q = g * T + r;
-      const uint64_t pb = cb;
-      const uint32_t pl = cl;
-      // issue the next round's loads first
-      u32x4 nxt[S];
-      if (r + 1 < T) {
-        cb = __shfl(base, q + 1);
-        cl = __shfl(flen, q + 1);
-        const int mn = (int)(cb & 15);
-        const u32x4 *c0n = (const u32x4 *)(a.frames + (cb - (uint64_t)mn));
-        const int nchn = (mn + (int)cl + 15) >> 4;
+#endif
+    for (int r0 = 0; r0 < T; r0 += D + 1) {
+#pragma unroll
+      for (int u = 0; u <= D; ++u) {
+        const int r = r0 + u;
+        {  // keep D rounds in flight: round r + D (of this or the next tile)
+          const int rr = r + D;
+          const Desc &dd = rr < T ? dc : dn;
+          b[(u + D) % (D + 1)] = load_round<T, S, AL, NT>(a, dd, rr < T ? rr : rr - T, g, j);
+        }
+        const Buf<S> &cb = b[u];
+        const int q = g * T + r;
+        const int m = (int)(cb.pb & ALM);       // frame start inside its first chunk row
+        const int c_img = m >> 4;                  // first chunk holding frame bytes
+        const int nch = (m + (int)cb.pl + 15) >> 4;
+        uint8_t *img = wimg + q * IMG_STRIDE;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          if (s * T < IMGC + (int)(ALM >> 4)) {
+            const int ci = s * T + j - c_img;      // image = 16-byte chunks from floor16(frame)
+            if (ci >= 0 && ci < IMGC)
+              *(u32x4 *)(img + 16 * ci) = cb.v[s];
+          }
+        }
+        uint32_t acc = 0;
+        const int ts = team_start_of(m & 15);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           const int c = s * T + j;
-          nxt[s] = c < nchn ? c0n[c] : (u32x4){0, 0, 0, 0};
+          acc = sum_chunk_from(cb.v[s], 16 * c - m, ts, (int)cb.pl, acc);
         }
-      }
-      const int m = (int)(pb & 15);
-      const int nch = (m + (int)pl + 15) >> 4;
-      uint8_t *img = wimg + q * IMG_STRIDE;
-      // park the first IMGC chunks of the frame in LDS
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if (s * T < IMGC) {
-          const int c = s * T + j;
-          if (c < IMGC)
-            *(u32x4 *)(img + 16 * c) = cur[s];
+        if (!UNROLL && nch > S * T) {  // frames longer than the staged chunks
+          const u32x4 *c0 = (const u32x4 *)(a.frames + (cb.pb - (uint64_t)m));
+          for (int c = S * T + j; c < nch; c += T)
+            acc = sum_chunk_from(ldc<NT>(c0 + c), 16 * c - m, ts, (int)cb.pl, acc);
         }
+        acc = team_sum<T>(acc);
+        if (j == r)
+          my_sum = acc;
       }
-      __builtin_amdgcn_wave_barrier();
-      const uint8_t *gf = a.frames + pb;
-      const FrameView v = {img, gf, m, 16 * IMGC - m};
-      const Parse p = parse_frame(v, pl);
-      int rs = 0, re = 0;
-      if (p.flags & PPTK_RX_F_L4) {
-        rs = (int)p.rs;
-        re = (int)p.re;
-      }
-      uint32_t acc = 0;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const int c = s * T + j;
-        if (c < nch)
-          acc = sum_chunk(cur[s], 16 * c - m, rs, re, acc);
-      }
-      if (nch > S * T) {  // long frames: unbuffered tail
-        const u32x4 *c0 = (const u32x4 *)(a.frames + (pb - (uint64_t)m));
-        for (int c = S * T + j; c < nch; c += T)
-          acc = sum_chunk(c0[c], 16 * c - m, rs, re, acc);
-      }
-      acc = team_sum<T>(acc);
-      if (j == r) {
-        my_sum = acc;
-        my_p0 = p.flags | (p.l3 << 16) | (p.ver << 24);
-        my_p1 = p.rs | (p.re << 16);
-        my_p2 = p.et | (p.proto << 16);
-      }
-      if (r + 1 < T) {
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-          cur[s] = nxt[s];
-      }
-      __builtin_amdgcn_wave_barrier();
     }
+    const Desc d2 = desc_fill<GATHER>(a, idx2);
 
-    // ---- lane phase: frame `lane` -> record
-    if (!valid)
-      continue;
-    uint32_t flags = my_p0 & 0xffffu;
-    const uint32_t l3 = (my_p0 >> 16) & 0xffu, ver = my_p0 >> 24;
-    const uint32_t rs = my_p1 & 0xffffu, re = my_p1 >> 16;
-    const uint32_t et = my_p2 & 0xffffu, proto = my_p2 >> 16;
-    const int m = (int)(base & 15);
-    const FrameView v = {wimg + lane * IMG_STRIDE, a.frames + base, m, 16 * IMGC - m};
-
-    uint32_t w[16];
+    // ---- lane phase: frame `lane` -> record (parsed once per frame)
+    const bool stage = !(GATHER && a.perm) && !(a.tune & 2u);
+    // tune bit 4 (diagnostics only, output invalid): skip the lane phase
+    if (dc.idx != 0xffffffffu && !(a.tune & 16u)) {
+      const int m = (int)(dc.base & 15);
+      if (UNROLL) {  // unrolled variants: chunks past the staged S*T, summed here (rare)
+        const int ma = (int)(dc.base & ALM);
+        const int nch = (ma + (int)dc.len + 15) >> 4;
+        if (nch > S * T) {
+          const u32x4 *c0 = (const u32x4 *)(a.frames + (dc.base - (uint64_t)ma));
+          for (int c = S * T; c < nch; ++c)
+            my_sum = sum_chunk_from(ldc<NT>(c0 + c), 16 * c - ma, 0, (int)dc.len, my_sum);
+        }
+      }
+      const FrameView v = {wimg + lane * IMG_STRIDE, a.frames + dc.base, m, 16 * IMGC - m};
+      const Parse p = parse_frame(v, dc.len);
+      uint32_t flags = p.flags;
+      const uint32_t l3 = p.l3, rs = p.rs, re = p.re, proto = p.proto;
+      uint32_t w[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = 0;
-    uint64_t fh = 0;
-    if (flags & PPTK_RX_F_MALFORMED) {
-      flags &= PPTK_RX_F_MALFORMED | PPTK_RX_F_VLAN | PPTK_RX_F_IPV6;
-    } else if (flags & PPTK_RX_F_PARSED) {
-      const bool v6 = flags & PPTK_RX_F_IPV6;
-      uint32_t s0, s1 = 0, s2 = 0, s3 = 0, d0, d1 = 0, d2 = 0, d3 = 0;
-      uint32_t ipc = 0;
-      if (v6) {
-        s0 = v.le32(l3 + 8);  s1 = v.le32(l3 + 12); s2 = v.le32(l3 + 16); s3 = v.le32(l3 + 20);
-        d0 = v.le32(l3 + 24); d1 = v.le32(l3 + 28); d2 = v.le32(l3 + 32); d3 = v.le32(l3 + 36);
+      for (int k = 0; k < 16; ++k) w[k] = 0;
+      uint64_t fh = 0;
+      if (flags & PPTK_RX_F_MALFORMED) {
+        flags &= PPTK_RX_F_MALFORMED | PPTK_RX_F_VLAN | PPTK_RX_F_IPV6;
+      } else if (flags & PPTK_RX_F_PARSED) {
+        const bool v6 = flags & PPTK_RX_F_IPV6;
+        uint32_t s0, s1 = 0, s2 = 0, s3 = 0, d0, d1 = 0, d2 = 0, d3 = 0;
+        uint32_t ipc = 0;
+        if (v6) {
+          s0 = v.le32(l3 + 8);  s1 = v.le32(l3 + 12); s2 = v.le32(l3 + 16); s3 = v.le32(l3 + 20);
+          d0 = v.le32(l3 + 24); d1 = v.le32(l3 + 28); d2 = v.le32(l3 + 32); d3 = v.le32(l3 + 36);
+        } else {
+          s0 = v.le32(l3 + 12);
+          d0 = v.le32(l3 + 16);
+          // ip_hdr_cksum_calc over ihl = rs - l3 bytes (frame-relative pairing)
+          uint32_t hs = 0;
+          for (uint32_t k = l3; k < rs; k += 4)
+            hs = dot16(v.le32((int)k), hs);
+          ipc = finish16(hs);
+          if (ipc == 0)
+            flags |= PPTK_RX_F_IP_OK;
+        }
+        uint32_t ports = 0, l4c = 0;
+        if (flags & PPTK_RX_F_L4) {
+          ports = v.le32((int)rs);
+          const uint32_t l4len = re - rs;
+          uint32_t ps = dot16(s0, 0);
+          ps = dot16(s1, ps); ps = dot16(s2, ps); ps = dot16(s3, ps);
+          ps = dot16(d0, ps); ps = dot16(d1, ps); ps = dot16(d2, ps); ps = dot16(d3, ps);
+          ps += bswap16(proto) + bswap16(l4len);   // > 0: proto is 6 or 17
+          // region [rs, re) = [ts, len) - [ts, rs) - [re, len), mod 0xffff
+          const int ts = team_start_of(m);
+          uint32_t rsum = fold16(my_sum);
+          if ((int)rs > ts)
+            rsum += 0xffffu - fold16(sum_abs(v, ts, (int)rs));
+          if (re < dc.len)
+            rsum += 0xffffu - fold16(sum_abs(v, (int)re, (int)dc.len));
+          rsum = fold16(rsum);
+          if ((m + (int)rs) & 1)
+            rsum = bswap16(rsum);   // region starts at an odd address
+          l4c = finish16(ps + rsum);
+          if (l4c == 0)
+            flags |= PPTK_RX_F_L4_OK;
+          if (proto == 17 && (v.le32((int)rs + 4) >> 16) == 0)
+            flags |= PPTK_RX_F_UDP_ZERO;
+        }
+        Sip sh(a.k0, a.k1);
+        sh.block((uint64_t)s0 | ((uint64_t)s1 << 32));
+        sh.block((uint64_t)s2 | ((uint64_t)s3 << 32));
+        sh.block((uint64_t)d0 | ((uint64_t)d1 << 32));
+        sh.block((uint64_t)d2 | ((uint64_t)d3 << 32));
+        sh.block((uint64_t)ports | ((uint64_t)proto << 32));
+        fh = sh.finish(40ull << 56);
+        uint32_t bucket = 0;
+        if (!v6 && a.bucket4) {
+          const uint32_t host = __builtin_bswap32(s0) & a.mask4;
+          Sip bh(a.k0, a.k1);
+          bh.block((uint64_t)host);
+          bucket = (uint32_t)bh.finish(8ull << 56) & a.hash_mask;
+        } else if (v6 && a.bucket6) {
+          Sip bh(a.k0, a.k1);
+          bh.block(((uint64_t)s0 | ((uint64_t)s1 << 32)) & a.mask6_0);
+          bh.block(((uint64_t)s2 | ((uint64_t)s3 << 32)) & a.mask6_1);
+          bucket = (uint32_t)bh.finish(16ull << 56) & a.hash_mask;
+        }
+        w[0] = (uint32_t)fh;
+        w[1] = (uint32_t)(fh >> 32);
+        w[2] = s0; w[3] = s1; w[4] = s2; w[5] = s3;
+        w[6] = d0; w[7] = d1; w[8] = d2; w[9] = d3;
+        w[10] = bswap16(ports & 0xffffu) | (bswap16(ports >> 16) << 16);
+        w[11] = ipc | (l4c << 16);
+        w[12] = rs | ((re - rs) << 16);
+        w[13] = proto << 8;
+        w[14] = bucket;
+      }
+      w[13] |= l3 | (flags << 16);
+      w[15] = p.et | (p.ver << 16);
+      if (a.hash)
+        a.hash[dc.idx] = fh;
+      const u32x4 r0 = {w[0], w[1], w[2], w[3]}, r1 = {w[4], w[5], w[6], w[7]};
+      const u32x4 r2 = {w[8], w[9], w[10], w[11]}, r3 = {w[12], w[13], w[14], w[15]};
+      if (!stage) {  // permuted order: records scatter, store per lane
+        u32x4 *dst = (u32x4 *)((uint8_t *)a.recs + (uint64_t)dc.idx * 64u);
+        dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
       } else {
-        s0 = v.le32(l3 + 12);
-        d0 = v.le32(l3 + 16);
-        // ip_hdr_cksum_calc over ihl = rs - l3 bytes
-        uint32_t hs = 0;
-        for (uint32_t k = l3; k < rs; k += 4)
-          hs = dot16(v.le32((int)k), hs);
-        ipc = finish16(hs);
-        if (ipc == 0)
-          flags |= PPTK_RX_F_IP_OK;
+        // park the record in LDS (every lane's image reads are behind us in
+        // program order) for the coalesced store below
+        u32x4 *st = (u32x4 *)wimg + lane * 5;   // 80-byte pitch
+        st[0] = r0; st[1] = r1; st[2] = r2; st[3] = r3;
       }
-      uint32_t ports = 0, l4c = 0;
-      if (flags & PPTK_RX_F_L4) {
-        ports = v.le32((int)rs);
-        const uint32_t l4len = re - rs;
-        uint32_t ps = dot16(s0, 0);
-        ps = dot16(s1, ps); ps = dot16(s2, ps); ps = dot16(s3, ps);
-        ps = dot16(d0, ps); ps = dot16(d1, ps); ps = dot16(d2, ps); ps = dot16(d3, ps);
-        ps += bswap16(proto) + bswap16(l4len);
-        uint32_t rsum = fold16(my_sum);
-        if ((m + (int)rs) & 1)
-          rsum = bswap16(rsum);
-        l4c = finish16(ps + rsum);
-        if (l4c == 0)
-          flags |= PPTK_RX_F_L4_OK;
-        if (proto == 17 && (v.le32((int)rs + 4) >> 16) == 0)
-          flags |= PPTK_RX_F_UDP_ZERO;
-      }
-      Sip sh(a.k0, a.k1);
-      sh.block((uint64_t)s0 | ((uint64_t)s1 << 32));
-      sh.block((uint64_t)s2 | ((uint64_t)s3 << 32));
-      sh.block((uint64_t)d0 | ((uint64_t)d1 << 32));
-      sh.block((uint64_t)d2 | ((uint64_t)d3 << 32));
-      sh.block((uint64_t)ports | ((uint64_t)proto << 32));
-      fh = sh.finish(40ull << 56);
-      uint32_t bucket = 0;
-      if (!v6 && a.bucket4) {
-        const uint32_t host = __builtin_bswap32(s0) & a.mask4;
-        Sip bh(a.k0, a.k1);
-        bh.block((uint64_t)host);
-        bucket = (uint32_t)bh.finish(8ull << 56) & a.hash_mask;
-      } else if (v6 && a.bucket6) {
-        Sip bh(a.k0, a.k1);
-        bh.block(((uint64_t)s0 | ((uint64_t)s1 << 32)) & a.mask6_0);
-        bh.block(((uint64_t)s2 | ((uint64_t)s3 << 32)) & a.mask6_1);
-        bucket = (uint32_t)bh.finish(16ull << 56) & a.hash_mask;
-      }
-      w[0] = (uint32_t)fh;
-      w[1] = (uint32_t)(fh >> 32);
-      w[2] = s0; w[3] = s1; w[4] = s2; w[5] = s3;
-      w[6] = d0; w[7] = d1; w[8] = d2; w[9] = d3;
-      w[10] = bswap16(ports & 0xffffu) | (bswap16(ports >> 16) << 16);
-      w[11] = ipc | (l4c << 16);
-      w[12] = rs | ((re - rs) << 16);
-      w[13] = proto << 8;
-      w[14] = bucket;
     }
-    if (a.hash)
-      a.hash[idx] = fh;
-    w[13] |= l3 | (flags << 16);
-    w[15] = et | (ver << 16);
-    u32x4 *dst = (u32x4 *)((uint8_t *)a.recs + (uint64_t)idx * 64u);
-    dst[0] = (u32x4){w[0], w[1], w[2], w[3]};
-    dst[1] = (u32x4){w[4], w[5], w[6], w[7]};
-    dst[2] = (u32x4){w[8], w[9], w[10], w[11]};
-    dst[3] = (u32x4){w[12], w[13], w[14], w[15]};
+    if (stage && !(a.tune & 8u)) {   // tune bit 3 (diagnostics only): no record stores
+      // identity order: the tile's 64 records are one contiguous 4 KB run;
+      // each store instruction writes 1 KB contiguously instead of 64
+      // scattered 16-byte pieces
+      __builtin_amdgcn_wave_barrier();
+      const u32x4 *st = (const u32x4 *)wimg;
+      u32x4 *dst = (u32x4 *)((uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
+      const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
+      const int kmax = (a.tune & 128u) ? 2 : 4;   // bit 7: diagnostics, half the bytes
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = k * WAVE + lane;   // 16-byte piece e of the tile's records
+        const int r = e >> 2;
+        if ((uint64_t)r < nrec && k < kmax) {
+          const u32x4 val = st[r * 5 + (e & 3)];
+          if (a.tune & 64u) {            // bit 6: write-through, drop from L2 (sc1)
+            uint64_t *d8 = (uint64_t *)(dst + e);
+            __hip_atomic_store(d8, (uint64_t)val.x | ((uint64_t)val.y << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d8 + 1, (uint64_t)val.z | ((uint64_t)val.w << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          } else if (a.tune & 32u) {     // bit 5: non-temporal stores
+            asm volatile("" ::: "memory");
+            __builtin_nontemporal_store(val, dst + e);
+          } else {
+            dst[e] = val;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    tile += nwaves;
+    dc = dn;
+    dn = d2;
   }
 }
 
-template <int T, int S>
+template <int T, int S, int D, int AL>
 hipError_t launch_variant(const RxKArgs &a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((rx_kernel<T, S>), dim3(grid), dim3(WAVE * WPB), 0, s, a);
+  const dim3 gd(grid), bd(WAVE * WPB);
+  const bool nt = a.tune & 1u;
+  const bool gather = a.off || a.len || a.perm;
+  if (gather) {
+    if (nt) hipLaunchKernelGGL((rx_kernel<T, S, D, AL, true, true>), gd, bd, 0, s, a);
+    else hipLaunchKernelGGL((rx_kernel<T, S, D, AL, false, true>), gd, bd, 0, s, a);
+  } else {
+    if (nt) hipLaunchKernelGGL((rx_kernel<T, S, D, AL, true, false>), gd, bd, 0, s, a);
+    else hipLaunchKernelGGL((rx_kernel<T, S, D, AL, false, false>), gd, bd, 0, s, a);
+  }
   return hipGetLastError();
 }
 
-template <int T, int S>
+template <int T, int S, int D, int AL>
 int blocks_per_cu() {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<T, S>, WAVE * WPB, 0) !=
-      hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<T, S, D, AL, true, true>,
+                                                   WAVE * WPB, 0) != hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
 }
+
+// variant table: T, S, D, AL
+#define PPTK_RX_VARIANTS(X)       \
+  X(RX_T4S1, 4, 1, 3, 4)          \
+  X(RX_T4S2, 4, 2, 3, 4)          \
+  X(RX_T16S2, 16, 2, 3, 4)        \
+  X(RX_T16S6, 16, 6, 3, 4)        \
+  X(RX_T32S3, 32, 3, 3, 4)        \
+  X(RX_T64S2, 64, 2, 1, 4)        \
+  X(RX_T16S7L, 16, 7, 1, 7)       \
+  X(RX_T32S4L, 32, 4, 3, 7)       \
+  X(RX_T32S3D7, 32, 3, 7, 4)      \
+  X(RX_T16S6D1, 16, 6, 1, 4)
 
 }  // namespace
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s) {
   switch (variant) {
-    case RX_T4S1: return launch_variant<4, 1>(a, grid, s);
-    case RX_T4S2: return launch_variant<4, 2>(a, grid, s);
-    case RX_T16S2: return launch_variant<16, 2>(a, grid, s);
-    case RX_T16S6: return launch_variant<16, 6>(a, grid, s);
-    case RX_T64S2: return launch_variant<64, 2>(a, grid, s);
+#define X(name, T, S, D, AL) \
+  case name: return launch_variant<T, S, D, AL>(a, grid, s);
+    PPTK_RX_VARIANTS(X)
+#undef X
     default: return hipErrorInvalidValue;
   }
 }
 
 int rx_variant_blocks_per_cu(int variant) {
   switch (variant) {
-    case RX_T4S1: return blocks_per_cu<4, 1>();
-    case RX_T4S2: return blocks_per_cu<4, 2>();
-    case RX_T16S2: return blocks_per_cu<16, 2>();
-    case RX_T16S6: return blocks_per_cu<16, 6>();
-    case RX_T64S2: return blocks_per_cu<64, 2>();
+#define X(name, T, S, D, AL) \
+  case name: return blocks_per_cu<T, S, D, AL>();
+    PPTK_RX_VARIANTS(X)
+#undef X
     default: return 1;
   }
 }

@@ -11,7 +11,8 @@ import numpy as np
 
 from .records import REC_DTYPE
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpptkrx.so")
+LIB_PATH = os.environ.get("PPTK_RX_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libpptkrx.so")   # env: A/B builds
 
 
 class RxOpts(ctypes.Structure):
@@ -40,7 +41,8 @@ assert ctypes.sizeof(RxOpts) == 36
 
 EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_batch", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
-           "pptk_rx_bin_device", "pptk_rx_version",
+           "pptk_rx_bin_device", "pptk_rx_version", "pptk_rx_set_tuning",
+           "pptk_rx_variant_count",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
@@ -71,6 +73,9 @@ def lib():
         L.pptk_rx_bin_device.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp]
         L.pptk_rx_bin_device.restype = ctypes.c_int
         L.pptk_rx_version.restype = ctypes.c_char_p
+        L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.pptk_rx_set_tuning.restype = ctypes.c_int
+        L.pptk_rx_variant_count.restype = ctypes.c_int
         L.ip_hdr_cksum_calc.argtypes = [vp, ctypes.c_uint16]
         L.ip_hdr_cksum_calc.restype = ctypes.c_uint16
         for f in ("tcp_cksum_calc", "udp_cksum_calc", "tcp6_cksum_calc", "udp6_cksum_calc"):
@@ -105,6 +110,12 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_ctx_create failed ({rc})")
         self.device = device
+
+    def set_tuning(self, variant=-1, flags=-1):
+        """Force kernel variant / memory-policy flags (speed only; -1 = auto)."""
+        rc = lib().pptk_rx_set_tuning(self._ctx, variant, flags)
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_set_tuning({variant}, {flags}) failed")
 
     def close(self):
         if self._ctx:

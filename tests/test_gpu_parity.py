@@ -18,12 +18,12 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _ctx(z, bucket=True):
+def _ctx(z, bucket=True, max_frame=65535):
     from pptk_amd.rx import RxContext
     b4, b6, hs = (int(x) for x in z["iphash"])
     if not bucket:
         b4 = b6 = 0
-    return RxContext(0, z["key"].tobytes(), b4, b6, hs)
+    return RxContext(0, z["key"].tobytes(), b4, b6, hs, max_frame=max_frame)
 
 
 def _upload(buf, dev, shift=0):
@@ -78,6 +78,25 @@ def test_every_variant(name, max_len, dev):
     assert not d, d
 
 
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_every_forced_variant(name, dev):
+    """pptk_rx_set_tuning: every kernel variant, offsets and fixed-stride
+    layouts, aligned and misaligned buffers -- identical records."""
+    from pptk_amd.rx import lib
+    z = load_golden(name)
+    ctx = _ctx(z)
+    for v in range(lib().pptk_rx_variant_count()):
+        ctx.set_tuning(v, v % 4)
+        for shift in (0, 5):
+            got = _run(ctx, z, dev, shift=shift)
+            d = diff_records(got, z["recs"])
+            assert not d, f"variant {v} shift {shift}: {d}"
+        if name in ("c64", "c1500"):
+            got = _run(ctx, z, dev, shift=3, stride=64 if name == "c64" else 1500)
+            d = diff_records(got, z["recs"])
+            assert not d, f"variant {v} fixed stride: {d}"
+
+
 @pytest.mark.parametrize("name,stride", [("c64", 64), ("c1500", 1500)])
 @pytest.mark.parametrize("shift", [0, 4, 5, 13])
 def test_fixed_stride(name, stride, shift, dev):
@@ -125,6 +144,20 @@ def test_host_batch_ldp_packets(name, dev):
     d = diff_records(got, z["recs"])
     assert not d, d
     assert [p.ancillary64 for p in pkts] == ancillary_before
+
+
+def test_host_batch_max_frame(dev):
+    """Frames longer than opts.max_frame come back MALFORMED-only."""
+    from pptk_amd.records import F_MALFORMED
+    from pptk_amd.rx import ldp_packets
+    z = load_golden("edge")
+    ctx = _ctx(z, max_frame=1514)
+    buf = np.ascontiguousarray(z["buf"])
+    got = ctx.batch_host(ldp_packets(buf, z["off"], z["len"]))
+    long = z["len"] > 1514
+    assert long.any()
+    assert np.all(got["flags"][long] == F_MALFORMED)
+    assert not diff_records(got[~long], z["recs"][~long])
 
 
 def test_empty_and_single(dev):

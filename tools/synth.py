@@ -5,7 +5,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libpptksynth.so")
-CFG = {"c64": 0, "c1500": 1, "cmix": 2}
+CFG = {"c64": 0, "c1500": 1, "cmix": 2, "c1500a": 1}   # c1500a: 1536-byte slots
 SEED = 0x5EED
 
 _lib = None
@@ -33,13 +33,14 @@ def make_batch(cfg, n, device, first=0, seed=SEED, stream=None):
     sp = ctypes.c_void_p(s.cuda_stream)
     out = {"n": n, "cfg": cfg}
     expect = torch.empty(n, dtype=torch.uint8, device=device)
-    if cfg in ("c64", "c1500"):
-        stride = 64 if cfg == "c64" else 1500
+    if cfg in ("c64", "c1500", "c1500a"):
+        stride = {"c64": 64, "c1500": 1500, "c1500a": 1536}[cfg]
+        flen = 64 if cfg == "c64" else 1500
         frames = torch.empty(n * stride + 64, dtype=torch.uint8, device=device)
         rc = lib().synth_frames(c, seed, first, n, frames.data_ptr(), None, stride,
                                 expect.data_ptr(), sp)
-        out.update(frames=frames, stride=stride, fixed_len=stride, max_len=stride,
-                   bytes=n * stride)
+        out.update(frames=frames, stride=stride, fixed_len=flen, max_len=flen,
+                   bytes=n * flen)
     else:
         lens = torch.empty(n, dtype=torch.int16, device=device)
         rc = lib().synth_sizes(c, seed, first, n, lens.data_ptr(), sp)
