@@ -79,7 +79,7 @@ def sum_over_ranks(x, ws, dev):
     return float(t.item())
 
 
-def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check):
+def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=SETTLE_S):
     """Generate shard `rank` of config `cfg`, time `steps` launches."""
     import torch
     from pptk_amd.shard import allgather_flow_hash
@@ -117,7 +117,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check):
     # before the W warmup steps, so the K timed steps see steady state
     t_settle = time.perf_counter()
     k = 0
-    while time.perf_counter() - t_settle < SETTLE_S:
+    while time.perf_counter() - t_settle < settle:
         step(k)
         k += 1
         if k % 16 == 0:
@@ -270,8 +270,6 @@ def main():
     ap.add_argument("--settle", type=float, default=SETTLE_S,
                     help="seconds of untimed launches before the warmup steps")
     args = ap.parse_args()
-    global SETTLE_S
-    SETTLE_S = args.settle
 
     import torch
     from pptk_amd.rx import RxContext
@@ -281,11 +279,13 @@ def main():
     check = not args.no_check
 
     primary_cfg = args.only or "c1500"
-    prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, True, check)
+    prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, True, check,
+                      args.settle)
     log(f"[rank {rank}] {primary_cfg}: {prim['mpkts']:.1f} Mpkts/s, kernel {prim['kernel_ms']:.3f} ms")
     nog = None
     if ws > 1:
-        nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False)
+        nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False,
+                         args.settle)
 
     box = None
     if not args.no_membench:
@@ -314,7 +314,8 @@ def main():
     secondary = {}
     if not args.no_secondary and args.only is None:
         for cfg in ("c64", "cmix"):
-            r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check)
+            r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check,
+                           args.settle)
             ach = r["bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
             secondary[cfg] = {"value": round(r["mpkts"], 1), "unit": "Mpkts/s",
                               "kernel_ms": round(r["kernel_ms"], 4),

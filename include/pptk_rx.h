@@ -77,9 +77,9 @@ struct pptk_rx_opts {
   uint8_t key[16];      /* SipHash key (hash_seed in the reference)        */
   uint8_t iphash_bits4; /* ip_permitted prefix bits, 1..32; 0 = no bucket  */
   uint8_t iphash_bits6; /* ipv6_permitted prefix bits, 1..128; 0 = off     */
-  uint16_t pad0;
+  uint16_t gather_threads; /* host threads gathering staged frames (0 = 1) */
   uint32_t iphash_size; /* struct ip_hash.hash_size (power of two)         */
-  uint32_t max_batch;   /* largest num passed to pptk_rx_batch             */
+  uint32_t max_batch;   /* pptk_rx_batch chunk (frames per staged transfer) */
   uint32_t max_frame;   /* largest frame accepted by pptk_rx_batch (<=65535)*/
 };
 
@@ -89,12 +89,22 @@ int pptk_rx_ctx_create(struct pptk_rx_ctx **ctx, const struct pptk_rx_opts *opts
 void pptk_rx_ctx_destroy(struct pptk_rx_ctx *ctx);
 
 /* Host in -> host out.  Gathers the borrowed ldp_packet frames into pinned
- * staging, copies them to HBM, runs the transform and copies the records
- * back; synchronous: on return recs[0..num) are final and no pointer in pkts
- * is retained.  ancillary fields are neither read nor written.
- * Frames longer than opts.max_frame get PPTK_RX_F_MALFORMED only. */
+ * staging (or reads them in place from a registered ring, see below), copies
+ * them to HBM, runs the transform and copies the records back, in chunks of
+ * opts.max_batch frames double-buffered over two streams; synchronous: on
+ * return recs[0..num) are final and no pointer in pkts is retained.
+ * ancillary fields are neither read nor written.  Frames longer than
+ * opts.max_frame get PPTK_RX_F_MALFORMED only. */
 int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
                   int num, struct pptk_rx_rec *recs);
+
+/* Zero-copy rx rings: register a host region (e.g. a netmap ring's buffer
+ * area or a socket ring) once; pptk_rx_batch() calls whose frames all lie in
+ * one registered ring are read by the GPU in place over PCIe instead of
+ * being gathered into staging.  Every frame's end rounded up to 16 bytes
+ * must lie inside the region.  Unregister before freeing the memory. */
+int pptk_rx_register_ring(struct pptk_rx_ctx *ctx, void *base, size_t bytes);
+int pptk_rx_unregister_ring(struct pptk_rx_ctx *ctx, void *base);
 
 /* Device-resident batch (asynchronous on `stream`, a hipStream_t or NULL).
  * Frame i starts at d_frames + (d_off ? d_off[i] : i * stride) and is

@@ -11,6 +11,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
+#include <thread>
+#include <vector>
 
 #include "../../include/hashseed.h"
 #include "rx_internal.h"
@@ -23,6 +26,28 @@ constexpr uint32_t kStageAlign = 16;
 
 }  // namespace
 
+// One half of the host-batch double buffer: pinned staging, device copies,
+// and the chunk currently in flight on its stream.
+struct RxSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  size_t cap_pkts = 0, cap_bytes = 0;
+  uint8_t *h_frames = nullptr, *d_frames = nullptr;
+  uint64_t *h_off = nullptr, *d_off = nullptr;
+  uint16_t *h_len = nullptr, *d_len = nullptr;
+  pptk_rx_rec *h_recs = nullptr, *d_recs = nullptr;
+  pptk_rx_rec *out = nullptr;   // caller's records of the chunk in flight
+  size_t count = 0;
+  bool busy = false;
+};
+
+// A host rx ring registered for zero-copy reads (hipHostRegister, mapped).
+struct RxRing {
+  uint8_t *host;
+  size_t bytes;
+  const uint8_t *dev;
+};
+
 struct pptk_rx_ctx {
   int device = 0;
   pptk_rx_opts opts{};
@@ -31,13 +56,8 @@ struct pptk_rx_ctx {
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
   int forced_flags = -1;
-  // host-batch staging (pptk_rx_batch)
-  hipStream_t stream = nullptr;
-  size_t cap_pkts = 0, cap_bytes = 0;
-  uint8_t *h_frames = nullptr, *d_frames = nullptr;
-  uint64_t *h_off = nullptr, *d_off = nullptr;
-  uint16_t *h_len = nullptr, *d_len = nullptr;
-  pptk_rx_rec *h_recs = nullptr, *d_recs = nullptr;
+  RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch)
+  std::vector<RxRing> rings;
 };
 
 static int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -104,28 +124,31 @@ int pptk_rx_ctx_create(struct pptk_rx_ctx **out, const struct pptk_rx_opts *opts
   return 0;
 }
 
+static void free_slot(RxSlot &sl) {
+  if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+  if (sl.done) (void)hipEventDestroy(sl.done);
+  if (sl.stream) (void)hipStreamDestroy(sl.stream);
+  (void)hipHostFree(sl.h_frames);
+  (void)hipHostFree(sl.h_off);
+  (void)hipHostFree(sl.h_len);
+  (void)hipHostFree(sl.h_recs);
+  (void)hipFree(sl.d_frames);
+  (void)hipFree(sl.d_off);
+  (void)hipFree(sl.d_len);
+  (void)hipFree(sl.d_recs);
+  sl = RxSlot();
+}
+
 static void free_staging(pptk_rx_ctx *c) {
-  if (c->stream) (void)hipStreamDestroy(c->stream);
-  (void)hipHostFree(c->h_frames);
-  (void)hipHostFree(c->h_off);
-  (void)hipHostFree(c->h_len);
-  (void)hipHostFree(c->h_recs);
-  (void)hipFree(c->d_frames);
-  (void)hipFree(c->d_off);
-  (void)hipFree(c->d_len);
-  (void)hipFree(c->d_recs);
-  c->stream = nullptr;
-  c->h_frames = c->d_frames = nullptr;
-  c->h_off = c->d_off = nullptr;
-  c->h_len = c->d_len = nullptr;
-  c->h_recs = c->d_recs = nullptr;
-  c->cap_pkts = c->cap_bytes = 0;
+  free_slot(c->slot[0]);
+  free_slot(c->slot[1]);
 }
 
 void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   free_staging(c);
+  for (const RxRing &r : c->rings) (void)hipHostUnregister(r.host);
   delete c;
 }
 
@@ -227,27 +250,83 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *c, const uint16_t *d_len, uint64_t n,
   return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, 2048));
 }
 
-static int ensure_staging(pptk_rx_ctx *c, size_t pkts, size_t bytes) {
-  if (pkts <= c->cap_pkts && bytes <= c->cap_bytes) return 0;
-  free_staging(c);
+static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {
+  if (sl.stream && pkts <= sl.cap_pkts && bytes <= sl.cap_bytes) return 0;
+  free_slot(sl);
   pkts = std::max(pkts, (size_t)c->opts.max_batch);
-  bytes = std::max(bytes, (size_t)c->opts.max_batch * ((c->opts.max_frame + 15) & ~15u));
-  bytes += 64;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void **)&c->h_frames, bytes, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void **)&c->h_off, pkts * 8, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void **)&c->h_len, pkts * 2, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void **)&c->h_recs, pkts * 64, hipHostMallocDefault) != hipSuccess ||
-      hipMalloc((void **)&c->d_frames, bytes) != hipSuccess ||
-      hipMalloc((void **)&c->d_off, pkts * 8) != hipSuccess ||
-      hipMalloc((void **)&c->d_len, pkts * 2) != hipSuccess ||
-      hipMalloc((void **)&c->d_recs, pkts * 64) != hipSuccess) {
-    free_staging(c);
+  bytes = std::max(bytes, (size_t)c->opts.max_batch * ((c->opts.max_frame + 15) & ~15u)) + 64;
+  if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc((void **)&sl.h_frames, bytes, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&sl.h_off, pkts * 8, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&sl.h_len, pkts * 2, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&sl.h_recs, pkts * 64, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void **)&sl.d_frames, bytes) != hipSuccess ||
+      hipMalloc((void **)&sl.d_off, pkts * 8) != hipSuccess ||
+      hipMalloc((void **)&sl.d_len, pkts * 2) != hipSuccess ||
+      hipMalloc((void **)&sl.d_recs, pkts * 64) != hipSuccess) {
+    free_slot(sl);
     return -ENOMEM;
   }
-  c->cap_pkts = pkts;
-  c->cap_bytes = bytes;
+  sl.cap_pkts = pkts;
+  sl.cap_bytes = bytes;
   return 0;
+}
+
+// Wait for the slot's chunk and hand its records to the caller.
+static int retire(RxSlot &sl) {
+  if (!sl.busy) return 0;
+  sl.busy = false;
+  if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
+  memcpy(sl.out, sl.h_recs, sl.count * 64);
+  return 0;
+}
+
+// The registered ring holding every frame of pkts[0, num), so that frame
+// bytes can be read in place (the kernel reads whole 16-byte chunks, so each
+// frame's chunk-rounded end must lie inside the ring too); NULL otherwise.
+static const RxRing *ring_of(const pptk_rx_ctx *c, const struct ldp_packet *pkts, int num) {
+  if (c->rings.empty() || num <= 0) return nullptr;
+  const uint8_t *p0 = (const uint8_t *)pkts[0].data;
+  for (const RxRing &r : c->rings) {
+    if (p0 < r.host || p0 >= r.host + r.bytes) continue;
+    for (int i = 0; i < num; ++i) {
+      const uint8_t *p = (const uint8_t *)pkts[i].data;
+      if (!p || p < r.host) return nullptr;
+      const size_t off = (size_t)(p - r.host);
+      if (((off + pkts[i].sz + 15) & ~(size_t)15) > r.bytes) return nullptr;
+    }
+    return &r;
+  }
+  return nullptr;
+}
+
+int pptk_rx_register_ring(struct pptk_rx_ctx *c, void *base, size_t bytes) {
+  if (!c || !base || bytes == 0) return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  if (hipHostRegister(base, bytes, hipHostRegisterMapped) != hipSuccess) return -EIO;
+  void *dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
+    (void)hipHostUnregister(base);
+    return -EIO;
+  }
+  c->rings.push_back(RxRing{(uint8_t *)base, bytes, (const uint8_t *)dev});
+  return 0;
+}
+
+int pptk_rx_unregister_ring(struct pptk_rx_ctx *c, void *base) {
+  if (!c || !base) return -EINVAL;
+  for (size_t i = 0; i < c->rings.size(); ++i) {
+    if (c->rings[i].host == (uint8_t *)base) {
+      if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+      for (RxSlot &sl : c->slot)   // no chunk may still read the ring
+        if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+      (void)hipHostUnregister(base);
+      c->rings.erase(c->rings.begin() + (long)i);
+      return 0;
+    }
+  }
+  return -EINVAL;
 }
 
 int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
@@ -256,47 +335,88 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   if (num == 0) return 0;
   if (hipSetDevice(c->device) != hipSuccess) return -EIO;
   const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
-  // gather: frames packed at 16-byte aligned offsets; over-long frames are
-  // staged with length 0, which yields a MALFORMED-only record.
-  size_t bytes = 0;
-  for (int i = 0; i < num; ++i)
-    if (pkts[i].data && pkts[i].sz <= maxf)
-      bytes += (pkts[i].sz + kStageAlign - 1) & ~(size_t)(kStageAlign - 1);
-  int rc = ensure_staging(c, (size_t)num, bytes);
-  if (rc) return rc;
-  size_t pos = 0;
-  uint32_t maxlen = 0;
-  for (int i = 0; i < num; ++i) {
-    const bool ok = pkts[i].data && pkts[i].sz <= maxf;
-    const uint32_t sz = ok ? pkts[i].sz : 0u;
-    c->h_off[i] = pos;
-    c->h_len[i] = (uint16_t)sz;
-    if (sz) memcpy(c->h_frames + pos, pkts[i].data, sz);
-    pos += (sz + kStageAlign - 1) & ~(size_t)(kStageAlign - 1);
-    maxlen = std::max(maxlen, sz);
+  const RxRing *ring = ring_of(c, pkts, num);
+  const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
+  const size_t chunk_bytes = chunk * ((maxf + 15) & ~15u);
+  int rc = 0;
+  // Double-buffered: while chunk k runs on one slot's stream (H2D, kernel,
+  // D2H), the host gathers chunk k+1 into the other slot.  In a registered
+  // ring the kernel reads the frames in place over PCIe and only the 10-byte
+  // descriptors go down.
+  size_t k = 0;
+  for (size_t first = 0; first < (size_t)num && rc == 0; first += chunk, ++k) {
+    RxSlot &sl = c->slot[k & 1];
+    if ((rc = retire(sl)) != 0) break;
+    const size_t cnt = std::min(chunk, (size_t)num - first);
+    if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes)) != 0) break;
+    // descriptors (and staging offsets) first, serially; then the frame
+    // bytes, split over opts.gather_threads threads (the host memcpy is the
+    // staged path's bottleneck, see DESIGN.md "End-to-end")
+    size_t pos = 0;
+    uint32_t maxlen = 0;
+    for (size_t i = 0; i < cnt; ++i) {
+      const struct ldp_packet &pk = pkts[first + i];
+      const bool ok = pk.data && pk.sz <= maxf;
+      const uint32_t sz = ok ? pk.sz : 0u;
+      sl.h_len[i] = (uint16_t)sz;
+      if (ring) {
+        sl.h_off[i] = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
+      } else {
+        sl.h_off[i] = pos;
+        pos += (sz + 15) & ~(size_t)15;
+      }
+      maxlen = std::max(maxlen, sz);
+    }
+    if (!ring) {
+      const struct ldp_packet *cp = pkts + first;
+      auto gather = [&sl, cp](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i)
+          if (sl.h_len[i]) memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
+      };
+      const size_t nth = std::max<size_t>(1, std::min<size_t>(c->opts.gather_threads, 64));
+      if (nth == 1 || cnt < 1024) {
+        gather(0, cnt);
+      } else {
+        std::vector<std::thread> th;
+        th.reserve(nth - 1);
+        for (size_t t = 1; t < nth; ++t)
+          th.emplace_back(gather, cnt * t / nth, cnt * (t + 1) / nth);
+        gather(0, cnt / nth);
+        for (std::thread &x : th) x.join();
+      }
+    }
+    hipStream_t s = sl.stream;
+    if ((!ring && hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
+                                 hipMemcpyHostToDevice, s) != hipSuccess) ||
+        hipMemcpyAsync(sl.d_off, sl.h_off, cnt * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(sl.d_len, sl.h_len, cnt * 2, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    pptk_rx_dev_batch b;
+    memset(&b, 0, sizeof(b));
+    b.d_frames = ring ? ring->dev : sl.d_frames;
+    b.d_off = sl.d_off;
+    b.d_len = sl.d_len;
+    b.max_len = maxlen;
+    b.n = cnt;
+    b.d_recs = sl.d_recs;
+    if ((rc = pptk_rx_batch_device(c, &b, s)) != 0) break;
+    if (hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipEventRecord(sl.done, s) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    sl.out = recs + first;
+    sl.count = cnt;
+    sl.busy = true;
   }
-  hipStream_t s = c->stream;
-  if (hipMemcpyAsync(c->d_frames, c->h_frames, std::max<size_t>(pos, 16), hipMemcpyHostToDevice, s) !=
-          hipSuccess ||
-      hipMemcpyAsync(c->d_off, c->h_off, (size_t)num * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(c->d_len, c->h_len, (size_t)num * 2, hipMemcpyHostToDevice, s) != hipSuccess)
-    return -EIO;
-  pptk_rx_dev_batch b;
-  memset(&b, 0, sizeof(b));
-  b.d_frames = c->d_frames;
-  b.d_off = c->d_off;
-  b.d_len = c->d_len;
-  b.max_len = maxlen;
-  b.n = (uint64_t)num;
-  b.d_recs = c->d_recs;
-  rc = pptk_rx_batch_device(c, &b, s);
-  if (rc) return rc;
-  if (hipMemcpyAsync(c->h_recs, c->d_recs, (size_t)num * 64, hipMemcpyDeviceToHost, s) !=
-          hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return -EIO;
-  memcpy(recs, c->h_recs, (size_t)num * 64);
-  return 0;
+  // drain (also on error: nothing may still read the caller's buffers)
+  for (RxSlot &sl : c->slot) {
+    const int r2 = retire(sl);
+    if (rc == 0) rc = r2;
+  }
+  return rc;
 }
 
 }  // extern "C"

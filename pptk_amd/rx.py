@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("PPTK_RX_LIB") or os.path.join(
 class RxOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("key", ctypes.c_uint8 * 16),
                 ("iphash_bits4", ctypes.c_uint8), ("iphash_bits6", ctypes.c_uint8),
-                ("pad0", ctypes.c_uint16), ("iphash_size", ctypes.c_uint32),
+                ("gather_threads", ctypes.c_uint16), ("iphash_size", ctypes.c_uint32),
                 ("max_batch", ctypes.c_uint32), ("max_frame", ctypes.c_uint32)]
 
 
@@ -42,7 +42,7 @@ assert ctypes.sizeof(RxOpts) == 36
 EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_batch", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
            "pptk_rx_bin_device", "pptk_rx_version", "pptk_rx_set_tuning",
-           "pptk_rx_variant_count",
+           "pptk_rx_variant_count", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
@@ -76,6 +76,10 @@ def lib():
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
         L.pptk_rx_variant_count.restype = ctypes.c_int
+        L.pptk_rx_register_ring.argtypes = [vp, vp, ctypes.c_size_t]
+        L.pptk_rx_register_ring.restype = ctypes.c_int
+        L.pptk_rx_unregister_ring.argtypes = [vp, vp]
+        L.pptk_rx_unregister_ring.restype = ctypes.c_int
         L.ip_hdr_cksum_calc.argtypes = [vp, ctypes.c_uint16]
         L.ip_hdr_cksum_calc.restype = ctypes.c_uint16
         for f in ("tcp_cksum_calc", "udp_cksum_calc", "tcp6_cksum_calc", "udp6_cksum_calc"):
@@ -96,7 +100,7 @@ class RxContext:
     """One pptk_rx_ctx (one per rx thread in a C application)."""
 
     def __init__(self, device=0, key=bytes(16), iphash_bits4=0, iphash_bits6=0,
-                 iphash_size=1, max_batch=8192, max_frame=9216):
+                 iphash_size=1, max_batch=8192, max_frame=9216, gather_threads=1):
         L = lib()
         o = RxOpts()
         L.pptk_rx_opts_default(ctypes.byref(o))
@@ -104,7 +108,7 @@ class RxContext:
         for i, b in enumerate(bytes(key)):
             o.key[i] = b
         o.iphash_bits4, o.iphash_bits6, o.iphash_size = iphash_bits4, iphash_bits6, iphash_size
-        o.max_batch, o.max_frame = max_batch, max_frame
+        o.max_batch, o.max_frame, o.gather_threads = max_batch, max_frame, gather_threads
         self._ctx = ctypes.c_void_p()
         rc = L.pptk_rx_ctx_create(ctypes.byref(self._ctx), ctypes.byref(o))
         if rc != 0:
@@ -159,6 +163,17 @@ class RxContext:
             raise OSError(-rc, f"pptk_rx_bin_device failed ({rc})")
         return perm
 
+    def register_ring(self, buf):
+        """Register numpy buffer `buf` as a zero-copy rx ring."""
+        rc = lib().pptk_rx_register_ring(self._ctx, ctypes.c_void_p(buf.ctypes.data), buf.nbytes)
+        if rc != 0:
+            raise OSError(-rc, "pptk_rx_register_ring failed")
+
+    def unregister_ring(self, buf):
+        rc = lib().pptk_rx_unregister_ring(self._ctx, ctypes.c_void_p(buf.ctypes.data))
+        if rc != 0:
+            raise OSError(-rc, "pptk_rx_unregister_ring failed")
+
     def batch_host(self, pkts):
         """pptk_rx_batch over a ctypes array of LdpPacket; returns records."""
         n = len(pkts)
@@ -170,14 +185,18 @@ class RxContext:
         return recs
 
 
+LDP_PACKET_DTYPE = np.dtype([("data", "<u8"), ("sz", "<u4"), ("pad", "<u4"),
+                             ("ancillary64", "<u8")])
+
+
 def ldp_packets(buf, off, lens):
     """Build an LdpPacket array pointing into numpy buffer `buf` (kept alive
     by the caller), as ldp_in_nextpkts() would hand out."""
     n = len(off)
-    arr = (LdpPacket * n)()
-    base = buf.ctypes.data
-    for i in range(n):
-        arr[i].data = base + int(off[i])
-        arr[i].sz = int(lens[i])
-        arr[i].ancillary64 = i
+    a = np.zeros(n, dtype=LDP_PACKET_DTYPE)
+    a["data"] = buf.ctypes.data + np.asarray(off, dtype=np.uint64)
+    a["sz"] = np.asarray(lens, dtype=np.uint32)
+    a["ancillary64"] = np.arange(n, dtype=np.uint64)
+    arr = (LdpPacket * n).from_buffer(a)
+    arr._keep = a
     return arr

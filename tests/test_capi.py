@@ -6,6 +6,7 @@ import glob
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -133,3 +134,15 @@ def test_record_layout_matches_header():
         off = REC_DTYPE.fields[name][1]
         m = re.search(rf"\b{name}(\[\d+\])?;\s*/\*\s*(\d+)", txt)
         assert m and int(m.group(2)) == off, name
+
+
+def test_bench_and_tools_compile():
+    """bench.py and the tooling must at least compile on CPU (the GPU box's
+    interpreter rejects what the local parser might let through)."""
+    import py_compile
+    for f in ("bench.py", "__graft_entry__.py", "tools/ab.py", "tools/e2e.py",
+              "tools/membench.py", "tools/synth.py", "tools/pmc_summary.py"):
+        py_compile.compile(os.path.join(ROOT, f), doraise=True)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "--steps" in out.stdout

@@ -146,6 +146,46 @@ def test_host_batch_ldp_packets(name, dev):
     assert [p.ancillary64 for p in pkts] == ancillary_before
 
 
+@pytest.mark.parametrize("max_batch,threads", [(97, 1), (4096, 1), (1500, 6)])
+@pytest.mark.parametrize("name", ["fuzz", "cmix"])
+def test_host_batch_chunked_and_ring(name, max_batch, threads, dev):
+    """pptk_rx_batch in chunks of max_batch (double-buffered pipeline), from
+    staging and from a registered zero-copy ring; then unregistered."""
+    from pptk_amd.rx import RxContext, ldp_packets
+    z = load_golden(name)
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_batch=max_batch, max_frame=65535,
+                    gather_threads=threads)
+    ring = np.zeros(z["buf"].size + 4096, dtype=np.uint8)
+    ring[:z["buf"].size] = z["buf"]
+    pkts = ldp_packets(ring, z["off"], z["len"])
+    d = diff_records(ctx.batch_host(pkts), z["recs"])
+    assert not d, "staged: " + d
+    ctx.register_ring(ring)
+    d = diff_records(ctx.batch_host(pkts), z["recs"])
+    assert not d, "ring: " + d
+    ctx.unregister_ring(ring)
+    d = diff_records(ctx.batch_host(pkts), z["recs"])
+    assert not d, "after unregister: " + d
+
+
+def test_ring_edge_falls_back(dev):
+    """A frame whose 16-byte-rounded end leaves the registered region makes
+    the batch use staging; results stay exact."""
+    from pptk_amd.rx import RxContext, ldp_packets
+    z = load_golden("edge")
+    i = int(np.argmax(z["len"] % 16 == 7))
+    fr = z["buf"][int(z["off"][i]):int(z["off"][i]) + int(z["len"][i])]
+    ring = np.zeros(int(z["len"][i]) + 3, dtype=np.uint8)   # end not 16-rounded
+    ring[:fr.size] = fr
+    ctx = _ctx(z)
+    ctx.register_ring(ring)
+    got = ctx.batch_host(ldp_packets(ring, [0], [fr.size]))
+    d = diff_records(got, z["recs"][i:i + 1])
+    assert not d, d
+    ctx.unregister_ring(ring)
+
+
 def test_host_batch_max_frame(dev):
     """Frames longer than opts.max_frame come back MALFORMED-only."""
     from pptk_amd.records import F_MALFORMED

@@ -1,0 +1,64 @@
+"""BENCH TOOLING: end-to-end host-to-host rate of pptk_rx_batch (the LDP rx
+loop's view: borrowed frames in host memory -> records in host memory),
+for the staged path (pinned gather + H2D) and the zero-copy registered-ring
+path (GPU reads the frames in place over PCIe).
+
+    python tools/e2e.py [frames] [chunk]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from pptk_amd.records import diff_records
+    from pptk_amd.rx import RxContext, ldp_packets
+    from tools.synth import make_batch
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+    dev = torch.device("cuda", 0)
+    out = {"frames": n, "chunk": chunk}
+    for cfg in ("c1500", "c64"):
+        b = make_batch(cfg, n, dev)
+        stride = b["stride"]
+        ring = b["frames"][: n * stride + 64].cpu().numpy()     # pageable host "ring"
+        ref = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        gt = int(os.environ.get("E2E_GATHER_THREADS", "8"))
+        ctx = RxContext(0, bytes(range(1, 17)), max_batch=chunk, max_frame=1518,
+                        gather_threads=gt)
+        out["gather_threads"] = gt
+        ctx.batch_device(b["frames"], n, stride=stride, fixed_len=b["fixed_len"], recs=ref)
+        want = ref.cpu().numpy()
+        pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
+                           np.full(n, b["fixed_len"], np.uint16))
+        res = {}
+        for mode in ("staged", "ring"):
+            if mode == "ring":
+                ctx.register_ring(ring)
+            got = ctx.batch_host(pkts)          # warm-up (allocations)
+            assert not diff_records(got, want), f"{cfg} {mode} parity"
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < 3.0:
+                ctx.batch_host(pkts)
+                reps += 1
+            el = (time.perf_counter() - t0) / reps
+            res[mode] = {"mpkts": round(n / el / 1e6, 2),
+                         "frame_gbs": round(n * b["fixed_len"] / el / 1e9, 2),
+                         "ms_per_batch": round(el * 1e3, 2)}
+            if mode == "ring":
+                ctx.unregister_ring(ring)
+        out[cfg] = res
+        del b, ref
+        torch.cuda.empty_cache()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
