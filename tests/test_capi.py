@@ -146,3 +146,26 @@ def test_bench_and_tools_compile():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and "--steps" in out.stdout
+
+
+def _build_rx_loop(tmp_path):
+    exe = str(tmp_path / "rx_loop")
+    libdir = os.path.join(ROOT, "pptk_amd")
+    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Werror",
+                           "-I", INCLUDE, os.path.join(ROOT, "examples", "rx_loop.c"),
+                           "-L", libdir, "-lpptkrx", f"-Wl,-rpath,{libdir}", "-o", exe])
+    return exe
+
+
+def test_example_rx_loop_builds(tmp_path):
+    """examples/rx_loop.c (the INTEGRATION.md walk-through) builds with gcc."""
+    _build_rx_loop(tmp_path)
+
+
+@pytest.mark.gpu
+def test_example_rx_loop_runs(tmp_path):
+    """The LDP-style rx loop verifies every frame but the one it corrupted."""
+    out = subprocess.run([_build_rx_loop(tmp_path), "20"], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "20000 frames" in out.stdout and "19995 verified, 5 failed" in out.stdout
