@@ -88,11 +88,17 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     torch.cuda.synchronize(dev)
     recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)] if (gather and ws > 1) else None
-    perm = None
-    kw = {}
-    if "off" in b:
-        kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
-        perm = ctx.bin_device(b["lens"], n)        # length binning (part of setup)
+    mixed = "off" in b
+    if mixed:
+        # mixed sizes: device length binning + one launch per length group,
+        # all inside the timed step (pptk_rx_batch_device_mixed)
+        import ctypes
+        from pptk_amd.rx import lib as rxlib
+        perm_buf = torch.empty(n, dtype=torch.int32, device=dev)
+        scratch = torch.empty(rxlib().pptk_rx_bin_scratch_bytes(ctypes.c_uint64(n)),
+                              dtype=torch.uint8, device=dev)
+        kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"], perm=perm_buf,
+                  scratch=scratch)
     else:
         kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
     gout = None
@@ -105,7 +111,10 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
         # the dense flow-hash array only feeds the all-gather (N > 1); at
         # N = 1 the records (which carry flow_hash) are the whole output
         h = hbuf[k & 1] if gout is not None else None
-        ctx.batch_device(b["frames"], n, perm=perm, recs=recs, hash_out=h, **kw)
+        if mixed:
+            ctx.batch_device_mixed(b["frames"], n, recs=recs, hash_out=h, **kw)
+        else:
+            ctx.batch_device(b["frames"], n, recs=recs, hash_out=h, **kw)
         if gout is not None:
             if work[0] is not None:
                 work[0].wait()                  # previous gather done before reuse
@@ -197,46 +206,102 @@ def oracle_sample(b, recs, n, dev, k=4096):
     return {"frames": int(len(idx)), "mismatches": 0 if not d else int(d.split()[0])}
 
 
-def cpu_baseline(b, seconds=10.0, sample=262144):
-    """PPTK's CPU path on this host's cores over a sample of the same C1500
-    batch: the reference's own functions when oracle/_ref was built, else
-    the C restatement."""
-    from oracle.oracle import REF_SO, Oracle, Reference, make_opts
-    n = min(sample, b["n"])
-    host = b["frames"][: n * b["stride"]].cpu().numpy()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    kind = "reference" if os.path.exists(REF_SO) else "port"
-    lib = Reference() if kind == "reference" else Oracle()
-    opts = make_opts(KEY)
-    kw = {"with_bucket": False} if kind == "reference" else {}
-
-    def timed(nth):
-        done, t0 = 0, time.perf_counter()
-        while True:
-            lib.rx_batch(host, None, None, stride=b["stride"], fixed_len=b["fixed_len"],
-                         n=n, opts=opts, nthreads=nth, **kw)
-            done += n
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                return done / el / 1e6, el
-
-    mt, el_mt = timed(threads)
-    st, el_st = timed(1) if seconds >= 1 else (None, 0)
-    cpu = "unknown"
+def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
+    return "unknown"
+
+
+def _cpu_lib():
+    from oracle.oracle import REF_SO, Oracle, Reference
+    kind = "reference" if os.path.exists(REF_SO) else "port"
+    lib = Reference() if kind == "reference" else Oracle()
+    kw = {"with_bucket": False} if kind == "reference" else {}
+    return kind, lib, kw
+
+
+def _cpu_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+
+
+def _cpu_rate(b, n, nth, seconds):
+    """Mpkts/s of the CPU full path over the first n frames of batch b."""
+    from oracle.oracle import make_opts
+    kind, lib, kw = _cpu_lib()
+    host = b["frames"][: n * b["stride"]].cpu().numpy()
+    opts = make_opts(KEY)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        lib.rx_batch(host, None, None, stride=b["stride"], fixed_len=b["fixed_len"],
+                     n=n, opts=opts, nthreads=nth, **kw)
+        done += n
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return done / el / 1e6, el
+
+
+def cpu_baseline(b, seconds=10.0, sample=262144):
+    """PPTK's CPU path on this host's cores over a sample of the
+    same C1500 batch: the reference's own functions when oracle/_ref was
+    built, else the C restatement.  Full path on all threads (the value) and
+    on one thread, plus ipcksumperf semantics (iphdr/ipcksumperf.c:21-29:
+    ip_cksum_feed over one 1500 B buffer, one thread, Gbit/s)."""
+    kind, lib, _ = _cpu_lib()
+    n = min(sample, b["n"])
+    threads = _cpu_threads()
+    mt, el_mt = _cpu_rate(b, n, threads, seconds)
+    st, _ = _cpu_rate(b, n, 1, seconds / 2) if seconds >= 1 else (None, 0)
+    one = b["frames"][: b["stride"]].cpu().numpy()
+    iters, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min(2.0, seconds / 4):
+        lib.cksum_loop(one, 200000)
+        iters += 200000
+    gbps = iters * one.size * 8 / (time.perf_counter() - t0) / 1e9
     return {"value": round(mt, 3), "unit": "Mpkts/s", "cores": threads, "kind": kind,
             "sample": f"{n} distinct C1500 frames (1500 B IPv4/TCP) from the same batch, "
                       f"full path (IPv4 hdr cksum + TCP cksum + parse + 40 B SipHash), "
                       f"repeated for {el_mt:.1f} s on {threads} threads",
             "single_thread_mpkts": None if st is None else round(st, 3),
-            "cpu_model": cpu}
+            "ipcksumperf_gbps_1thread": round(gbps, 2),
+            "cpu_model": _cpu_model()}
+
+
+def cpu_baseline_small(b, seconds=4.0, sample=1 << 20):
+    """The same CPU full path over a sample of the C64 batch."""
+    kind, _, _ = _cpu_lib()
+    n = min(sample, b["n"])
+    threads = _cpu_threads()
+    mt, el = _cpu_rate(b, n, threads, seconds)
+    st, _ = _cpu_rate(b, n, 1, seconds / 2)
+    return {"value": round(mt, 3), "unit": "Mpkts/s", "cores": threads, "kind": kind,
+            "sample": f"{n} distinct C64 frames (64 B IPv4/UDP), full path, "
+                      f"repeated for {el:.1f} s on {threads} threads",
+            "single_thread_mpkts": round(st, 3)}
+
+
+def gather_bench(n, ws, dev, steps):
+    """All-gather of n u64 flow hashes per rank alone: time,
+    algorithmic and bus bandwidth (RCCL convention: bus = alg * (ws-1)/ws)."""
+    import torch
+    from pptk_amd.shard import allgather_flow_hash
+    h = torch.zeros(n, dtype=torch.int64, device=dev)
+    out = torch.empty(n * ws, dtype=torch.int64, device=dev)
+    for _ in range(3):
+        allgather_flow_hash(h, out)
+    barrier(ws, dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        allgather_flow_hash(h, out)
+    barrier(ws, dev)
+    t = max_over_ranks((time.perf_counter() - t0) / steps, ws, dev)
+    alg = n * ws * 8 / t / 1e9
+    return {"bytes_per_rank": n * 8, "ms": round(t * 1e3, 4), "algbw_gbs": round(alg, 1),
+            "busbw_gbs": round(alg * (ws - 1) / ws, 1)}
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
@@ -259,7 +324,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=N_PER_GPU, help="frames per GPU")
+    ap.add_argument("--frames", type=int, default=N_PER_GPU,
+                    help="frames per GPU (weak) or in total (strong)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: --frames per GPU; strong: --frames split over the GPUs")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
@@ -275,17 +343,27 @@ def main():
     from pptk_amd.rx import RxContext
     ws, rank, dev = dist_setup(args.gpus)
     ctx = RxContext(dev.index, KEY)
-    n = args.frames
+    if args.scaling == "strong":
+        if args.frames % ws:
+            raise SystemExit(f"--frames {args.frames} not divisible by {ws} GPUs")
+        n = args.frames // ws          # equal shards: the all-gather needs them
+    else:
+        n = args.frames
     check = not args.no_check
 
     primary_cfg = args.only or "c1500"
     prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, True, check,
                       args.settle)
     log(f"[rank {rank}] {primary_cfg}: {prim['mpkts']:.1f} Mpkts/s, kernel {prim['kernel_ms']:.3f} ms")
-    nog = None
+    nog = gat = None
     if ws > 1:
+        # same launches without the collective: the kernel-only duration the
+        # roofline uses, and the rate "without the gather" 
         nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False,
                          args.settle)
+        del nog["_batch"], nog["_recs"]
+        gat = gather_bench(n, ws, dev, args.steps)
+        log(f"[rank {rank}] no gather: {nog['mpkts']:.1f} Mpkts/s; all-gather {gat}")
 
     box = None
     if not args.no_membench:
@@ -294,13 +372,17 @@ def main():
         log(f"[rank {rank}] box HBM: {box}")
 
     bytes_per_launch = prim["bytes"]
-    achieved = bytes_per_launch / (prim["kernel_ms"] * 1e-3) / 1e9
+    # with N > 1 the primary run's event pair also spans the wait on the
+    # previous batch's gather, so the kernel duration comes from the run
+    # without the collective
+    kernel_ms = (nog or prim)["kernel_ms"]
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(primary_cfg)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_source": tsrc,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
-                "kernel_ms": round(prim["kernel_ms"], 4)}
+                "kernel_ms": round(kernel_ms, 4)}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu and primary_cfg == "c1500":
@@ -325,6 +407,9 @@ def main():
                                            "frac": round(ach / HBM_PEAK_GBS, 4)},
                               "full_batch_check": r.get("full_batch_check"),
                               "oracle_sample": r.get("oracle_sample")}
+            if cfg == "c64" and rank == 0 and ws == 1 and not args.no_cpu:
+                secondary[cfg]["cpu_baseline"] = cpu_baseline_small(
+                    r["_batch"], seconds=max(1.0, args.cpu_seconds / 2.5))
             del r["_batch"], r["_recs"]
             torch.cuda.empty_cache()
 
@@ -338,7 +423,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(prim["ms_per_step"], 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
@@ -350,6 +435,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "value_no_gather": None if nog is None else round(nog["mpkts"], 1),
+            "allgather": gat,
             "box_hbm": box,
             "parity": {"full_batch": full_check, "oracle_sample": sample_check},
             "secondary": secondary,

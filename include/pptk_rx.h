@@ -132,13 +132,27 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *ctx,
                          const struct pptk_rx_dev_batch *b, void *stream);
 
 /* Length binning for mixed-size batches: writes into d_perm a stable
- * permutation of 0..n-1 ordered by ceil(len/256), so the lanes of one
- * wavefront sum frames of similar length.  d_scratch must hold
+ * permutation of 0..n-1 ordered by length group (the groups of
+ * pptk_rx_batch_device_mixed), so the lanes of one wavefront sum frames of
+ * similar length.  d_scratch must hold
  * pptk_rx_bin_scratch_bytes(n) bytes.  Asynchronous on `stream`. */
 size_t pptk_rx_bin_scratch_bytes(uint64_t n);
 int pptk_rx_bin_device(struct pptk_rx_ctx *ctx, const uint16_t *d_len,
                        uint64_t n, uint32_t *d_perm, void *d_scratch,
                        void *stream);
+
+/* Mixed-size batch in one call: pptk_rx_bin_device() into d_perm/d_scratch,
+ * then one launch per length group (64..113, ..241, ..497, ..1009, ..1521
+ * bytes, longer), each streamed by the kernel shape sized for that group
+ * instead of every frame by the shape of the longest.  Requires d_len;
+ * b->d_perm is ignored (d_perm receives the processing order).  b->max_len
+ * (when nonzero) is a hint: the groups above it are folded into the group
+ * that holds it (one launch fewer each; a wrong hint changes speed only).
+ * Records land at d_recs[i] for frame i.  d_perm holds n u32, d_scratch pptk_rx_bin_scratch_bytes(n)
+ * bytes; both stay in use until the stream reaches the end of the call. */
+int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *ctx,
+                               const struct pptk_rx_dev_batch *b, uint32_t *d_perm,
+                               void *d_scratch, void *stream);
 
 /* Tuning: force kernel variant `variant` (0 .. pptk_rx_variant_count()-1)
  * and/or memory-policy flags for every later batch of this context; -1

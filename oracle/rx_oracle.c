@@ -8,7 +8,7 @@
  * Parity is pinned: tests/test_oracle.py checks this file against the
  * reference's own known-answer tests (iphdr/ipcksumtest.c:23-36,58-114,
  * iphdr/iphdrtest.c:12-54, misc/siphashtest.c:16, the SipHash-2-4 paper
- * vectors) and against tests/golden/*.npz, whose records were produced by
+ * vectors) and against the tests/golden npz fixtures, whose records were produced by
  * the reference sources compiled unmodified (oracle/_ref, see
  * oracle/Makefile and oracle/refgen.c).
  *

@@ -1,24 +1,29 @@
-// rx_bin.hip -- stable counting sort of frame indices by length class, so
-// that the T lanes of every team in a wavefront round sum frames of similar
-// length (mixed-size batches, SURVEY.md 8(d) CMIX).  Three small launches:
+// rx_bin.hip -- stable counting sort of frame indices by length group
+// (rx_internal.h kGroupMaxLen), so that every wavefront sums frames of
+// similar length and pptk_rx_batch_device_mixed can stream each group with
+// a kernel shape sized for it (mixed-size batches, SURVEY.md 8(d) CMIX).
+// Three small launches:
 //   1. per-block histograms over a contiguous index range (bin-major matrix)
 //   2. one-block exclusive scan of the matrix
 //   3. per-block stable scatter of indices (wave ballots give the rank)
 // Reads 2 x 2 bytes and writes 4 bytes per frame: <1 % of the frame bytes
-// the transform itself reads.
+// the transform itself reads.  The scan also leaves the group start table
+// (kGroups + 1 entries) behind the counters for the group launches.
 #include "rx_internal.h"
 
 namespace pptk {
 
 namespace {
 
-constexpr int NB = 16;        // length classes: len >> 8, clamped (256-byte steps)
+constexpr int NB = kGroups;   // length groups
 constexpr int BT = 256;       // threads per block
 constexpr int NWARP = BT / 64;
 
 __device__ __forceinline__ int bin_of(uint32_t len) {
-  const int b = (int)(len >> 8);
-  return b < NB - 1 ? b : NB - 1;
+  int b = 0;
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k) b += len > kGroupMaxLen[k];
+  return b;
 }
 
 __global__ __launch_bounds__(BT) void bin_count(const uint16_t *len, uint64_t n,
@@ -34,8 +39,9 @@ __global__ __launch_bounds__(BT) void bin_count(const uint16_t *len, uint64_t n,
   if (threadIdx.x < NB) counts[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan of m = NB * nblocks counters, one block
-__global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m) {
+// exclusive scan of m = NB * nblocks counters (bin-major), one block; then
+// table[k] = start of bin k, table[NB] = total
+__global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, uint32_t *table) {
   __shared__ uint32_t part[1024];
   const uint32_t per = (m + 1023) / 1024;
   const uint32_t lo = threadIdx.x * per;
@@ -56,6 +62,10 @@ __global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m) {
     counts[k] = run;
     run += c;
   }
+  __syncthreads();
+  const uint32_t g = m / NB;
+  if (threadIdx.x <= (unsigned)NB)
+    table[threadIdx.x] = threadIdx.x < (unsigned)NB ? counts[threadIdx.x * g] : part[1023];
 }
 
 __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t n,
@@ -100,7 +110,11 @@ __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t 
 
 size_t bin_scratch_bytes(uint64_t n, int grid) {
   (void)n;
-  return (size_t)NB * (size_t)grid * sizeof(uint32_t);
+  return ((size_t)NB * (size_t)grid + NB + 1) * sizeof(uint32_t);
+}
+
+const uint32_t *bin_table(const void *scratch, int grid) {
+  return (const uint32_t *)scratch + (size_t)NB * (size_t)grid;
 }
 
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm, void *scratch,
@@ -110,7 +124,8 @@ hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm, void *scr
   const int g = (int)((n + per_block - 1) / per_block);
   uint32_t *counts = (uint32_t *)scratch;
   hipLaunchKernelGGL(bin_count, dim3(g), dim3(BT), 0, s, len, n, per_block, counts);
-  hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, s, counts, (uint32_t)(NB * g));
+  hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, s, counts, (uint32_t)(NB * g),
+                     counts + (size_t)NB * grid);
   hipLaunchKernelGGL(bin_scatter, dim3(g), dim3(BT), 0, s, len, n, per_block,
                      (const uint32_t *)counts, perm);
   return hipGetLastError();

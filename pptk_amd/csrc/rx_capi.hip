@@ -20,12 +20,6 @@
 
 using namespace pptk;
 
-namespace {
-
-constexpr uint32_t kStageAlign = 16;
-
-}  // namespace
-
 // One half of the host-batch double buffer: pinned staging, device copies,
 // and the chunk currently in flight on its stream.
 struct RxSlot {
@@ -52,6 +46,7 @@ struct pptk_rx_ctx {
   int device = 0;
   pptk_rx_opts opts{};
   RxKArgs tmpl{};      // key/iphash part of the kernel arguments
+  void *d_zero = nullptr;  // 64 zeroed device bytes (RxKArgs::zero)
   int ncu = 256;
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
@@ -104,8 +99,14 @@ int pptk_rx_ctx_create(struct pptk_rx_ctx **out, const struct pptk_rx_opts *opts
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->ncu = prop.multiProcessorCount;
   for (int v = 0; v < RX_NVARIANTS; ++v) c->bpc[v] = rx_variant_blocks_per_cu(v);
+  if (hipMalloc(&c->d_zero, 64) != hipSuccess || hipMemset(c->d_zero, 0, 64) != hipSuccess) {
+    (void)hipFree(c->d_zero);
+    delete c;
+    return -ENOMEM;
+  }
 
   RxKArgs &t = c->tmpl;
+  t.zero = c->d_zero;
   t.k0 = le64(opts->key);
   t.k1 = le64(opts->key + 8);
   t.bucket4 = opts->iphash_bits4 ? 1u : 0u;
@@ -148,6 +149,7 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   free_staging(c);
+  (void)hipFree(c->d_zero);
   for (const RxRing &r : c->rings) (void)hipHostUnregister(r.host);
   delete c;
 }
@@ -155,9 +157,50 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
 static int pick_variant(uint32_t span) {
   if (span <= 64) return RX_T4S1;
   if (span <= 128) return RX_T4S2;
+  if (span <= 256) return RX_T8S2;
   if (span <= 512) return RX_T16S2;
+  if (span <= 1024) return RX_T16S4;
   if (span <= 1536) return RX_T16S6;
   return RX_T64S2;
+}
+
+// Memory policy (PPTK_RX_TUNE_*).  Default: non-temporal frame loads and
+// record stores for the streaming variants (frames are read once, records
+// written once: measured 4.47 -> 4.25 ms on C1500 in one process, see
+// DESIGN.md "Measurement log"), plain for the small-frame variants (nt
+// measured slower on C64).  PPTK_RX_TUNE overrides for A/B runs.
+static uint32_t pick_tune(const pptk_rx_ctx *c, int variant) {
+  static int tune = -2;
+  if (tune == -2) {
+    const char *e = getenv("PPTK_RX_TUNE");
+    tune = e ? atoi(e) : -1;
+  }
+  if (c->forced_flags >= 0) return (uint32_t)c->forced_flags;
+  if (tune >= 0) return (uint32_t)tune;
+  const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2;
+  return small ? 0u : 33u;
+}
+
+static int forced_variant(const pptk_rx_ctx *c) {
+  static int force = -2;   // PPTK_RX_VARIANT: A/B override (results never change)
+  if (force == -2) {
+    const char *e = getenv("PPTK_RX_VARIANT");
+    force = e ? atoi(e) : -1;
+  }
+  if (c->forced_variant >= 0) return c->forced_variant;
+  return force >= 0 && force < RX_NVARIANTS ? force : -1;
+}
+
+static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n) {
+  const uint64_t ntiles = (n + 63) / 64;
+  const uint64_t want_blocks = (ntiles + 3) / 4;
+  static int grid_mult = -1;
+  if (grid_mult < 0) {
+    const char *e = getenv("PPTK_RX_GRID_MULT");
+    grid_mult = e ? std::max(1, atoi(e)) : 1;
+  }
+  const uint64_t cap = (uint64_t)c->ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, cap));
 }
 
 static uint64_t gcd64(uint64_t a, uint64_t b) {
@@ -169,33 +212,17 @@ static uint64_t gcd64(uint64_t a, uint64_t b) {
   return a;
 }
 
-int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
-                         void *stream) {
+static int check_batch(const pptk_rx_ctx *c, const pptk_rx_dev_batch *b) {
   if (!c || !b) return -EINVAL;
   if (b->n == 0) return 0;
   if (!b->d_frames || !b->d_recs) return -EINVAL;
   if (b->n > 0xffffffffull) return -EINVAL;  // indices are 32-bit (d_perm)
   if (!b->d_off && b->stride == 0 && b->n > 1) return -EINVAL;
   if (!b->d_len && b->fixed_len > 65535) return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  return 0;
+}
 
-  // worst misalignment of a frame start inside a 16-byte chunk
-  uint32_t mmax = 15;
-  if (!b->d_off) {
-    const uint64_t p = (uint64_t)(uintptr_t)b->d_frames;
-    const uint64_t gg = gcd64(b->stride % 16 ? b->stride % 16 : 16, 16);
-    mmax = (uint32_t)((p % gg) + 16 - gg);
-  }
-  uint32_t maxlen = b->d_len ? (b->max_len ? b->max_len : 65535u) : b->fixed_len;
-  int variant = pick_variant(maxlen + mmax);
-  static int force = -2;   // PPTK_RX_VARIANT: A/B override (results never change)
-  if (force == -2) {
-    const char *e = getenv("PPTK_RX_VARIANT");
-    force = e ? atoi(e) : -1;
-  }
-  if (force >= 0 && force < RX_NVARIANTS) variant = force;
-  if (c->forced_variant >= 0) variant = c->forced_variant;
-
+static RxKArgs batch_args(const pptk_rx_ctx *c, const pptk_rx_dev_batch *b) {
   RxKArgs a = c->tmpl;
   a.frames = b->d_frames;
   a.off = b->d_off;
@@ -206,29 +233,58 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   a.n = b->n;
   a.recs = b->d_recs;
   a.hash = b->d_hash;
+  return a;
+}
 
-  // Memory policy (PPTK_RX_TUNE_*).  Default: non-temporal frame loads and
-  // record stores for the streaming variants (frames are read once, records
-  // written once: measured 4.47 -> 4.25 ms on C1500 in one process, see
-  // DESIGN.md "Measurement log"), plain for the small-frame variants (nt
-  // measured slower on C64).  PPTK_RX_TUNE overrides for A/B runs.
-  static int tune = -2;
-  if (tune == -2) {
-    const char *e = getenv("PPTK_RX_TUNE");
-    tune = e ? atoi(e) : -1;
+int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
+                         void *stream) {
+  int rc = check_batch(c, b);
+  if (rc || b->n == 0) return rc;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+
+  // worst misalignment of a frame start inside a 16-byte chunk
+  uint32_t mmax = 15;
+  if (!b->d_off) {
+    const uint64_t p = (uint64_t)(uintptr_t)b->d_frames;
+    const uint64_t gg = gcd64(b->stride % 16 ? b->stride % 16 : 16, 16);
+    mmax = (uint32_t)((p % gg) + 16 - gg);
   }
-  a.tune = tune >= 0 ? (uint32_t)tune : (variant >= RX_T16S2 ? 33u : 0u);
-  if (c->forced_flags >= 0) a.tune = (uint32_t)c->forced_flags;
-  const uint64_t ntiles = (b->n + 63) / 64;
-  const uint64_t want_blocks = (ntiles + 3) / 4;
-  static int grid_mult = -1;
-  if (grid_mult < 0) {
-    const char *e = getenv("PPTK_RX_GRID_MULT");
-    grid_mult = e ? std::max(1, atoi(e)) : 1;
+  const uint32_t maxlen = b->d_len ? (b->max_len ? b->max_len : 65535u) : b->fixed_len;
+  int variant = pick_variant(maxlen + mmax);
+  const int fv = forced_variant(c);
+  if (fv >= 0) variant = fv;
+  RxKArgs a = batch_args(c, b);
+  a.tune = pick_tune(c, variant);
+  return hip_err(launch_rx(variant, a, grid_for(c, variant, b->n), (hipStream_t)stream));
+}
+
+int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
+                               uint32_t *d_perm, void *d_scratch, void *stream) {
+  int rc = check_batch(c, b);
+  if (rc || b->n == 0) return rc;
+  if (!b->d_len || !d_perm || !d_scratch) return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  const hipStream_t s = (hipStream_t)stream;
+  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid);
+  if (e != hipSuccess) return -EIO;
+  RxKArgs a = batch_args(c, b);
+  a.perm = d_perm;
+  const uint32_t *tab = bin_table(d_scratch, kBinGrid);
+  const uint32_t maxlen = b->max_len ? b->max_len : 65535u;
+  const int fv = forced_variant(c);
+  for (int g = 0; g < kGroups; ++g) {
+    // the group holding max_len also takes every group above it (all empty
+    // when the hint is right; a wrong hint costs speed, never results)
+    const bool last = g == kGroups - 1 || kGroupMaxLen[g] >= maxlen;
+    const int variant = fv >= 0 ? fv : kGroupVariant[g];
+    a.range_lo = tab + g;
+    a.range_hi = tab + (last ? kGroups : g + 1);
+    a.tune = pick_tune(c, variant);
+    e = launch_rx(variant, a, grid_for(c, variant, b->n), s);
+    if (e != hipSuccess) return -EIO;
+    if (last) break;
   }
-  const uint64_t cap = (uint64_t)c->ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
-  const int grid = (int)std::min<uint64_t>(want_blocks, cap);
-  return hip_err(launch_rx(variant, a, grid, (hipStream_t)stream));
+  return 0;
 }
 
 int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
@@ -240,14 +296,14 @@ int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
 
 int pptk_rx_variant_count(void) { return RX_NVARIANTS; }
 
-size_t pptk_rx_bin_scratch_bytes(uint64_t n) { return bin_scratch_bytes(n, 2048); }
+size_t pptk_rx_bin_scratch_bytes(uint64_t n) { return bin_scratch_bytes(n, kBinGrid); }
 
 int pptk_rx_bin_device(struct pptk_rx_ctx *c, const uint16_t *d_len, uint64_t n,
                        uint32_t *d_perm, void *d_scratch, void *stream) {
   if (!c || (n && (!d_len || !d_perm || !d_scratch))) return -EINVAL;
   if (n > 0xffffffffull) return -EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) return -EIO;
-  return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, 2048));
+  return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, kBinGrid));
 }
 
 static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {

@@ -24,6 +24,17 @@ struct RxKArgs {
   uint32_t fixed_len;
   uint32_t bucket4, bucket6;  // 1 = compute src_bucket for that family
   uint32_t tune;         // A/B knobs (PPTK_RX_TUNE): bit0 nt frame loads, bit1 no LDS record staging
+  const void *zero;      // >= 16 zeroed device bytes (owned by the context)
+  // Derived by launch_rx for the GATHER kernels: branch-free descriptor
+  // loads.  An absent array is read at index 0 of `zero` (msk = 0) and its
+  // arithmetic stand-in (identity, i * stride_g, fixed_g) is added instead.
+  const uint32_t *perm_ld;
+  const uint64_t *off_ld;
+  const uint16_t *len_ld;
+  uint32_t perm_msk, off_msk, len_msk, fixed_g;
+  uint64_t stride_g;
+  // nullable (GATHER + perm): process perm[*range_lo .. *range_hi) only
+  const uint32_t *range_lo, *range_hi;
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S
@@ -33,14 +44,29 @@ enum RxVariant {
   RX_T4S1 = 0, RX_T4S2, RX_T16S2, RX_T16S6, RX_T32S3, RX_T64S2,
   RX_T16S7L, RX_T32S4L,   // chunk grid on 128-byte lines
   RX_T32S3D7, RX_T16S6D1, // prefetch-depth experiments
+  RX_T8S2, RX_T16S4,      // length-group shapes (256 and 1024 bytes)
   RX_NVARIANTS
 };
+
+// Length groups of pptk_rx_batch_device_mixed: group g holds the frames with
+// len <= kGroupMaxLen[g] (and above the previous bound) and is streamed by
+// kGroupVariant[g], whose 16*T*S-byte shape covers len + 15 bytes of chunk
+// misalignment; the last group takes everything longer (tail loop).
+constexpr int kGroups = 6;
+constexpr uint32_t kGroupMaxLen[kGroups] = {113, 241, 497, 1009, 1521, 0xffffffffu};
+constexpr int kGroupVariant[kGroups] = {RX_T4S2, RX_T8S2, RX_T16S2, RX_T16S4, RX_T16S6,
+                                        RX_T64S2};
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
 int rx_variant_blocks_per_cu(int variant);
 
+// Stable counting sort of 0..n-1 into kGroups length groups.  After it,
+// bin_table(scratch, grid)[g] is the first position of group g in perm and
+// [kGroups] = n (device memory, written by the launch).
+constexpr int kBinGrid = 2048;   // blocks of the binning sort (scratch layout)
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm,
                       void *scratch, hipStream_t s, int grid);
 size_t bin_scratch_bytes(uint64_t n, int grid);
+const uint32_t *bin_table(const void *scratch, int grid);
 
 }  // namespace pptk

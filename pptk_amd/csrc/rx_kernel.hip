@@ -323,27 +323,38 @@ struct Desc {
 
 // Descriptors come either from arithmetic (FIXED: frame i at i * stride,
 // fixed_len bytes, identity order -- no memory traffic, nothing to wait for)
-// or from the d_perm / d_off / d_len arrays (GATHER).
+// or from the d_perm / d_off / d_len arrays (GATHER).  The GATHER loads are
+// unconditional and their results are combined arithmetically (absent arrays
+// and lanes past n read zeros from a.zero, see RxKArgs): a load under a
+// branch or feeding a select leaves the compiler an unknown number of loads
+// in flight, and it answers with a full vmcnt(0) drain of the streaming
+// rounds.  Past-the-end lanes describe frame 0 with idx = ~0 (no record).
 template <bool GATHER>
 __device__ __forceinline__ uint32_t desc_idx(const RxKArgs &a, uint64_t tile, int lane) {
   const uint64_t i = tile * WAVE + lane;
-  if (i >= a.n) return 0xffffffffu;
-  if constexpr (GATHER) return a.perm ? a.perm[i] : (uint32_t)i;
-  else return (uint32_t)i;
+  const uint32_t bad = 0u - (uint32_t)(i >= a.n);
+  if constexpr (GATHER) {
+    const uint32_t ic = (uint32_t)i & ~bad;
+    const uint32_t v = a.perm_ld[ic & a.perm_msk];
+    return (v + (ic & ~a.perm_msk)) | bad;
+  } else {
+    return (uint32_t)i | bad;
+  }
 }
 
 template <bool GATHER>
 __device__ __forceinline__ Desc desc_fill(const RxKArgs &a, uint32_t idx) {
-  Desc d = {0, 0, 0xffffffffu};
-  if (idx != 0xffffffffu) {
-    d.idx = idx;
-    if constexpr (GATHER) {
-      d.base = a.off ? a.off[idx] : (uint64_t)idx * a.stride;
-      d.len = a.len ? (uint32_t)a.len[idx] : a.fixed_len;
-    } else {
-      d.base = (uint64_t)idx * a.stride;
-      d.len = a.fixed_len;
-    }
+  Desc d;
+  d.idx = idx;
+  const uint32_t ic = idx == 0xffffffffu ? 0u : idx;
+  if constexpr (GATHER) {
+    const uint64_t o = a.off_ld[ic & a.off_msk];
+    const uint32_t l = a.len_ld[ic & a.len_msk];
+    d.base = o + (uint64_t)ic * a.stride_g;
+    d.len = l + a.fixed_g;
+  } else {
+    d.base = (uint64_t)ic * a.stride;
+    d.len = a.fixed_len;
   }
   return d;
 }
@@ -397,6 +408,16 @@ constexpr int min_waves_per_simd() { return S * T >= 32 ? 2 : 4; }
 // load destinations, which would force vmcnt waits).
 template <int T, int S, int D, int AL, bool NT, bool GATHER>
 __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_kernel(RxKArgs a) {
+  if constexpr (GATHER) {
+    // length-group launch (pptk_rx_batch_device_mixed): this launch owns
+    // positions [*range_lo, *range_hi) of the binned order, known on the
+    // device only
+    if (a.range_lo) {
+      const uint32_t lo = *a.range_lo, hi = *a.range_hi;
+      a.perm_ld += lo;
+      a.n = hi > lo ? hi - lo : 0;
+    }
+  }
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * IMG_STRIDE];
   constexpr int IMGC = (S * T < IMG_CHUNKS) ? S * T : IMG_CHUNKS;  // chunks parked
   constexpr uint32_t ALM = (1u << AL) - 1;
@@ -412,6 +433,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
   uint64_t tile = (uint64_t)blockIdx.x * WPB + wv;
   Desc dc = load_desc<GATHER>(a, tile, lane);
   Desc dn = load_desc<GATHER>(a, tile + nwaves, lane);
+  uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * nwaves, lane);
   // prologue: the first D rounds of the first tile, in slots 0 .. D-1
   Buf<S> b[D + 1];
   // (issued strictly in slot order: the loop-header wait is computed from
@@ -425,21 +447,16 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
 
   while (tile < ntiles) {
     uint32_t my_sum = 0;
-    // Descriptors of tile + 2 nwaves, in two stages so that no wait on them
-    // ever has to drain the chunk loads in flight: the index load (perm) is
-    // issued before this tile's rounds, the dependent offset/length loads
-    // after them; both complete long before they are needed.
-    const uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * nwaves, lane);
+    // Descriptors run ahead in two stages so that no wait on them ever has
+    // to drain the chunk loads in flight: the index (perm) of tile + 3 nwaves
+    // is loaded here, the dependent offset/length of tile + 2 nwaves (whose
+    // index arrived during the previous tile) before the last round group.
+    const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * nwaves, lane);
     // ---- streaming rounds: team g sums frame g*T + r over [team_start, len).
-    // Fixed-slot ring of D + 1 rounds: round r lives in slot r % (D + 1); the
-    // loop is unrolled by D + 1 so every slot index is a constant and no
-    // register of an in-flight load is ever copied.
-#ifdef PPTK_RX_FULL_UNROLL
-#pragma unroll(T <= 16 ? T : 1)
-#else
-#pragma unroll 1
-#endif
-    for (int r0 = 0; r0 < T; r0 += D + 1) {
+    // Fixed-slot ring of D + 1 rounds: round r lives in slot r % (D + 1); a
+    // group of D + 1 rounds is unrolled so every slot index is a constant and
+    // no register of an in-flight load is ever copied.
+    auto group = [&](const int r0) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u <= D; ++u) {
         const int r = r0 + u;
@@ -478,8 +495,20 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
         if (j == r)
           my_sum = acc;
       }
-    }
+    };
+#ifdef PPTK_RX_FULL_UNROLL
+#pragma unroll(T <= 16 ? T : 1)
+#else
+#pragma unroll 1
+#endif
+    for (int r0 = 0; r0 < T - (D + 1); r0 += D + 1)
+      group(r0);
+    // the descriptors two tiles ahead are loaded BEFORE the last group issues
+    // the next tile's first D rounds: the copies dc <- dn <- d2 at the tile
+    // boundary then wait only for these loads, not for the rounds in flight
     const Desc d2 = desc_fill<GATHER>(a, idx2);
+    __builtin_amdgcn_sched_barrier(0);
+    group(T - (D + 1));
 
     // ---- lane phase: frame `lane` -> record (parsed once per frame)
     const bool stage = !(GATHER && a.perm) && !(a.tune & 2u);
@@ -626,14 +655,26 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
     tile += nwaves;
     dc = dn;
     dn = d2;
+    idx2 = idx3;
   }
 }
 
 template <int T, int S, int D, int AL>
-hipError_t launch_variant(const RxKArgs &a, int grid, hipStream_t s) {
+hipError_t launch_variant(const RxKArgs &a0, int grid, hipStream_t s) {
   const dim3 gd(grid), bd(WAVE * WPB);
+  RxKArgs a = a0;
   const bool nt = a.tune & 1u;
   const bool gather = a.off || a.len || a.perm;
+  if (gather) {
+    a.perm_ld = a.perm ? a.perm : (const uint32_t *)a.zero;
+    a.perm_msk = a.perm ? ~0u : 0u;
+    a.off_ld = a.off ? a.off : (const uint64_t *)a.zero;
+    a.off_msk = a.off ? ~0u : 0u;
+    a.stride_g = a.off ? 0u : a.stride;
+    a.len_ld = a.len ? a.len : (const uint16_t *)a.zero;
+    a.len_msk = a.len ? ~0u : 0u;
+    a.fixed_g = a.len ? 0u : a.fixed_len;
+  }
   if (gather) {
     if (nt) hipLaunchKernelGGL((rx_kernel<T, S, D, AL, true, true>), gd, bd, 0, s, a);
     else hipLaunchKernelGGL((rx_kernel<T, S, D, AL, false, true>), gd, bd, 0, s, a);
@@ -664,7 +705,9 @@ int blocks_per_cu() {
   X(RX_T16S7L, 16, 7, 1, 7)       \
   X(RX_T32S4L, 32, 4, 3, 7)       \
   X(RX_T32S3D7, 32, 3, 7, 4)      \
-  X(RX_T16S6D1, 16, 6, 1, 4)
+  X(RX_T16S6D1, 16, 6, 1, 4)       \
+  X(RX_T8S2, 8, 2, 3, 4)          \
+  X(RX_T16S4, 16, 4, 3, 4)
 
 }  // namespace
 

@@ -41,22 +41,23 @@ assert ctypes.sizeof(RxOpts) == 36
 
 EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_batch", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
-           "pptk_rx_bin_device", "pptk_rx_version", "pptk_rx_set_tuning",
+           "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """Load libpptkrx.so once; raise if it is missing (no fallback)."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"{LIB_PATH} not built: run `make` or __graft_entry__.build()")
-        L = ctypes.CDLL(LIB_PATH)
+def lib(path=None):
+    """Load libpptkrx.so (or the A/B build at `path`) once; raise if it is
+    missing (no fallback)."""
+    path = path or LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not built: run `make` or __graft_entry__.build()")
+        L = ctypes.CDLL(path)
         vp = ctypes.c_void_p
         L.pptk_rx_opts_default.argtypes = [ctypes.POINTER(RxOpts)]
         L.pptk_rx_opts_default.restype = None
@@ -72,6 +73,8 @@ def lib():
         L.pptk_rx_bin_scratch_bytes.restype = ctypes.c_size_t
         L.pptk_rx_bin_device.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp]
         L.pptk_rx_bin_device.restype = ctypes.c_int
+        L.pptk_rx_batch_device_mixed.argtypes = [vp, ctypes.POINTER(RxDevBatch), vp, vp, vp]
+        L.pptk_rx_batch_device_mixed.restype = ctypes.c_int
         L.pptk_rx_version.restype = ctypes.c_char_p
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
@@ -87,8 +90,8 @@ def lib():
             getattr(L, f).restype = ctypes.c_uint16
         L.ip_cksum_feed.argtypes = [ctypes.POINTER(ctypes.c_uint32), vp, ctypes.c_size_t]
         L.ip_cksum_feed.restype = None
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _dp(t):
@@ -100,8 +103,9 @@ class RxContext:
     """One pptk_rx_ctx (one per rx thread in a C application)."""
 
     def __init__(self, device=0, key=bytes(16), iphash_bits4=0, iphash_bits6=0,
-                 iphash_size=1, max_batch=8192, max_frame=9216, gather_threads=1):
-        L = lib()
+                 iphash_size=1, max_batch=8192, max_frame=9216, gather_threads=1,
+                 lib_path=None):
+        self._L = L = lib(lib_path)
         o = RxOpts()
         L.pptk_rx_opts_default(ctypes.byref(o))
         o.device = device
@@ -117,13 +121,13 @@ class RxContext:
 
     def set_tuning(self, variant=-1, flags=-1):
         """Force kernel variant / memory-policy flags (speed only; -1 = auto)."""
-        rc = lib().pptk_rx_set_tuning(self._ctx, variant, flags)
+        rc = self._L.pptk_rx_set_tuning(self._ctx, variant, flags)
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_set_tuning({variant}, {flags}) failed")
 
     def close(self):
         if self._ctx:
-            lib().pptk_rx_ctx_destroy(self._ctx)
+            self._L.pptk_rx_ctx_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
 
     def __del__(self):
@@ -145,19 +149,41 @@ class RxContext:
                        max_len, n, recs.data_ptr(),
                        None if hash_out is None else hash_out.data_ptr())
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
-        rc = lib().pptk_rx_batch_device(self._ctx, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
+        rc = self._L.pptk_rx_batch_device(self._ctx, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch_device failed ({rc})")
+        return recs
+
+    def batch_device_mixed(self, frames, n, off, lens, recs=None, hash_out=None, max_len=0,
+                           perm=None, scratch=None, stream=None):
+        """Mixed-size batch: device binning + one launch per length group
+        (asynchronous).  perm/scratch: optional preallocated device buffers."""
+        import torch
+        if recs is None:
+            recs = torch.empty((n, 64), dtype=torch.uint8, device=frames.device)
+        if perm is None:
+            perm = torch.empty(n, dtype=torch.int32, device=frames.device)
+        if scratch is None:
+            scratch = torch.empty(self._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
+                                  device=frames.device)
+        b = RxDevBatch(frames.data_ptr(), off.data_ptr(), lens.data_ptr(), None, 0, 0,
+                       max_len, n, recs.data_ptr(),
+                       None if hash_out is None else hash_out.data_ptr())
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = self._L.pptk_rx_batch_device_mixed(self._ctx, ctypes.byref(b), _dp(perm),
+                                                _dp(scratch), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_batch_device_mixed failed ({rc})")
         return recs
 
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""
         import torch
         perm = torch.empty(n, dtype=torch.int32, device=lens.device)
-        scratch = torch.empty(lib().pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
+        scratch = torch.empty(self._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
                               device=lens.device)
         s = stream if stream is not None else torch.cuda.current_stream(lens.device)
-        rc = lib().pptk_rx_bin_device(self._ctx, _dp(lens), n, _dp(perm), _dp(scratch),
+        rc = self._L.pptk_rx_bin_device(self._ctx, _dp(lens), n, _dp(perm), _dp(scratch),
                                       ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_bin_device failed ({rc})")
@@ -165,12 +191,12 @@ class RxContext:
 
     def register_ring(self, buf):
         """Register numpy buffer `buf` as a zero-copy rx ring."""
-        rc = lib().pptk_rx_register_ring(self._ctx, ctypes.c_void_p(buf.ctypes.data), buf.nbytes)
+        rc = self._L.pptk_rx_register_ring(self._ctx, ctypes.c_void_p(buf.ctypes.data), buf.nbytes)
         if rc != 0:
             raise OSError(-rc, "pptk_rx_register_ring failed")
 
     def unregister_ring(self, buf):
-        rc = lib().pptk_rx_unregister_ring(self._ctx, ctypes.c_void_p(buf.ctypes.data))
+        rc = self._L.pptk_rx_unregister_ring(self._ctx, ctypes.c_void_p(buf.ctypes.data))
         if rc != 0:
             raise OSError(-rc, "pptk_rx_unregister_ring failed")
 
@@ -178,7 +204,7 @@ class RxContext:
         """pptk_rx_batch over a ctypes array of LdpPacket; returns records."""
         n = len(pkts)
         recs = np.zeros(n, dtype=REC_DTYPE)
-        rc = lib().pptk_rx_batch(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n,
+        rc = self._L.pptk_rx_batch(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n,
                                  ctypes.c_void_p(recs.ctypes.data))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch failed ({rc})")

@@ -68,7 +68,7 @@ def test_offsets_mode(name, shift, dev):
 
 
 @pytest.mark.parametrize("name", GOLDEN_SETS)
-@pytest.mark.parametrize("max_len", [1, 40, 100, 400, 1500, 65535])
+@pytest.mark.parametrize("max_len", [1, 40, 100, 200, 400, 900, 1500, 65535])
 def test_every_variant(name, max_len, dev):
     """max_len is a tuning hint: a wrong hint selects another kernel variant
     (T4S1 ... T64S2) but must never change a result."""
@@ -114,11 +114,91 @@ def test_binned_order_and_hash_out(name, dev):
     assert not d, d
     want = as_records(z["recs"])
     assert np.array_equal(h, np.where(want["flags"] & F_PARSED, want["flow_hash"], 0))
-    # the permutation is a stable sort of indices by length class
+    # the permutation is a stable sort of indices by length group
     n = len(z["off"])
     assert np.array_equal(np.sort(perm), np.arange(n))
-    cls = np.minimum(z["len"].astype(np.int64) >> 8, 15)
-    assert np.array_equal(perm, np.argsort(cls, kind="stable"))
+    assert np.array_equal(perm, np.argsort(_group_of(z["len"]), kind="stable"))
+
+
+GROUP_MAX_LEN = [113, 241, 497, 1009, 1521]   # rx_internal.h kGroupMaxLen
+
+
+def _group_of(lens):
+    return np.searchsorted(np.array(GROUP_MAX_LEN), lens.astype(np.int64), side="left")
+
+
+def _run_mixed(ctx, z, dev, shift=0, max_len=0):
+    buf, off, lens = z["buf"], z["off"], z["len"]
+    n = len(off)
+    _keep, frames = _upload(buf, dev, shift)
+    lens_t = torch.from_numpy(lens.view(np.int16)).to(dev)
+    off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+    perm = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    h = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    recs = ctx.batch_device_mixed(frames, n, off_t, lens_t, hash_out=h, max_len=max_len,
+                                  perm=perm)
+    torch.cuda.synchronize()
+    return (recs.cpu().numpy().reshape(-1), h.cpu().numpy().view(np.uint64),
+            perm.cpu().numpy().view(np.uint32))
+
+
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+@pytest.mark.parametrize("shift", [0, 7])
+@pytest.mark.parametrize("max_len", [0, 100, 600, 1500])
+def test_mixed_length_groups(name, shift, max_len, dev):
+    """pptk_rx_batch_device_mixed: device binning + one launch per length
+    group; max_len is a hint (a low one folds the upper groups into one
+    launch) -- records, hashes and the order are exact either way."""
+    z = load_golden(name)
+    got, h, perm = _run_mixed(_ctx(z), z, dev, shift=shift, max_len=max_len)
+    d = diff_records(got, z["recs"])
+    assert not d, d
+    want = as_records(z["recs"])
+    assert np.array_equal(h, np.where(want["flags"] & F_PARSED, want["flow_hash"], 0))
+    assert np.array_equal(perm, np.argsort(_group_of(z["len"]), kind="stable"))
+
+
+def _frame_of_len(fg, rng, L):
+    """A frame of exactly L bytes: IPv4/IPv6 TCP/UDP when it fits, else the
+    truncated head of one (malformed)."""
+    proto = 6 if rng.random() < 0.5 else 17
+    v6 = rng.random() < 0.3
+    need = 14 + (40 if v6 else 20) + (20 if proto == 6 else 8)
+    if L >= need:
+        return fg.frame_v6(rng, proto, L) if v6 else fg.frame_v4(rng, proto, L)
+    return fg.frame_v4(rng, 17, 64)[:L]
+
+
+def test_mixed_every_group_boundary(dev):
+    """Frames at both sides of every group bound (and jumbo frames past the
+    last one), in random order, through the grouped launches."""
+    import framegen
+    from oracle.oracle import Oracle, make_opts
+    rng = np.random.default_rng(77)
+    sizes = []
+    for b in GROUP_MAX_LEN:
+        sizes += [b - 1, b, b + 1]
+    sizes += [14, 42, 60, 64, 2000, 4000, 9000, 9018]
+    sizes = np.array(sizes * 40)
+    rng.shuffle(sizes)
+    frames = [_frame_of_len(framegen, rng, int(L)) for L in sizes]
+    off = np.zeros(len(frames), np.uint64)
+    pos = 0
+    for i, f in enumerate(frames):
+        off[i] = pos
+        pos += len(f) + int(rng.integers(0, 5))
+    buf = np.zeros(pos + 64, np.uint8)
+    for i, f in enumerate(frames):
+        buf[int(off[i]):int(off[i]) + len(f)] = np.frombuffer(f, np.uint8)
+    lens = np.array([len(f) for f in frames], np.uint16)
+    key = bytes(range(1, 17))
+    want = Oracle().rx_batch(buf, off, lens, opts=make_opts(key, 24, 48, 1 << 12))
+    z = {"buf": buf, "off": off, "len": lens, "key": np.frombuffer(key, np.uint8),
+         "iphash": np.array([24, 48, 1 << 12])}
+    got, _, perm = _run_mixed(_ctx(z), z, dev, shift=3)
+    d = diff_records(got, want)
+    assert not d, d
+    assert np.array_equal(perm, np.argsort(_group_of(lens), kind="stable"))
 
 
 @pytest.mark.parametrize("name", ["edge", "cmix"])

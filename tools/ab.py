@@ -1,10 +1,17 @@
-"""BENCH TOOLING: in-process A/B of kernel variants / flags on one batch.
+"""BENCH TOOLING: in-process A/B of kernel variants / flags / library builds
+on one batch.
 
-    python tools/ab.py c1500 3:1 3:0 6:1 7:1 ...   (variant:flags pairs)
+    python tools/ab.py c1500 3:1 3:0 6:1 ...        (variant:flags pairs)
+    AB_LIBS=old=build/ab_old/libpptkrx.so python tools/ab.py cmix 3:33 old:3:33
 
+A setting is [lib:]variant:flags; variant or flags -1 = automatic choice;
+lib names come from AB_LIBS (name=path,...), default = pptk_amd/libpptkrx.so.
 Generates the batch once, then times every setting in interleaved rounds
 (A B C A B C ...) so that clock and thermal drift hit all settings alike;
-prints one JSON line with the median kernel ms and GB/s per setting."""
+prints one JSON line with the median kernel ms and GB/s per setting.
+AB_BIN=1 processes mixed batches in length-binned order (pptk_rx_bin_device,
+timed inside each launch's window); AB_MIXED=1 through
+pptk_rx_batch_device_mixed (binning + one launch per length group)."""
 import json
 import os
 import sys
@@ -15,39 +22,77 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def parse_setting(a):
+    p = a.split(":")
+    if len(p) == 2:
+        return ("", int(p[0]), int(p[1]))
+    return (p[0], int(p[1]), int(p[2]))
+
+
 def main():
     import torch
     from pptk_amd.rx import RxContext
     from tools.membench import measure
     from tools.synth import make_batch
     cfg = sys.argv[1]
-    settings = [tuple(int(x) for x in a.split(":")) for a in sys.argv[2:]]
+    settings = [parse_setting(a) for a in sys.argv[2:]]
+    libs = {"": None}
+    for kv in filter(None, os.environ.get("AB_LIBS", "").split(",")):
+        k, v = kv.split("=", 1)
+        libs[k] = os.path.join(ROOT, v) if not os.path.isabs(v) else v
     n = int(os.environ.get("AB_FRAMES", 16 * 1024 * 1024))
     rounds = int(os.environ.get("AB_ROUNDS", 5))
     reps = int(os.environ.get("AB_REPS", 5))
+    binned = bool(os.environ.get("AB_BIN"))
     dev = torch.device("cuda", 0)
     b = make_batch(cfg, n, dev)
     kw = (dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]) if "off" in b
           else dict(stride=b["stride"], fixed_len=b["fixed_len"]))
     recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-    ctx = RxContext(0, bytes(range(1, 17)))
+    ctxs = {k: RxContext(0, bytes(range(1, 17)), lib_path=v) for k, v in libs.items()}
+
+    mixed = bool(os.environ.get("AB_MIXED")) and "off" in b
+    if mixed:
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        scratch = torch.empty(ctxs[""]._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
+                              device=dev)
+
+    def launch(ctx):
+        if mixed:
+            ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], recs=recs,
+                                   max_len=b["max_len"], perm=perm, scratch=scratch)
+        elif binned and "off" in b:
+            ctx.batch_device(b["frames"], n, recs=recs, perm=ctx.bin_device(b["lens"], n), **kw)
+        else:
+            ctx.batch_device(b["frames"], n, recs=recs, **kw)
+
+    ref = None
     times = {s: [] for s in settings}
+    same = {}
     for _ in range(rounds):
         for s in settings:
-            ctx.set_tuning(*s)
-            ctx.batch_device(b["frames"], n, recs=recs, **kw)
+            ctx = ctxs[s[0]]
+            ctx.set_tuning(s[1], s[2])
+            launch(ctx)
+            torch.cuda.synchronize()
+            if s not in same:       # every setting must give the same records
+                if ref is None:
+                    ref = recs.clone()
+                same[s] = bool(torch.equal(recs, ref))
             for _ in range(reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                ctx.batch_device(b["frames"], n, recs=recs, **kw)
+                launch(ctx)
                 e1.record()
                 torch.cuda.synchronize()
                 times[s].append(e0.elapsed_time(e1))
-    out = {"cfg": cfg, "frames": n, "box": measure(b["frames"])}
+    out = {"cfg": cfg, "frames": n, "binned": binned, "mixed": mixed,
+           "box": measure(b["frames"])}
     for s, t in times.items():
         ms = float(np.median(t))
-        out[f"{s[0]}:{s[1]}"] = {"ms": round(ms, 4), "gbs": round(b["bytes"] / ms / 1e6, 1),
-                                 "mpkts": round(n / ms / 1e3, 1)}
+        key = ":".join(str(x) for x in s if x != "")
+        out[key] = {"ms": round(ms, 4), "gbs": round(b["bytes"] / ms / 1e6, 1),
+                    "mpkts": round(n / ms / 1e3, 1), "same_records": same[s]}
     print(json.dumps(out))
 
 

@@ -5,7 +5,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libpptksynth.so")
-CFG = {"c64": 0, "c1500": 1, "cmix": 2, "c1500a": 1}   # c1500a: 1536-byte slots
+CFG = {"c64": 0, "c1500": 1, "cmix": 2, "c1500a": 1, "c1500g": 1}
+# c1500a: 1536-byte slots; c1500g: C1500 frames described by off/len arrays
 SEED = 0x5EED
 
 _lib = None
@@ -33,14 +34,17 @@ def make_batch(cfg, n, device, first=0, seed=SEED, stream=None):
     sp = ctypes.c_void_p(s.cuda_stream)
     out = {"n": n, "cfg": cfg}
     expect = torch.empty(n, dtype=torch.uint8, device=device)
-    if cfg in ("c64", "c1500", "c1500a"):
-        stride = {"c64": 64, "c1500": 1500, "c1500a": 1536}[cfg]
+    if cfg in ("c64", "c1500", "c1500a", "c1500g"):
+        stride = {"c64": 64, "c1500": 1500, "c1500a": 1536, "c1500g": 1500}[cfg]
         flen = 64 if cfg == "c64" else 1500
         frames = torch.empty(n * stride + 64, dtype=torch.uint8, device=device)
         rc = lib().synth_frames(c, seed, first, n, frames.data_ptr(), None, stride,
                                 expect.data_ptr(), sp)
         out.update(frames=frames, stride=stride, fixed_len=flen, max_len=flen,
                    bytes=n * flen)
+        if cfg == "c1500g":
+            out["off"] = torch.arange(n, dtype=torch.int64, device=device) * stride
+            out["lens"] = torch.full((n,), flen, dtype=torch.int16, device=device)
     else:
         lens = torch.empty(n, dtype=torch.int16, device=device)
         rc = lib().synth_sizes(c, seed, first, n, lens.data_ptr(), sp)
