@@ -53,7 +53,8 @@ def dist_setup(ngpus):
 
 def barrier(ws, dev):
     import torch
-    torch.cuda.synchronize(dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     if ws > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -79,26 +80,22 @@ def sum_over_ranks(x, ws, dev):
     return float(t.item())
 
 
-def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=SETTLE_S):
-    """Generate shard `rank` of config `cfg`, time `steps` launches."""
+def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=SETTLE_S,
+               compact=False, batch=None):
+    """Generate shard `rank` of config `cfg` (or reuse `batch`), time `steps`
+    launches.  compact: 32-byte records (struct pptk_rx_rec32)."""
     import torch
     from pptk_amd.shard import allgather_flow_hash
     from tools.synth import make_batch
-    b = make_batch(cfg, n, dev, first=rank * n)
+    b = batch if batch is not None else make_batch(cfg, n, dev, first=rank * n)
     torch.cuda.synchronize(dev)
-    recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
     hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)] if (gather and ws > 1) else None
-    mixed = "off" in b
-    if mixed:
-        # mixed sizes: device length binning + one launch per length group,
-        # all inside the timed step (pptk_rx_batch_device_mixed)
-        import ctypes
-        from pptk_amd.rx import lib as rxlib
-        perm_buf = torch.empty(n, dtype=torch.int32, device=dev)
-        scratch = torch.empty(rxlib().pptk_rx_bin_scratch_bytes(ctypes.c_uint64(n)),
-                              dtype=torch.uint8, device=dev)
-        kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"], perm=perm_buf,
-                  scratch=scratch)
+    if "off" in b:
+        # mixed sizes: per-frame offset/length arrays, frames in batch order
+        # (measured faster than length-binned order, whose per-frame record
+        # scatter costs more than the uniform team shape wastes; DESIGN.md)
+        kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
     else:
         kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
     gout = None
@@ -111,10 +108,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
         # the dense flow-hash array only feeds the all-gather (N > 1); at
         # N = 1 the records (which carry flow_hash) are the whole output
         h = hbuf[k & 1] if gout is not None else None
-        if mixed:
-            ctx.batch_device_mixed(b["frames"], n, recs=recs, hash_out=h, **kw)
-        else:
-            ctx.batch_device(b["frames"], n, recs=recs, hash_out=h, **kw)
+        ctx.batch_device(b["frames"], n, recs=recs, hash_out=h, compact=compact, **kw)
         if gout is not None:
             if work[0] is not None:
                 work[0].wait()                  # previous gather done before reuse
@@ -155,7 +149,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     kms = [a.elapsed_time(z) for a, z in ev]
     kernel_ms = float(np.median(kms))
     res = {
-        "n": n, "bytes": b["bytes"], "wall_s": wall,
+        "n": n, "bytes": b["bytes"], "rec_bytes": n * (32 if compact else 64), "wall_s": wall,
         "ms_per_step": wall / steps * 1e3, "kernel_ms": kernel_ms,
         "mpkts": n * ws * steps / wall / 1e6,
     }
@@ -163,7 +157,8 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     # checksum verdicts equal what the generator planted
     if check:
         from pptk_amd.records import F_IP_OK, F_L4_OK, F_PARSED
-        r = recs.view(torch.int16)[:, 27].to(torch.int32) & 0xFFFF   # flags @54
+        fcol = 10 if compact else 27                                  # flags @20 / @54
+        r = recs.view(torch.int16)[:, fcol].to(torch.int32) & 0xFFFF
         exp = b["expect"].to(torch.int32)
         ok_parsed = bool(((r & F_PARSED) != 0).all().item())
         ip_ok = ((r & F_IP_OK) != 0).to(torch.int32)
@@ -173,17 +168,34 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
         res["full_batch_check"] = {"parsed": ok_parsed, "ip_verdicts": ok_ip,
                                    "l4_verdicts": ok_l4,
                                    "corrupted": int((exp != 3).sum().item())}
-        res["oracle_sample"] = oracle_sample(b, recs, n, dev)
+        res["oracle_sample"] = oracle_sample(b, recs, n, dev, compact=compact)
     res["_batch"] = b
     res["_recs"] = recs
     return res
 
 
-def oracle_sample(b, recs, n, dev, k=4096):
+def summary(r, n):
+    """Per-config result: rate, kernel time, read roofline fraction (SURVEY
+    8(d): frame bytes / kernel time / peak) and read+write fraction (frame
+    bytes + record bytes), parity checks."""
+    ks = r["kernel_ms"] * 1e-3
+    ach = r["bytes"] / ks / 1e9
+    rw = (r["bytes"] + r["rec_bytes"]) / ks / 1e9
+    return {"value": round(r["mpkts"], 1), "unit": "Mpkts/s",
+            "kernel_ms": round(r["kernel_ms"], 4), "frames_per_gpu": n,
+            "frame_bytes": r["bytes"], "record_bytes": r["rec_bytes"],
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "rw_achieved": round(rw, 1), "rw_frac": round(rw / HBM_PEAK_GBS, 4)},
+            "full_batch_check": r.get("full_batch_check"),
+            "oracle_sample": r.get("oracle_sample")}
+
+
+def oracle_sample(b, recs, n, dev, k=4096, compact=False):
     """Bit-exact check of k random frames against the CPU oracle."""
     import torch
     from oracle.oracle import Oracle, make_opts
-    from pptk_amd.records import diff_records
+    from pptk_amd.records import REC32_DTYPE, REC_DTYPE, diff_records, to_rec32
     rng = np.random.default_rng(1234)
     idx = np.sort(rng.choice(n, size=min(k, n), replace=False))
     if "off" in b:
@@ -202,7 +214,9 @@ def oracle_sample(b, recs, n, dev, k=4096):
     want = Oracle().rx_batch(buf, np.array(offs, np.uint64), lens,
                              opts=make_opts(KEY), nthreads=8)
     got = recs[torch.from_numpy(idx).to(dev)].cpu().numpy()
-    d = diff_records(got, want)
+    if compact:
+        want = to_rec32(want)
+    d = diff_records(got, want, dtype=REC32_DTYPE if compact else REC_DTYPE)
     return {"frames": int(len(idx)), "mismatches": 0 if not d else int(d.split()[0])}
 
 
@@ -360,7 +374,7 @@ def main():
         # same launches without the collective: the kernel-only duration the
         # roofline uses, and the rate "without the gather" 
         nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False,
-                         args.settle)
+                         args.settle, batch=prim["_batch"])
         del nog["_batch"], nog["_recs"]
         gat = gather_bench(n, ws, dev, args.steps)
         log(f"[rank {rank}] no gather: {nog['mpkts']:.1f} Mpkts/s; all-gather {gat}")
@@ -378,11 +392,20 @@ def main():
     kernel_ms = (nog or prim)["kernel_ms"]
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(primary_cfg)
+    rw = (bytes_per_launch + prim["rec_bytes"]) / (kernel_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "rw_achieved": round(rw, 1), "rw_frac": round(rw / HBM_PEAK_GBS, 4),
                 "traffic_source": tsrc,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_ms": round(kernel_ms, 4)}
+
+    # the same batch with compact 32-byte records (struct pptk_rx_rec32)
+    r32 = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check,
+                     args.settle, compact=True, batch=prim["_batch"])
+    rec32 = summary(r32, n)
+    del r32["_batch"], r32["_recs"]
+    log(f"[rank {rank}] {primary_cfg} rec32: {rec32['value']} Mpkts/s")
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu and primary_cfg == "c1500":
@@ -398,15 +421,12 @@ def main():
         for cfg in ("c64", "cmix"):
             r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check,
                            args.settle)
-            ach = r["bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
-            secondary[cfg] = {"value": round(r["mpkts"], 1), "unit": "Mpkts/s",
-                              "kernel_ms": round(r["kernel_ms"], 4),
-                              "frames_per_gpu": n, "frame_bytes": r["bytes"],
-                              "roofline": {"bound": "hbm", "achieved": round(ach, 1),
-                                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                           "frac": round(ach / HBM_PEAK_GBS, 4)},
-                              "full_batch_check": r.get("full_batch_check"),
-                              "oracle_sample": r.get("oracle_sample")}
+            secondary[cfg] = summary(r, n)
+            if cfg == "c64":
+                r32 = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False,
+                                 check, args.settle, compact=True, batch=r["_batch"])
+                secondary[cfg]["rec32"] = summary(r32, n)
+                del r32["_batch"], r32["_recs"]
             if cfg == "c64" and rank == 0 and ws == 1 and not args.no_cpu:
                 secondary[cfg]["cpu_baseline"] = cpu_baseline_small(
                     r["_batch"], seconds=max(1.0, args.cpu_seconds / 2.5))
@@ -435,6 +455,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "value_no_gather": None if nog is None else round(nog["mpkts"], 1),
+            "rec32": rec32,
             "allgather": gat,
             "box_hbm": box,
             "parity": {"full_batch": full_check, "oracle_sample": sample_check},

@@ -58,6 +58,25 @@ struct pptk_rx_rec {
   uint8_t reserved;    /* 63 always 0                                       */
 };
 
+/* ---- compact record (32 bytes): the same values minus the raw checksum
+ * words, ethertype, version and the IPv6 addresses (IPv6 frames carry 0 in
+ * src4/dst4; the addresses are at frame + l3_off + 8 / + 24).  Written
+ * instead of pptk_rx_rec when pptk_rx_dev_batch.d_recs32 is set: half the
+ * record bytes, which is what bounds small frames. */
+struct pptk_rx_rec32 {
+  uint64_t flow_hash;  /*  0 as pptk_rx_rec.flow_hash                       */
+  uint32_t src4;       /*  8 IPv4 source, network byte order; 0 for IPv6    */
+  uint32_t dst4;       /* 12 IPv4 destination; 0 for IPv6                   */
+  uint16_t sport;      /* 16 host order                                     */
+  uint16_t dport;      /* 18                                                */
+  uint16_t flags;      /* 20 PPTK_RX_F_*                                    */
+  uint8_t proto;       /* 22                                                */
+  uint8_t l3_off;      /* 23                                                */
+  uint16_t l4_off;     /* 24                                                */
+  uint16_t l4_len;     /* 26                                                */
+  uint32_t src_bucket; /* 28                                                */
+};
+
 #define PPTK_RX_F_PARSED 0x0001u      /* IPv4/IPv6 header parsed            */
 #define PPTK_RX_F_IP_OK 0x0002u       /* ip_cksum == 0 (always for IPv6)    */
 #define PPTK_RX_F_L4_OK 0x0004u       /* L4 present and l4_cksum == 0       */
@@ -110,7 +129,8 @@ int pptk_rx_unregister_ring(struct pptk_rx_ctx *ctx, void *base);
  * Frame i starts at d_frames + (d_off ? d_off[i] : i * stride) and is
  * (d_len ? d_len[i] : fixed_len) bytes long.  d_perm (nullable) gives the
  * processing order (a permutation of 0..n-1, e.g. from
- * pptk_rx_bin_device); records always land at recs[i] for frame i.
+ * pptk_rx_bin_device); records always land at d_recs[i] (or d_recs32[i]
+ * when that is set: compact records, d_recs unused) for frame i.
  * d_hash (nullable) additionally receives flow_hash[i] as a dense u64 array,
  * the send buffer of the multi-GPU all-gather.
  * The frame buffer must stay readable up to the next 16-byte boundary past
@@ -124,8 +144,9 @@ struct pptk_rx_dev_batch {
   uint32_t fixed_len;
   uint32_t max_len;       /* upper bound of frame lengths (tuning only)   */
   uint64_t n;
-  struct pptk_rx_rec *d_recs;
+  struct pptk_rx_rec *d_recs;     /* nullable when d_recs32 is set     */
   uint64_t *d_hash;       /* nullable                                     */
+  struct pptk_rx_rec32 *d_recs32; /* nullable: compact records instead */
 };
 
 int pptk_rx_batch_device(struct pptk_rx_ctx *ctx,
@@ -153,6 +174,29 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *ctx, const uint16_t *d_len,
 int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *ctx,
                                const struct pptk_rx_dev_batch *b, uint32_t *d_perm,
                                void *d_scratch, void *stream);
+
+/* Batched rate limiting: ip_permitted / ipv6_permitted (reference
+ * iphash/iphash.c:108-197) for a device batch, with the result the
+ * reference gives when called once per frame in frame order.  The subject
+ * frames are the PARSED frames of `family` (4 or 6; the context must have
+ * that family's iphash_bits set, so the records carry its bucket) for which
+ * d_subject[i] != 0 (d_subject nullable = all of them).  d_tokens holds
+ * opts.iphash_size u32 counters (the entries of struct ip_hash, widened to
+ * u32); verdict[i] = 1 permitted (a token was consumed), 0 denied, 2 not a
+ * subject.  Reads one of d_recs / d_recs32 (the other NULL).  d_scratch:
+ * pptk_rx_permit_scratch_bytes(n, opts.iphash_size) bytes.  Asynchronous. */
+size_t pptk_rx_permit_scratch_bytes(uint64_t n, uint32_t hash_size);
+int pptk_rx_permit_device(struct pptk_rx_ctx *ctx, const struct pptk_rx_rec *d_recs,
+                          const struct pptk_rx_rec32 *d_recs32, uint64_t n, int family,
+                          const uint8_t *d_subject, uint32_t *d_tokens,
+                          uint8_t *d_verdict, void *d_scratch, void *stream);
+
+/* The token refill timer (batch_timer_fn, reference iphash/iphash.c:
+ * 290-350) for buckets [start, end): tokens = min(tokens + add, initial).
+ * Asynchronous; order it with pptk_rx_permit_device on one stream. */
+int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *ctx, uint32_t *d_tokens,
+                                 uint32_t start, uint32_t end, uint32_t add,
+                                 uint32_t initial_tokens, void *stream);
 
 /* Tuning: force kernel variant `variant` (0 .. pptk_rx_variant_count()-1)
  * and/or memory-policy flags for every later batch of this context; -1

@@ -101,6 +101,26 @@ class Oracle(_Lib):
                                    ctypes.c_int]
         L.orc_cksum_loop.restype = ctypes.c_uint32
         L.orc_cksum_loop.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint64]
+        L.orc_permit_batch.restype = None
+        L.orc_permit_batch.argtypes = [_vp, ctypes.c_size_t, ctypes.c_int, _vp, _vp, _vp]
+        L.orc_tokens_refill.restype = None
+        L.orc_tokens_refill.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_uint32]
+
+    def permit_batch(self, recs, family, subject, tokens):
+        """Sequential ip(v6)_permitted over records; returns (verdict,
+        tokens after)."""
+        recs = np.ascontiguousarray(recs)
+        tok = np.array(tokens, dtype=np.uint32)
+        subj = None if subject is None else np.ascontiguousarray(subject, dtype=np.uint8)
+        v = np.zeros(len(recs), dtype=np.uint8)
+        self.lib.orc_permit_batch(_ptr(recs), len(recs), family, _ptr(subj), _ptr(tok), _ptr(v))
+        return v, tok
+
+    def tokens_refill(self, tokens, start, end, add, initial):
+        tok = np.array(tokens, dtype=np.uint32)
+        self.lib.orc_tokens_refill(_ptr(tok), start, end, add, initial)
+        return tok
 
     def cksum(self, data):
         b = bytes(data)
@@ -163,6 +183,30 @@ class Reference(_Lib):
                                    ctypes.c_int, ctypes.c_int]
         L.ref_cksum_loop.restype = ctypes.c_uint32
         L.ref_cksum_loop.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint64]
+        L.ref_permit_batch.restype = None
+        L.ref_permit_batch.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint8,
+                                       _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]
+        L.ref_tokens_refill.restype = None
+        L.ref_tokens_refill.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_uint32, _vp]
+
+    def permit_batch(self, key, recs, family, bits, subject, hash_size, initial, tokens):
+        """The reference's ip_permitted / ipv6_permitted, once per subject
+        frame in frame order; returns (verdict, tokens after)."""
+        recs = np.ascontiguousarray(recs)
+        tok = np.array(tokens, dtype=np.uint32)
+        subj = None if subject is None else np.ascontiguousarray(subject, dtype=np.uint8)
+        v = np.zeros(len(recs), dtype=np.uint8)
+        self.lib.ref_permit_batch(bytes(key), _ptr(recs), len(recs), family, bits, _ptr(subj),
+                                  hash_size, initial, _ptr(tok), _ptr(v))
+        return v, tok
+
+    def tokens_refill(self, hash_size, batch_size, initial, add, k, tokens):
+        """The reference's batch_timer_fn for timer k (buckets
+        [k*batch_size, (k+1)*batch_size))."""
+        tok = np.array(tokens, dtype=np.uint32)
+        self.lib.ref_tokens_refill(hash_size, batch_size, initial, add, k, _ptr(tok))
+        return tok
 
     def cksum(self, data):
         b = bytes(data)

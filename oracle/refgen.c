@@ -345,3 +345,110 @@ uint32_t ref_cksum_loop(const uint8_t *buf, size_t sz, uint64_t iters)
   }
   return x;
 }
+
+/* ---- the reference's own rate limiter over a batch: ip_permitted /
+ * ipv6_permitted called once per subject frame in frame order on a struct
+ * ip_hash whose entries (tiny / small / full, chosen by initial_tokens as
+ * iphash.h:53-61 does) hold `tokens` (copied in, and back out after).  The
+ * source address comes from the record (its src bytes); the reference
+ * recomputes the bucket from it, so this pins the record's src_bucket too. */
+static void entries_alloc(struct ip_hash *h)
+{
+  if (use_tiny(h))
+    h->u.entries_tiny = calloc(h->hash_size, sizeof(*h->u.entries_tiny));
+  else if (use_small(h))
+    h->u.entries_small = calloc(h->hash_size, sizeof(*h->u.entries_small));
+  else
+    h->u.entries = calloc(h->hash_size, sizeof(*h->u.entries));
+}
+
+static void entries_set(struct ip_hash *h, const uint32_t *tokens)
+{
+  uint32_t i;
+  for (i = 0; i < h->hash_size; i++) {
+    if (use_tiny(h))
+      h->u.entries_tiny[i].tokens = (uint8_t)tokens[i];
+    else if (use_small(h))
+      h->u.entries_small[i].tokens = (uint16_t)tokens[i];
+    else
+      h->u.entries[i].tokens = tokens[i];
+  }
+}
+
+static void entries_get(struct ip_hash *h, uint32_t *tokens)
+{
+  uint32_t i;
+  for (i = 0; i < h->hash_size; i++) {
+    if (use_tiny(h))
+      tokens[i] = h->u.entries_tiny[i].tokens;
+    else if (use_small(h))
+      tokens[i] = h->u.entries_small[i].tokens;
+    else
+      tokens[i] = h->u.entries[i].tokens;
+  }
+}
+
+static void entries_free(struct ip_hash *h)
+{
+  if (use_tiny(h))
+    free(h->u.entries_tiny);
+  else if (use_small(h))
+    free(h->u.entries_small);
+  else
+    free(h->u.entries);
+}
+
+void ref_permit_batch(const uint8_t key[16], const struct pptk_rx_rec *recs, size_t n,
+                      int family, uint8_t bits, const uint8_t *subject,
+                      uint32_t hash_size, uint32_t initial_tokens, uint32_t *tokens,
+                      uint8_t *verdict)
+{
+  struct ip_hash h;
+  size_t i;
+  set_seed(key);
+  memset(&h, 0, sizeof(h));
+  h.hash_size = hash_size;
+  h.initial_tokens = initial_tokens;
+  entries_alloc(&h);
+  entries_set(&h, tokens);
+  for (i = 0; i < n; i++) {
+    const struct pptk_rx_rec *r = &recs[i];
+    const int v6 = (r->flags & PPTK_RX_F_IPV6) != 0;
+    if (!(r->flags & PPTK_RX_F_PARSED) || v6 != (family == 6) ||
+        (subject && !subject[i])) {
+      verdict[i] = 2;
+      continue;
+    }
+    if (v6)
+      verdict[i] = (uint8_t)ipv6_permitted(r->src, bits, &h);
+    else
+      verdict[i] = (uint8_t)ip_permitted(((uint32_t)r->src[0] << 24) | ((uint32_t)r->src[1] << 16) |
+                                         ((uint32_t)r->src[2] << 8) | r->src[3], bits, &h);
+  }
+  entries_get(&h, tokens);
+  entries_free(&h);
+}
+
+/* The reference's refill timer itself: ip_hash_init() registers
+ * batch_timer_fn for every batch_size buckets; as the timer loop would,
+ * take batch k's timer off the heap and run it. */
+void ref_tokens_refill(uint32_t hash_size, uint32_t batch_size, uint32_t initial_tokens,
+                       uint32_t timer_add, uint32_t k, uint32_t *tokens)
+{
+  struct ip_hash h;
+  struct timer_linkheap heap;
+  timer_linkheap_init(&heap);
+  memset(&h, 0, sizeof(h));
+  h.hash_size = hash_size;
+  h.batch_size = batch_size;
+  h.initial_tokens = initial_tokens;
+  h.timer_add = timer_add;
+  h.timer_period = 1000;
+  ip_hash_init(&h, &heap, NULL);
+  entries_set(&h, tokens);
+  timer_linkheap_remove(&heap, &h.timers[k]);
+  h.timers[k].fn(&h.timers[k], &heap, h.timers[k].userdata, NULL);
+  entries_get(&h, tokens);
+  ip_hash_free(&h, &heap);
+  timer_linkheap_free(&heap);
+}

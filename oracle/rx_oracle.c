@@ -458,3 +458,44 @@ uint32_t orc_cksum_loop(const uint8_t *buf, size_t sz, uint64_t iters)
     x ^= orc_cksum_buf(buf, sz) + (uint32_t)i;
   return x;
 }
+
+/* ---- ip_permitted / ipv6_permitted over a batch, one frame at a time in
+ * frame order (iphash/iphash.c:108-197: a bucket with 0 tokens denies, else
+ * it loses one and permits); the bucket is the record's src_bucket (the
+ * hash step, iphash.c:157-162 / :108-120, is checked by orc_rx_one).
+ * verdict: 1 permitted, 0 denied, 2 not a subject frame. */
+void orc_permit_batch(const struct pptk_rx_rec *recs, size_t n, int family,
+                      const uint8_t *subject, uint32_t *tokens, uint8_t *verdict)
+{
+  size_t i;
+  for (i = 0; i < n; i++) {
+    const struct pptk_rx_rec *r = &recs[i];
+    const int v6 = (r->flags & PPTK_RX_F_IPV6) != 0;
+    uint32_t *t;
+    if (!(r->flags & PPTK_RX_F_PARSED) || v6 != (family == 6) ||
+        (subject && !subject[i])) {
+      verdict[i] = 2;
+      continue;
+    }
+    t = &tokens[r->src_bucket];
+    if (*t == 0) {
+      verdict[i] = 0;
+      continue;
+    }
+    (*t)--;
+    verdict[i] = 1;
+  }
+}
+
+/* batch_timer_fn (iphash/iphash.c:290-350) for buckets [start, end). */
+void orc_tokens_refill(uint32_t *tokens, uint32_t start, uint32_t end,
+                       uint32_t add, uint32_t initial)
+{
+  uint32_t i;
+  for (i = start; i < end; i++) {
+    uint32_t t = tokens[i] + add;
+    if (t >= initial)
+      t = initial;
+    tokens[i] = t;
+  }
+}

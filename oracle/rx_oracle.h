@@ -42,5 +42,9 @@ int orc_rx_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
                  const struct orc_opts *o, struct pptk_rx_rec *recs,
                  int nthreads);
 uint32_t orc_cksum_loop(const uint8_t *buf, size_t sz, uint64_t iters);
+void orc_permit_batch(const struct pptk_rx_rec *recs, size_t n, int family,
+                      const uint8_t *subject, uint32_t *tokens, uint8_t *verdict);
+void orc_tokens_refill(uint32_t *tokens, uint32_t start, uint32_t end,
+                       uint32_t add, uint32_t initial);
 
 #endif

@@ -164,12 +164,12 @@ static int pick_variant(uint32_t span) {
   return RX_T64S2;
 }
 
-// Memory policy (PPTK_RX_TUNE_*).  Default: non-temporal frame loads and
-// record stores for the streaming variants (frames are read once, records
-// written once: measured 4.47 -> 4.25 ms on C1500 in one process, see
-// DESIGN.md "Measurement log"), plain for the small-frame variants (nt
-// measured slower on C64).  PPTK_RX_TUNE overrides for A/B runs.
-static uint32_t pick_tune(const pptk_rx_ctx *c, int variant) {
+// Memory policy (PPTK_RX_TUNE_*), from in-process A/B runs (DESIGN.md
+// "Measurement log"): non-temporal record stores always (C64 0.468 -> 0.463
+// ms, CMIX 3.05 -> 2.97 ms); non-temporal frame loads only for fixed-stride
+// batches with the streaming variants (C1500 4.47 -> 4.25 ms; they cost 14 %
+// on C64 and 10 % on offset-described CMIX).  PPTK_RX_TUNE overrides.
+static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
   static int tune = -2;
   if (tune == -2) {
     const char *e = getenv("PPTK_RX_TUNE");
@@ -178,7 +178,8 @@ static uint32_t pick_tune(const pptk_rx_ctx *c, int variant) {
   if (c->forced_flags >= 0) return (uint32_t)c->forced_flags;
   if (tune >= 0) return (uint32_t)tune;
   const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2;
-  return small ? 0u : 33u;
+  return (small || gather) ? PPTK_RX_TUNE_NT_STORES
+                           : (PPTK_RX_TUNE_NT_STORES | PPTK_RX_TUNE_NT_LOADS);
 }
 
 static int forced_variant(const pptk_rx_ctx *c) {
@@ -215,7 +216,7 @@ static uint64_t gcd64(uint64_t a, uint64_t b) {
 static int check_batch(const pptk_rx_ctx *c, const pptk_rx_dev_batch *b) {
   if (!c || !b) return -EINVAL;
   if (b->n == 0) return 0;
-  if (!b->d_frames || !b->d_recs) return -EINVAL;
+  if (!b->d_frames || (!b->d_recs && !b->d_recs32)) return -EINVAL;
   if (b->n > 0xffffffffull) return -EINVAL;  // indices are 32-bit (d_perm)
   if (!b->d_off && b->stride == 0 && b->n > 1) return -EINVAL;
   if (!b->d_len && b->fixed_len > 65535) return -EINVAL;
@@ -232,6 +233,7 @@ static RxKArgs batch_args(const pptk_rx_ctx *c, const pptk_rx_dev_batch *b) {
   a.fixed_len = b->fixed_len;
   a.n = b->n;
   a.recs = b->d_recs;
+  a.recs32 = b->d_recs32;
   a.hash = b->d_hash;
   return a;
 }
@@ -254,7 +256,7 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   const int fv = forced_variant(c);
   if (fv >= 0) variant = fv;
   RxKArgs a = batch_args(c, b);
-  a.tune = pick_tune(c, variant);
+  a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm);
   return hip_err(launch_rx(variant, a, grid_for(c, variant, b->n), (hipStream_t)stream));
 }
 
@@ -279,7 +281,7 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
     const int variant = fv >= 0 ? fv : kGroupVariant[g];
     a.range_lo = tab + g;
     a.range_hi = tab + (last ? kGroups : g + 1);
-    a.tune = pick_tune(c, variant);
+    a.tune = pick_tune(c, variant, true);
     e = launch_rx(variant, a, grid_for(c, variant, b->n), s);
     if (e != hipSuccess) return -EIO;
     if (last) break;
@@ -295,6 +297,43 @@ int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
 }
 
 int pptk_rx_variant_count(void) { return RX_NVARIANTS; }
+
+size_t pptk_rx_permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
+  if (hash_size == 0 || (hash_size & (hash_size - 1)) || n > 0xffffffffull) return 0;
+  return permit_scratch_bytes(n, hash_size);
+}
+
+int pptk_rx_permit_device(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs,
+                          const struct pptk_rx_rec32 *d_recs32, uint64_t n, int family,
+                          const uint8_t *d_subject, uint32_t *d_tokens, uint8_t *d_verdict,
+                          void *d_scratch, void *stream) {
+  if (!c || (family != 4 && family != 6) || n > 0xffffffffull) return -EINVAL;
+  if ((family == 4 && !c->opts.iphash_bits4) || (family == 6 && !c->opts.iphash_bits6))
+    return -EINVAL;   // the records carry no bucket for that family
+  const uint32_t hs = c->opts.iphash_size;
+  if (hs == 0 || (hs & (hs - 1))) return -EINVAL;
+  if (n == 0) return 0;
+  if ((!d_recs && !d_recs32) || !d_tokens || !d_verdict || !d_scratch) return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  PermitArgs a{};
+  a.recs = d_recs32 ? nullptr : d_recs;
+  a.recs32 = d_recs32;
+  a.n = n;
+  a.subject = d_subject;
+  a.tokens = d_tokens;
+  a.verdict = d_verdict;
+  a.hash_size = hs;
+  a.family = family;
+  return hip_err(launch_permit(a, d_scratch, (hipStream_t)stream));
+}
+
+int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *c, uint32_t *d_tokens, uint32_t start,
+                                 uint32_t end, uint32_t add, uint32_t initial_tokens,
+                                 void *stream) {
+  if (!c || !d_tokens || start > end || end > c->opts.iphash_size) return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  return hip_err(launch_refill(d_tokens, start, end, add, initial_tokens, (hipStream_t)stream));
+}
 
 size_t pptk_rx_bin_scratch_bytes(uint64_t n) { return bin_scratch_bytes(n, kBinGrid); }
 

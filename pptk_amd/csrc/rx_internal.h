@@ -16,6 +16,7 @@ struct RxKArgs {
   uint64_t stride;
   uint64_t n;
   pptk_rx_rec *recs;
+  pptk_rx_rec32 *recs32; // nullable: compact records instead of recs
   uint64_t *hash;        // nullable
   uint64_t k0, k1;       // SipHash key words (LE loads of key[0..7], key[8..15])
   uint64_t mask6_0, mask6_1;  // ipv6_permitted prefix mask over the 16 address bytes
@@ -68,5 +69,21 @@ hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm,
                       void *scratch, hipStream_t s, int grid);
 size_t bin_scratch_bytes(uint64_t n, int grid);
 const uint32_t *bin_table(const void *scratch, int grid);
+
+// Batched ip_permitted / ipv6_permitted (rx_permit.hip).
+struct PermitArgs {
+  const pptk_rx_rec *recs;      // one of recs / recs32
+  const pptk_rx_rec32 *recs32;
+  uint64_t n;
+  const uint8_t *subject;       // nullable: every parsed frame of the family
+  uint32_t *tokens;             // hash_size counters
+  uint8_t *verdict;             // 1 permitted, 0 denied, 2 not subject
+  uint32_t hash_size;
+  int family;                   // 4 or 6
+};
+size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size);
+hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t s);
+hipError_t launch_refill(uint32_t *tokens, uint32_t start, uint32_t end, uint32_t add,
+                         uint32_t initial, hipStream_t s);
 
 }  // namespace pptk

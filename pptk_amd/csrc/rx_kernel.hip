@@ -77,6 +77,10 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x) {
   }
 }
 
+// SipHash-2-4 on uint64_t state: 64-bit adds become one v_lshl_add_u64
+// each.  (A variant on 32-bit halves with add/add-carry pairs, which saves
+// the v_mov pairs that rotl-by-32 costs on aligned register pairs, measured
+// 3 % slower on C64 -- 0.488 vs 0.474 ms, same box, in-process A/B.)
 struct Sip {
   uint64_t v0, v1, v2, v3;
   __device__ __forceinline__ Sip(uint64_t k0, uint64_t k1)
@@ -512,6 +516,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
 
     // ---- lane phase: frame `lane` -> record (parsed once per frame)
     const bool stage = !(GATHER && a.perm) && !(a.tune & 2u);
+    const bool c32 = a.recs32 != nullptr;   // compact 32-byte records
     // tune bit 4 (diagnostics only, output invalid): skip the lane phase
     if (dc.idx != 0xffffffffu && !(a.tune & 16u)) {
       const int m = (int)(dc.base & 15);
@@ -609,33 +614,50 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
       w[15] = p.et | (p.ver << 16);
       if (a.hash)
         a.hash[dc.idx] = fh;
-      const u32x4 r0 = {w[0], w[1], w[2], w[3]}, r1 = {w[4], w[5], w[6], w[7]};
-      const u32x4 r2 = {w[8], w[9], w[10], w[11]}, r3 = {w[12], w[13], w[14], w[15]};
+      u32x4 r0, r1, r2, r3;
+      if (c32) {   // struct pptk_rx_rec32: a projection of the same words
+        const bool v6 = flags & PPTK_RX_F_IPV6;
+        r0 = (u32x4){w[0], w[1], v6 ? 0u : w[2], v6 ? 0u : w[6]};
+        r1 = (u32x4){w[10], (w[13] >> 16) | (((w[13] >> 8) & 0xffu) << 16) | (w[13] << 24),
+                     w[12], w[14]};
+        r2 = r3 = (u32x4){0u, 0u, 0u, 0u};
+      } else {
+        r0 = (u32x4){w[0], w[1], w[2], w[3]};
+        r1 = (u32x4){w[4], w[5], w[6], w[7]};
+        r2 = (u32x4){w[8], w[9], w[10], w[11]};
+        r3 = (u32x4){w[12], w[13], w[14], w[15]};
+      }
       if (!stage) {  // permuted order: records scatter, store per lane
-        u32x4 *dst = (u32x4 *)((uint8_t *)a.recs + (uint64_t)dc.idx * 64u);
-        dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
+        u32x4 *dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + (uint64_t)dc.idx * 32u
+                                   : (uint8_t *)a.recs + (uint64_t)dc.idx * 64u);
+        dst[0] = r0; dst[1] = r1;
+        if (!c32) { dst[2] = r2; dst[3] = r3; }
       } else {
         // park the record in LDS (every lane's image reads are behind us in
         // program order) for the coalesced store below
         u32x4 *st = (u32x4 *)wimg + lane * 5;   // 80-byte pitch
-        st[0] = r0; st[1] = r1; st[2] = r2; st[3] = r3;
+        st[0] = r0; st[1] = r1;
+        if (!c32) { st[2] = r2; st[3] = r3; }
       }
     }
     if (stage && !(a.tune & 8u)) {   // tune bit 3 (diagnostics only): no record stores
-      // identity order: the tile's 64 records are one contiguous 4 KB run;
-      // each store instruction writes 1 KB contiguously instead of 64
-      // scattered 16-byte pieces
+      // identity order: the tile's 64 records are one contiguous 4 KB run
+      // (2 KB compact); each store instruction writes 1 KB contiguously
+      // instead of 64 scattered 16-byte pieces
       __builtin_amdgcn_wave_barrier();
       const u32x4 *st = (const u32x4 *)wimg;
-      u32x4 *dst = (u32x4 *)((uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
+      u32x4 *dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + tile * (uint64_t)WAVE * 32u
+                                 : (uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
       const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
-      const int kmax = (a.tune & 128u) ? 2 : 4;   // bit 7: diagnostics, half the bytes
+      const int lg = c32 ? 1 : 2;                 // log2 16-byte pieces per record
+      int kmax = c32 ? 2 : 4;
+      if (a.tune & 128u) kmax >>= 1;              // bit 7: diagnostics, half the bytes
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int e = k * WAVE + lane;   // 16-byte piece e of the tile's records
-        const int r = e >> 2;
+        const int r = e >> lg;
         if ((uint64_t)r < nrec && k < kmax) {
-          const u32x4 val = st[r * 5 + (e & 3)];
+          const u32x4 val = st[r * 5 + (e & ((1 << lg) - 1))];
           if (a.tune & 64u) {            // bit 6: write-through, drop from L2 (sc1)
             uint64_t *d8 = (uint64_t *)(dst + e);
             __hip_atomic_store(d8, (uint64_t)val.x | ((uint64_t)val.y << 32), __ATOMIC_RELAXED,

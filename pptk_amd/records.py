@@ -1,5 +1,6 @@
-"""Record format of the rx transform: numpy view of ``struct pptk_rx_rec``
-(include/pptk_rx.h).  64 bytes per frame, little-endian."""
+"""Record formats of the rx transform: numpy views of ``struct pptk_rx_rec``
+(64 bytes per frame) and ``struct pptk_rx_rec32`` (32 bytes), little-endian
+(include/pptk_rx.h)."""
 import numpy as np
 
 REC_DTYPE = np.dtype([
@@ -22,6 +23,21 @@ REC_DTYPE = np.dtype([
 ])
 assert REC_DTYPE.itemsize == 64
 
+REC32_DTYPE = np.dtype([
+    ("flow_hash", "<u8"),
+    ("src4", "u1", 4),
+    ("dst4", "u1", 4),
+    ("sport", "<u2"),
+    ("dport", "<u2"),
+    ("flags", "<u2"),
+    ("proto", "u1"),
+    ("l3_off", "u1"),
+    ("l4_off", "<u2"),
+    ("l4_len", "<u2"),
+    ("src_bucket", "<u4"),
+])
+assert REC32_DTYPE.itemsize == 32
+
 F_PARSED = 0x0001
 F_IP_OK = 0x0002
 F_L4_OK = 0x0004
@@ -40,20 +56,35 @@ def as_records(raw):
     return raw.view(np.uint8).reshape(-1).view(REC_DTYPE)
 
 
-def diff_records(got, want, limit=5):
+def to_rec32(recs):
+    """The compact record the kernel writes for each full record: the same
+    values, IPv6 addresses left out (src4/dst4 = 0)."""
+    r = as_records(recs)
+    out = np.zeros(len(r), dtype=REC32_DTYPE)
+    v4 = (r["flags"] & F_IPV6) == 0
+    for f in ("flow_hash", "sport", "dport", "flags", "proto", "l3_off", "l4_off", "l4_len",
+              "src_bucket"):
+        out[f] = r[f]
+    out["src4"] = np.where(v4[:, None], r["src"][:, :4], 0)
+    out["dst4"] = np.where(v4[:, None], r["dst"][:, :4], 0)
+    return out
+
+
+def diff_records(got, want, limit=5, dtype=REC_DTYPE):
     """Return a human-readable description of the first mismatching records
     (empty string when identical byte for byte)."""
-    g = np.ascontiguousarray(got).view(np.uint8).reshape(-1, 64)
-    w = np.ascontiguousarray(want).view(np.uint8).reshape(-1, 64)
+    rb = dtype.itemsize
+    g = np.ascontiguousarray(got).view(np.uint8).reshape(-1, rb)
+    w = np.ascontiguousarray(want).view(np.uint8).reshape(-1, rb)
     if g.shape != w.shape:
         return f"shape mismatch {g.shape} vs {w.shape}"
     bad = np.nonzero((g != w).any(axis=1))[0]
     if bad.size == 0:
         return ""
     lines = [f"{bad.size} of {g.shape[0]} records differ"]
-    gr, wr = g.view(REC_DTYPE).reshape(-1), w.view(REC_DTYPE).reshape(-1)
+    gr, wr = g.view(dtype).reshape(-1), w.view(dtype).reshape(-1)
     for i in bad[:limit]:
-        fields = [n for n in REC_DTYPE.names
+        fields = [n for n in dtype.names
                   if not np.array_equal(gr[i][n], wr[i][n])]
         lines.append(f"  rec {i}: fields {fields}: got "
                      + ", ".join(f"{n}={gr[i][n]}" for n in fields)

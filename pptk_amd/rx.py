@@ -27,7 +27,8 @@ class RxDevBatch(ctypes.Structure):
                 ("d_len", ctypes.c_void_p), ("d_perm", ctypes.c_void_p),
                 ("stride", ctypes.c_uint64), ("fixed_len", ctypes.c_uint32),
                 ("max_len", ctypes.c_uint32), ("n", ctypes.c_uint64),
-                ("d_recs", ctypes.c_void_p), ("d_hash", ctypes.c_void_p)]
+                ("d_recs", ctypes.c_void_p), ("d_hash", ctypes.c_void_p),
+                ("d_recs32", ctypes.c_void_p)]
 
 
 class LdpPacket(ctypes.Structure):
@@ -43,6 +44,8 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_batch", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
+           "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
+           "pptk_rx_tokens_refill_device",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
@@ -73,8 +76,18 @@ def lib(path=None):
         L.pptk_rx_bin_scratch_bytes.restype = ctypes.c_size_t
         L.pptk_rx_bin_device.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp]
         L.pptk_rx_bin_device.restype = ctypes.c_int
-        L.pptk_rx_batch_device_mixed.argtypes = [vp, ctypes.POINTER(RxDevBatch), vp, vp, vp]
-        L.pptk_rx_batch_device_mixed.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_permit_device"):        # absent from older A/B builds
+            L.pptk_rx_permit_scratch_bytes.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+            L.pptk_rx_permit_scratch_bytes.restype = ctypes.c_size_t
+            L.pptk_rx_permit_device.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp,
+                                                vp, vp, vp, vp]
+            L.pptk_rx_permit_device.restype = ctypes.c_int
+            L.pptk_rx_tokens_refill_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32,
+                                                       ctypes.c_uint32, ctypes.c_uint32, vp]
+            L.pptk_rx_tokens_refill_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_batch_device_mixed"):   # absent from older A/B builds
+            L.pptk_rx_batch_device_mixed.argtypes = [vp, ctypes.POINTER(RxDevBatch), vp, vp, vp]
+            L.pptk_rx_batch_device_mixed.restype = ctypes.c_int
         L.pptk_rx_version.restype = ctypes.c_char_p
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
@@ -137,17 +150,21 @@ class RxContext:
             pass
 
     def batch_device(self, frames, n, off=None, lens=None, stride=0, fixed_len=0,
-                     perm=None, recs=None, hash_out=None, max_len=0, stream=None):
+                     perm=None, recs=None, hash_out=None, max_len=0, stream=None,
+                     compact=False):
         """Asynchronous device batch on `stream` (torch stream or None = current).
-        frames/off/lens/perm/recs/hash_out are torch CUDA tensors."""
+        frames/off/lens/perm/recs/hash_out are torch CUDA tensors; compact:
+        32-byte struct pptk_rx_rec32 records (recs is (n, 32) bytes)."""
         import torch
+        rb = 32 if compact else 64
         if recs is None:
-            recs = torch.empty((n, 64), dtype=torch.uint8, device=frames.device)
+            recs = torch.empty((n, rb), dtype=torch.uint8, device=frames.device)
         b = RxDevBatch(frames.data_ptr(), None if off is None else off.data_ptr(),
                        None if lens is None else lens.data_ptr(),
                        None if perm is None else perm.data_ptr(), stride, fixed_len,
-                       max_len, n, recs.data_ptr(),
-                       None if hash_out is None else hash_out.data_ptr())
+                       max_len, n, None if compact else recs.data_ptr(),
+                       None if hash_out is None else hash_out.data_ptr(),
+                       recs.data_ptr() if compact else None)
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
         rc = self._L.pptk_rx_batch_device(self._ctx, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
@@ -175,6 +192,35 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch_device_mixed failed ({rc})")
         return recs
+
+    def permit_device(self, recs, family, tokens, subject=None, compact=False, verdict=None,
+                      scratch=None, stream=None):
+        """Batched ip(v6)_permitted over device records (torch uint8 (n, 64)
+        or (n, 32) with compact); tokens: torch int32 (iphash_size) updated
+        in place; returns the uint8 verdicts (1 permit, 0 deny, 2 n/a)."""
+        import torch
+        n = recs.shape[0]
+        if verdict is None:
+            verdict = torch.empty(n, dtype=torch.uint8, device=recs.device)
+        if scratch is None:
+            scratch = torch.empty(self._L.pptk_rx_permit_scratch_bytes(n, tokens.numel()),
+                                  dtype=torch.uint8, device=recs.device)
+        s = stream if stream is not None else torch.cuda.current_stream(recs.device)
+        rc = self._L.pptk_rx_permit_device(self._ctx, None if compact else _dp(recs),
+                                           _dp(recs) if compact else None, n, family,
+                                           _dp(subject), _dp(tokens), _dp(verdict),
+                                           _dp(scratch), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_permit_device failed ({rc})")
+        return verdict
+
+    def tokens_refill_device(self, tokens, start, end, add, initial, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(tokens.device)
+        rc = self._L.pptk_rx_tokens_refill_device(self._ctx, _dp(tokens), start, end, add,
+                                                  initial, ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_tokens_refill_device failed ({rc})")
 
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""

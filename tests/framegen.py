@@ -112,7 +112,7 @@ def frame_v4(rng, proto, total, vlan=None, ihl_words=5, corrupt=None,
     return bytes(f)
 
 
-def frame_v6(rng, proto, total, vlan=None, ext=None, corrupt=None):
+def frame_v6(rng, proto, total, vlan=None, ext=None, corrupt=None, src=None):
     """IPv6 frame; ext = list of (type, bytes) extension headers."""
     l2 = eth(ETH_IP6, vlan)
     ext = ext or []
@@ -123,7 +123,8 @@ def frame_v6(rng, proto, total, vlan=None, ext=None, corrupt=None):
     l4min = 20 if proto == 6 else 8
     l4len = total - len(l2) - 40 - len(exth)
     assert l4len >= l4min
-    src = bytes([0x20, 0x01, 0x0d, 0xb8]) + bytes(rng.integers(0, 256, 12, dtype=np.uint8))
+    if src is None:
+        src = bytes([0x20, 0x01, 0x0d, 0xb8]) + bytes(rng.integers(0, 256, 12, dtype=np.uint8))
     dst = bytes([0xfd]) + bytes(rng.integers(0, 256, 15, dtype=np.uint8))
     sp, dp = (int(x) for x in rng.integers(0, 65536, 2))
     payload = bytes(rng.integers(0, 256, l4len - l4min, dtype=np.uint8))
@@ -367,4 +368,33 @@ def gen_fuzz(n, seed=0xF022):
         if rng.random() < 0.2:
             f = f[:int(rng.integers(0, len(f) + 1))]
         frames.append(bytes(f))
+    return pack(frames)
+
+
+def gen_permit(n=3000, seed=0x9E7):
+    """Rate-limiter workload: frames from few source prefixes (20 IPv4 /24s,
+    8 IPv6 /48s) so that token buckets see long runs, in random order, with a
+    few non-IP and malformed frames mixed in."""
+    rng = np.random.default_rng(seed)
+    v4_nets = [bytes([10, int(a), int(b)]) for a, b in rng.integers(0, 256, (20, 2))]
+    v6_nets = [bytes([0x20, 0x01, 0x0d, 0xb8]) + bytes(rng.integers(0, 256, 2, dtype=np.uint8))
+               for _ in range(8)]
+    weights = rng.random(20) ** 3
+    weights /= weights.sum()
+    frames = []
+    for _ in range(n):
+        u = rng.random()
+        proto = 6 if rng.random() < 0.5 else 17
+        if u < 0.65:
+            net = v4_nets[int(rng.choice(20, p=weights))]
+            src = net + bytes([int(rng.integers(0, 256))])
+            frames.append(frame_v4(rng, proto, int(rng.integers(64, 200)), src=src))
+        elif u < 0.95:
+            net = v6_nets[int(rng.integers(0, 8))]
+            src = net + bytes(rng.integers(0, 256, 10, dtype=np.uint8))
+            frames.append(frame_v6(rng, proto, int(rng.integers(90, 200)), src=src))
+        elif u < 0.98:
+            frames.append(eth(0x0806) + bytes(46))     # ARP: not IP
+        else:
+            frames.append(frame_v4(rng, 17, 64)[:30])  # runt: malformed
     return pack(frames)

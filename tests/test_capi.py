@@ -127,12 +127,17 @@ def test_c_dropin_program(tmp_path):
     assert "capi_dropin ok" in out.stdout
 
 
-def test_record_layout_matches_header():
-    from pptk_amd.records import REC_DTYPE
+@pytest.mark.parametrize("struct,dtname", [("pptk_rx_rec", "REC_DTYPE"),
+                                            ("pptk_rx_rec32", "REC32_DTYPE")])
+def test_record_layout_matches_header(struct, dtname):
+    import pptk_amd.records as R
+    dt = getattr(R, dtname)
     txt = open(os.path.join(INCLUDE, "pptk_rx.h")).read()
-    for name in REC_DTYPE.names:
-        off = REC_DTYPE.fields[name][1]
-        m = re.search(rf"\b{name}(\[\d+\])?;\s*/\*\s*(\d+)", txt)
+    body = txt[txt.index(f"struct {struct} {{"):]
+    body = body[:body.index("};")]
+    for name in dt.names:
+        off = dt.fields[name][1]
+        m = re.search(rf"\b{name}(\[\d+\])?;\s*/\*\s*(\d+)", body)
         assert m and int(m.group(2)) == off, name
 
 

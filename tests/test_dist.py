@@ -66,3 +66,41 @@ def test_shard_range_partitions(n, world):
     for (f0, c0), (f1, _) in zip(got, got[1:]):
         assert f0 + c0 == f1
     assert sum(c for _, c in got) == n
+
+
+def _bench_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cpu")
+        bench.barrier(world, dev)
+        mx = bench.max_over_ranks(float(rank + 1), world, dev)
+        sm = bench.sum_over_ranks(float(rank + 1), world, dev)
+        g = bench.gather_bench(1024, world, dev, 3)
+        if rank == 0:
+            q.put((mx, sm, g))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_multi_rank_helpers():
+    """bench.py's N > 1 bookkeeping (barrier, max/sum over ranks, the
+    all-gather timing and its bus-bandwidth arithmetic) on gloo, world 2."""
+    world, port = 2, 30600 + (os.getpid() % 1000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    mx, sm, g = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert mx == 2.0 and sm == 3.0
+    assert g["bytes_per_rank"] == 1024 * 8 and g["ms"] > 0
+    assert abs(g["busbw_gbs"] - g["algbw_gbs"] / 2) <= 0.1 + 1e-9

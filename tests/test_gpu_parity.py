@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN_SETS, load_golden
-from pptk_amd.records import F_PARSED, as_records, diff_records
+from pptk_amd.records import F_PARSED, REC32_DTYPE, as_records, diff_records, to_rec32
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +33,7 @@ def _upload(buf, dev, shift=0):
 
 
 def _run(ctx, z, dev, shift=0, perm=False, hash_out=False, max_len=None,
-         stride=None):
+         stride=None, compact=False):
     buf, off, lens = z["buf"], z["off"], z["len"]
     n = len(off)
     _keep, frames = _upload(buf, dev, shift)
@@ -49,7 +49,7 @@ def _run(ctx, z, dev, shift=0, perm=False, hash_out=False, max_len=None,
         kw["fixed_len"] = int(lens[0])
     p = ctx.bin_device(lens_t, n) if perm else None
     h = torch.full((n,), -1, dtype=torch.int64, device=dev) if hash_out else None
-    recs = ctx.batch_device(frames, n, perm=p, hash_out=h, **kw)
+    recs = ctx.batch_device(frames, n, perm=p, hash_out=h, compact=compact, **kw)
     torch.cuda.synchronize()
     out = recs.cpu().numpy().reshape(-1)
     if hash_out:
@@ -94,6 +94,26 @@ def test_every_forced_variant(name, dev):
         if name in ("c64", "c1500"):
             got = _run(ctx, z, dev, shift=3, stride=64 if name == "c64" else 1500)
             d = diff_records(got, z["recs"])
+            assert not d, f"variant {v} fixed stride: {d}"
+
+
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_compact_records(name, dev):
+    """d_recs32: the 32-byte record is the projection of the full one, in
+    every variant, identity and binned order, offsets and fixed stride."""
+    from pptk_amd.rx import lib
+    z = load_golden(name)
+    want = to_rec32(z["recs"])
+    ctx = _ctx(z)
+    for v in list(range(lib().pptk_rx_variant_count())) + [-1]:
+        ctx.set_tuning(v, -1 if v < 0 else (v % 4) | 32)
+        for shift, perm in ((0, False), (9, False), (3, True)):
+            got = _run(ctx, z, dev, shift=shift, perm=perm, compact=True)
+            d = diff_records(got, want, dtype=REC32_DTYPE)
+            assert not d, f"variant {v} shift {shift} perm {perm}: {d}"
+        if name in ("c64", "c1500"):
+            got = _run(ctx, z, dev, shift=5, stride=64 if name == "c64" else 1500, compact=True)
+            d = diff_records(got, want, dtype=REC32_DTYPE)
             assert not d, f"variant {v} fixed stride: {d}"
 
 

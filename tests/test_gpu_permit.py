@@ -1,0 +1,127 @@
+"""Batched ip_permitted / ipv6_permitted on the GPU (pptk_rx_permit_device,
+pptk_rx_tokens_refill_device) against the reference's own rate limiter
+(tests/golden/permit.npz, made by calling ip_permitted once per frame in
+frame order) and, for long chains and large batches, against the C
+restatement pinned to it (tests/test_oracle.py).  Needs an MI355X."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from pptk_amd.records import REC32_DTYPE, REC_DTYPE, diff_records, to_rec32
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def _ctx(z):
+    from pptk_amd.rx import RxContext
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    return RxContext(0, z["key"].tobytes(), b4, b6, hs)
+
+
+def _gpu_records(ctx, z, dev, compact=False):
+    frames = torch.zeros(z["buf"].size + 64, dtype=torch.uint8, device=dev)
+    frames[:z["buf"].size] = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    recs = ctx.batch_device(frames, len(z["off"]), off=off, lens=lens, max_len=int(z["len"].max()),
+                            compact=compact)
+    torch.cuda.synchronize()
+    return recs
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_permit_matches_reference(compact, dev):
+    """Records from the GPU rx transform, then the GPU rate limiter: every
+    verdict and every bucket's tokens as the reference's per-frame calls."""
+    z = load_golden("permit")
+    ctx = _ctx(z)
+    recs = _gpu_records(ctx, z, dev, compact)
+    want = z["recs"].reshape(-1).view(REC_DTYPE)
+    got = recs.cpu().numpy().reshape(-1)
+    d = (diff_records(got, to_rec32(want), dtype=REC32_DTYPE) if compact
+         else diff_records(got, want))
+    assert not d, d
+    for k, (fam, init, has_subj) in enumerate(z["case_meta"]):
+        tok = torch.from_numpy(z["case_tok_in"][k].view(np.int32).copy()).to(dev)
+        subj = torch.from_numpy(z["case_subject"][k]).to(dev) if has_subj else None
+        v = ctx.permit_device(recs, int(fam), tok, subject=subj, compact=compact)
+        torch.cuda.synchronize()
+        assert np.array_equal(v.cpu().numpy(), z["case_verdict"][k]), (fam, init, has_subj)
+        assert np.array_equal(tok.cpu().numpy().view(np.uint32), z["case_tok_out"][k])
+
+
+def test_refill_matches_reference(dev):
+    z = load_golden("permit")
+    ctx = _ctx(z)
+    for (init, add, lo, hi), tin, tout in zip(z["refill_meta"], z["refill_in"], z["refill_out"]):
+        tok = torch.from_numpy(tin.view(np.int32).copy()).to(dev)
+        ctx.tokens_refill_device(tok, int(lo), int(hi), int(add), int(init))
+        torch.cuda.synchronize()
+        assert np.array_equal(tok.cpu().numpy().view(np.uint32), tout)
+
+
+def test_permit_chain_with_refills(dev):
+    """Five batches with timer refills in between, one token array carried
+    through: identical to the frame-by-frame restatement."""
+    from oracle.oracle import Oracle
+    z = load_golden("permit")
+    ctx = _ctx(z)
+    recs = _gpu_records(ctx, z, dev)
+    host = z["recs"].reshape(-1).view(REC_DTYPE)
+    O = Oracle()
+    hs, init = int(z["iphash"][2]), 40
+    tok_h = np.full(hs, init, np.uint32)
+    tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
+    n = len(host)
+    cuts = [0, 100, 900, 1500, 2999, n]
+    for step, (a, b) in enumerate(zip(cuts, cuts[1:])):
+        v = ctx.permit_device(recs[a:b], 4 if step % 2 == 0 else 6, tok)
+        vh, tok_h = O.permit_batch(host[a:b], 4 if step % 2 == 0 else 6, None, tok_h)
+        torch.cuda.synchronize()
+        assert np.array_equal(v.cpu().numpy(), vh), step
+        lo = (step * 16) % hs
+        ctx.tokens_refill_device(tok, lo, lo + 16, 3, init)
+        tok_h = O.tokens_refill(tok_h, lo, lo + 16, 3, init)
+        torch.cuda.synchronize()
+        assert np.array_equal(tok.cpu().numpy().view(np.uint32), tok_h), step
+
+
+def test_permit_large_skewed_batch(dev):
+    """1 M synthetic records, Zipf-skewed buckets (one bucket holds ~10 % of
+    the frames), 2^16 buckets: GPU == frame-by-frame restatement."""
+    from oracle.oracle import Oracle
+    from pptk_amd.records import F_IPV6, F_PARSED
+    rng = np.random.default_rng(11)
+    n, hs = 1 << 20, 1 << 16
+    r = np.zeros(n, dtype=REC_DTYPE)
+    r["flags"] = np.where(rng.random(n) < 0.97, F_PARSED, 0) | np.where(rng.random(n) < 0.2,
+                                                                        F_IPV6, 0)
+    r["src_bucket"] = np.minimum(rng.zipf(1.3, n) - 1, hs - 1)
+    tok_h = rng.integers(0, 500, hs).astype(np.uint32)
+    subj = (rng.random(n) < 0.9).astype(np.uint8)
+    ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+    recs = torch.from_numpy(r.view(np.uint8).reshape(n, 64)).to(dev)
+    tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
+    v = ctx.permit_device(recs, 4, tok, subject=torch.from_numpy(subj).to(dev))
+    vh, th = Oracle().permit_batch(r, 4, subj, tok_h)
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), vh)
+    assert np.array_equal(tok.cpu().numpy().view(np.uint32), th)
+    assert (vh == 0).sum() > 1000 and (vh == 1).sum() > 1000
+
+
+def test_permit_rejects_disabled_family(dev):
+    from pptk_amd.rx import RxContext
+    ctx = RxContext(0, bytes(16), 24, 0, 64)
+    recs = torch.zeros((4, 64), dtype=torch.uint8, device=dev)
+    tok = torch.zeros(64, dtype=torch.int32, device=dev)
+    with pytest.raises(OSError):
+        ctx.permit_device(recs, 6, tok)
