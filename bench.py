@@ -104,12 +104,12 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
 
     work = [None]
 
-    def step(k):
+    def step(k, collective=True):
         # the dense flow-hash array only feeds the all-gather (N > 1); at
         # N = 1 the records (which carry flow_hash) are the whole output
         h = hbuf[k & 1] if gout is not None else None
         ctx.batch_device(b["frames"], n, recs=recs, hash_out=h, compact=compact, **kw)
-        if gout is not None:
+        if gout is not None and collective:
             if work[0] is not None:
                 work[0].wait()                  # previous gather done before reuse
             _, work[0] = allgather_flow_hash(h, gout, async_op=True)
@@ -117,11 +117,13 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     # settle: clocks ramp up over the first few hundred ms of sustained
     # load (the kernel trace shows the first launches 4-5 % slower, and a
     # cold first process up to 20 %); run until `settle` seconds have passed
-    # before the W warmup steps, so the K timed steps see steady state
+    # before the W warmup steps, so the K timed steps see steady state.  The
+    # settle launches issue no collective: their number depends on each
+    # rank's clock, and ranks must issue the same sequence of all-gathers.
     t_settle = time.perf_counter()
     k = 0
     while time.perf_counter() - t_settle < settle:
-        step(k)
+        step(k, collective=False)
         k += 1
         if k % 16 == 0:
             torch.cuda.synchronize(dev)
@@ -298,6 +300,37 @@ def cpu_baseline_small(b, seconds=4.0, sample=1 << 20):
             "single_thread_mpkts": round(st, 3)}
 
 
+def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
+    """Batched ip_permitted over the records of a C64
+    batch: buckets of the /24 source prefixes in 2^16 buckets, every IPv4
+    frame a subject, one token array carried across the timed batches."""
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    b = make_batch("c64", n, dev, first=rank * n)
+    ctx = RxContext(dev.index, KEY, 24, 0, hash_size)
+    recs = ctx.batch_device(b["frames"], n, stride=b["stride"], fixed_len=b["fixed_len"])
+    del b
+    tok = torch.full((hash_size,), 1 << 20, dtype=torch.int32, device=dev)
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    scratch = torch.empty(ctx._L.pptk_rx_permit_scratch_bytes(n, hash_size), dtype=torch.uint8,
+                          device=dev)
+    for _ in range(warmup):
+        ctx.permit_device(recs, 4, tok, verdict=verdict, scratch=scratch)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for a, z in ev:
+        a.record()
+        ctx.permit_device(recs, 4, tok, verdict=verdict, scratch=scratch)
+        z.record()
+    torch.cuda.synchronize(dev)
+    ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
+    return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "ms_per_batch": round(ms, 4),
+            "frames": n, "hash_size": hash_size,
+            "workload": "C64 records, IPv4 /24 buckets, all frames subject"}
+
+
 def gather_bench(n, ws, dev, steps):
     """All-gather of n u64 flow hashes per rank alone: time,
     algorithmic and bus bandwidth (RCCL convention: bus = alg * (ws-1)/ws)."""
@@ -347,6 +380,8 @@ def main():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--only", default=None, help="run just this config (profiling)")
+    ap.add_argument("--no-rec32", action="store_true",
+                    help="skip the compact-record runs (profiling: one record format per trace)")
     ap.add_argument("--no-membench", action="store_true",
                     help="skip the in-process HBM read/copy ceiling probe")
     ap.add_argument("--settle", type=float, default=SETTLE_S,
@@ -401,11 +436,13 @@ def main():
                 "kernel_ms": round(kernel_ms, 4)}
 
     # the same batch with compact 32-byte records (struct pptk_rx_rec32)
-    r32 = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check,
-                     args.settle, compact=True, batch=prim["_batch"])
-    rec32 = summary(r32, n)
-    del r32["_batch"], r32["_recs"]
-    log(f"[rank {rank}] {primary_cfg} rec32: {rec32['value']} Mpkts/s")
+    rec32 = None
+    if not args.no_rec32:
+        r32 = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False,
+                         check, args.settle, compact=True, batch=prim["_batch"])
+        rec32 = summary(r32, n)
+        del r32["_batch"], r32["_recs"]
+        log(f"[rank {rank}] {primary_cfg} rec32: {rec32['value']} Mpkts/s")
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu and primary_cfg == "c1500":
@@ -422,7 +459,7 @@ def main():
             r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check,
                            args.settle)
             secondary[cfg] = summary(r, n)
-            if cfg == "c64":
+            if cfg == "c64" and not args.no_rec32:
                 r32 = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False,
                                  check, args.settle, compact=True, batch=r["_batch"])
                 secondary[cfg]["rec32"] = summary(r32, n)
@@ -432,6 +469,11 @@ def main():
                     r["_batch"], seconds=max(1.0, args.cpu_seconds / 2.5))
             del r["_batch"], r["_recs"]
             torch.cuda.empty_cache()
+
+    permit = None
+    if not args.no_secondary and args.only is None:
+        permit = permit_bench(n, dev, ws, rank, args.steps, args.warmup)
+        log(f"[rank {rank}] permit: {permit}")
 
     if rank == 0:
         line = {
@@ -460,6 +502,7 @@ def main():
             "box_hbm": box,
             "parity": {"full_batch": full_check, "oracle_sample": sample_check},
             "secondary": secondary,
+            "permit": permit,
         }
         print(json.dumps(line), flush=True)
     if ws > 1:

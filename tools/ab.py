@@ -4,7 +4,8 @@ on one batch.
     python tools/ab.py c1500 3:1 3:0 6:1 ...        (variant:flags pairs)
     AB_LIBS=old=build/ab_old/libpptkrx.so python tools/ab.py cmix 3:33 old:3:33
 
-A setting is [lib:]variant:flags; variant or flags -1 = automatic choice;
+A setting is [lib:]variant:flags[:c]; variant or flags -1 = automatic choice;
+a trailing :c writes compact 32-byte records;
 lib names come from AB_LIBS (name=path,...), default = pptk_amd/libpptkrx.so.
 Generates the batch once, then times every setting in interleaved rounds
 (A B C A B C ...) so that clock and thermal drift hit all settings alike;
@@ -23,10 +24,14 @@ sys.path.insert(0, ROOT)
 
 
 def parse_setting(a):
+    """[lib:]variant:flags[:c] -> (lib, variant, flags, compact)."""
     p = a.split(":")
+    compact = p[-1] == "c"
+    if compact:
+        p = p[:-1]
     if len(p) == 2:
-        return ("", int(p[0]), int(p[1]))
-    return (p[0], int(p[1]), int(p[2]))
+        return ("", int(p[0]), int(p[1]), compact)
+    return (p[0], int(p[1]), int(p[2]), compact)
 
 
 def main():
@@ -48,7 +53,8 @@ def main():
     b = make_batch(cfg, n, dev)
     kw = (dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]) if "off" in b
           else dict(stride=b["stride"], fixed_len=b["fixed_len"]))
-    recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    recs64 = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    recs32 = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     ctxs = {k: RxContext(0, bytes(range(1, 17)), lib_path=v) for k, v in libs.items()}
 
     mixed = bool(os.environ.get("AB_MIXED")) and "off" in b
@@ -57,32 +63,35 @@ def main():
         scratch = torch.empty(ctxs[""]._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
                               device=dev)
 
-    def launch(ctx):
+    def launch(ctx, compact):
+        recs = recs32 if compact else recs64
         if mixed:
-            ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], recs=recs,
+            ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], recs=recs64,
                                    max_len=b["max_len"], perm=perm, scratch=scratch)
         elif binned and "off" in b:
-            ctx.batch_device(b["frames"], n, recs=recs, perm=ctx.bin_device(b["lens"], n), **kw)
+            ctx.batch_device(b["frames"], n, recs=recs, perm=ctx.bin_device(b["lens"], n),
+                             compact=compact, **kw)
         else:
-            ctx.batch_device(b["frames"], n, recs=recs, **kw)
+            ctx.batch_device(b["frames"], n, recs=recs, compact=compact, **kw)
 
-    ref = None
+    ref = {}
     times = {s: [] for s in settings}
     same = {}
     for _ in range(rounds):
         for s in settings:
             ctx = ctxs[s[0]]
             ctx.set_tuning(s[1], s[2])
-            launch(ctx)
+            launch(ctx, s[3])
             torch.cuda.synchronize()
             if s not in same:       # every setting must give the same records
-                if ref is None:
-                    ref = recs.clone()
-                same[s] = bool(torch.equal(recs, ref))
+                r = recs32 if s[3] else recs64
+                if s[3] not in ref:
+                    ref[s[3]] = r.clone()
+                same[s] = bool(torch.equal(r, ref[s[3]]))
             for _ in range(reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                launch(ctx)
+                launch(ctx, s[3])
                 e1.record()
                 torch.cuda.synchronize()
                 times[s].append(e0.elapsed_time(e1))
@@ -90,7 +99,7 @@ def main():
            "box": measure(b["frames"])}
     for s, t in times.items():
         ms = float(np.median(t))
-        key = ":".join(str(x) for x in s if x != "")
+        key = ":".join(str(x) for x in s[:3] if x != "") + (":c" if s[3] else "")
         out[key] = {"ms": round(ms, 4), "gbs": round(b["bytes"] / ms / 1e6, 1),
                     "mpkts": round(n / ms / 1e3, 1), "same_records": same[s]}
     print(json.dumps(out))
