@@ -198,13 +198,28 @@ int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *ctx, uint32_t *d_tokens,
                                  uint32_t start, uint32_t end, uint32_t add,
                                  uint32_t initial_tokens, void *stream);
 
+/* Tx side (reference iphdr/ipcksum.h:101-211, callers ldp/ldpsend.c:
+ * 162-167): set, in place, the checksums of every frame of a device batch as
+ * ip46_set_hdr_cksum_calc + tcp/udp(6)_set_cksum_calc would -- the IPv4
+ * header checksum of every parsed IPv4 frame, the TCP/UDP checksum of every
+ * frame with an L4 header (PPTK_RX_F_L4: not a fragment, long enough),
+ * located exactly as pptk_rx_batch_device parses.  Frames the receive
+ * transform would not parse are left untouched.  After it, the receive
+ * transform verifies every such frame (IP_OK / L4_OK).  Layout arguments as
+ * in pptk_rx_dev_batch; max_len is a tuning hint.  Asynchronous. */
+int pptk_tx_cksum_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint64_t *d_off,
+                         const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
+                         uint64_t n, uint32_t max_len, void *stream);
+
 /* Tuning: force kernel variant `variant` (0 .. pptk_rx_variant_count()-1)
  * and/or memory-policy flags for every later batch of this context; -1
  * restores the automatic choice (variant by frame length and alignment).
  * flags: PPTK_RX_TUNE_NT_LOADS (non-temporal frame loads),
  * PPTK_RX_TUNE_NO_STAGING (store records per lane, not via LDS),
  * PPTK_RX_TUNE_NT_STORES (non-temporal record stores),
- * PPTK_RX_TUNE_SC1_STORES (write-through record stores).
+ * PPTK_RX_TUNE_SC1_STORES (write-through record stores),
+ * PPTK_RX_TUNE_BLOCKED (each wavefront takes a contiguous block of tiles
+ * instead of every nwaves-th tile).
  * Variants and flags change speed only: results are identical for every
  * setting on every input.  (Flag bits 0x8 and 0x10 are diagnostics that skip
  * record stores / the per-frame phase: never set them outside profiling.) */
@@ -212,6 +227,7 @@ int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *ctx, uint32_t *d_tokens,
 #define PPTK_RX_TUNE_NO_STAGING 0x2
 #define PPTK_RX_TUNE_NT_STORES 0x20
 #define PPTK_RX_TUNE_SC1_STORES 0x40
+#define PPTK_RX_TUNE_BLOCKED 0x100   /* contiguous tiles per wavefront */
 int pptk_rx_set_tuning(struct pptk_rx_ctx *ctx, int variant, int flags);
 int pptk_rx_variant_count(void);
 

@@ -47,6 +47,17 @@ def _ptr(a, t=_vp):
     return ctypes.cast(a.ctypes.data, t)
 
 
+def _tx(fn, buf, off, lens, stride, fixed_len, n):
+    out = np.array(buf, dtype=np.uint8, copy=True)
+    off = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    lens = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    if n is None:
+        n = len(off) if off is not None else len(buf) // stride
+    fn(_ptr(out), _ptr(off), _ptr(lens), ctypes.c_uint64(stride), ctypes.c_uint32(fixed_len),
+       ctypes.c_size_t(n))
+    return out
+
+
 class _Lib:
     prefix = ""
 
@@ -101,6 +112,9 @@ class Oracle(_Lib):
                                    ctypes.c_int]
         L.orc_cksum_loop.restype = ctypes.c_uint32
         L.orc_cksum_loop.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint64]
+        L.orc_tx_batch.restype = None
+        L.orc_tx_batch.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
+                                   ctypes.c_size_t]
         L.orc_permit_batch.restype = None
         L.orc_permit_batch.argtypes = [_vp, ctypes.c_size_t, ctypes.c_int, _vp, _vp, _vp]
         L.orc_tokens_refill.restype = None
@@ -121,6 +135,10 @@ class Oracle(_Lib):
         tok = np.array(tokens, dtype=np.uint32)
         self.lib.orc_tokens_refill(_ptr(tok), start, end, add, initial)
         return tok
+
+    def tx_batch(self, buf, off=None, lens=None, stride=0, fixed_len=0, n=None):
+        """Tx-side checksum setting; returns an updated copy of buf."""
+        return _tx(self.lib.orc_tx_batch, buf, off, lens, stride, fixed_len, n)
 
     def cksum(self, data):
         b = bytes(data)
@@ -183,6 +201,9 @@ class Reference(_Lib):
                                    ctypes.c_int, ctypes.c_int]
         L.ref_cksum_loop.restype = ctypes.c_uint32
         L.ref_cksum_loop.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint64]
+        L.ref_tx_batch.restype = None
+        L.ref_tx_batch.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
+                                   ctypes.c_size_t]
         L.ref_permit_batch.restype = None
         L.ref_permit_batch.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint8,
                                        _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]
@@ -200,6 +221,11 @@ class Reference(_Lib):
         self.lib.ref_permit_batch(bytes(key), _ptr(recs), len(recs), family, bits, _ptr(subj),
                                   hash_size, initial, _ptr(tok), _ptr(v))
         return v, tok
+
+    def tx_batch(self, buf, off=None, lens=None, stride=0, fixed_len=0, n=None):
+        """The reference's *_set_cksum_calc on every parsed frame; returns an
+        updated copy of buf."""
+        return _tx(self.lib.ref_tx_batch, buf, off, lens, stride, fixed_len, n)
 
     def tokens_refill(self, hash_size, batch_size, initial, add, k, tokens):
         """The reference's batch_timer_fn for timer k (buckets

@@ -452,3 +452,41 @@ void ref_tokens_refill(uint32_t hash_size, uint32_t batch_size, uint32_t initial
   ip_hash_free(&h, &heap);
   timer_linkheap_free(&heap);
 }
+
+/* ---- tx side: the reference's own setters (iphdr/ipcksum.h:101-211) on
+ * every frame the record composition parses, located by that composition:
+ * ip_set_hdr_cksum_calc(ip, ihl) for IPv4, then tcp/udp(6)_set_cksum_calc
+ * (ip, ihl | 40, l4, l4_len) when the record has an L4 header. */
+void ref_tx_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                  uint32_t fixed_len, size_t n)
+{
+  struct ref_opts o;
+  size_t i;
+  memset(&o, 0, sizeof(o));
+  for (i = 0; i < n; i++) {
+    uint8_t *f = buf + (off ? off[i] : i * stride);
+    const uint32_t flen = len ? len[i] : fixed_len;
+    struct pptk_rx_rec r;
+    uint8_t *ip, *l4;
+    ref_rx_one(f, flen, &o, &r, 0);
+    if (!(r.flags & PPTK_RX_F_PARSED) || (r.flags & PPTK_RX_F_MALFORMED))
+      continue;
+    ip = f + r.l3_off;
+    l4 = f + r.l4_off;
+    if (!(r.flags & PPTK_RX_F_IPV6))
+      ip_set_hdr_cksum_calc(ip, ip_hdr_len(ip));
+    if (!(r.flags & PPTK_RX_F_L4))
+      continue;
+    if (r.flags & PPTK_RX_F_IPV6) {
+      if (r.proto == 6)
+        tcp6_set_cksum_calc(ip, 40, l4, r.l4_len);
+      else
+        udp6_set_cksum_calc(ip, 40, l4, r.l4_len);
+    } else {
+      if (r.proto == 6)
+        tcp_set_cksum_calc(ip, ip_hdr_len(ip), l4, r.l4_len);
+      else
+        udp_set_cksum_calc(ip, ip_hdr_len(ip), l4, r.l4_len);
+    }
+  }
+}

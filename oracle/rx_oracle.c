@@ -499,3 +499,44 @@ void orc_tokens_refill(uint32_t *tokens, uint32_t start, uint32_t end,
     tokens[i] = t;
   }
 }
+
+/* ---- tx side (iphdr/ipcksum.h:101-211): on every frame orc_rx_one parses,
+ * zero the checksum field and store the recomputed checksum in network
+ * order -- the IPv4 header checksum (ip_set_hdr_cksum_calc) and, when the
+ * record has an L4 header, the TCP/UDP one (tcp/udp(6)_set_cksum_calc). */
+static void put_be16(uint8_t *p, uint16_t v)
+{
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)v;
+}
+
+void orc_tx_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                  uint32_t fixed_len, size_t n)
+{
+  struct orc_opts o;
+  size_t i;
+  memset(&o, 0, sizeof(o));
+  for (i = 0; i < n; i++) {
+    uint8_t *f = buf + (off ? off[i] : i * stride);
+    const uint32_t flen = len ? len[i] : fixed_len;
+    struct pptk_rx_rec r;
+    uint8_t *ip, *l4;
+    orc_rx_one(f, flen, &o, &r);
+    if (!(r.flags & PPTK_RX_F_PARSED) || (r.flags & PPTK_RX_F_MALFORMED))
+      continue;
+    ip = f + r.l3_off;
+    l4 = f + r.l4_off;
+    if (!(r.flags & PPTK_RX_F_IPV6)) {
+      put_be16(ip + 10, 0);
+      put_be16(ip + 10, orc_ip_hdr_cksum(ip));
+    }
+    if (!(r.flags & PPTK_RX_F_L4))
+      continue;
+    {
+      uint8_t *fld = l4 + (r.proto == 6 ? 16 : 6);
+      put_be16(fld, 0);
+      put_be16(fld, (r.flags & PPTK_RX_F_IPV6) ? orc_l4_cksum_v6(ip, l4, r.l4_len, r.proto)
+                                               : orc_l4_cksum_v4(ip, l4, r.l4_len, r.proto));
+    }
+  }
+}

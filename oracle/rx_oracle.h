@@ -44,6 +44,8 @@ int orc_rx_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
 uint32_t orc_cksum_loop(const uint8_t *buf, size_t sz, uint64_t iters);
 void orc_permit_batch(const struct pptk_rx_rec *recs, size_t n, int family,
                       const uint8_t *subject, uint32_t *tokens, uint8_t *verdict);
+void orc_tx_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                  uint32_t fixed_len, size_t n);
 void orc_tokens_refill(uint32_t *tokens, uint32_t start, uint32_t end,
                        uint32_t add, uint32_t initial);
 

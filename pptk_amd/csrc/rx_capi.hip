@@ -260,6 +260,39 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   return hip_err(launch_rx(variant, a, grid_for(c, variant, b->n), (hipStream_t)stream));
 }
 
+int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,
+                         const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
+                         uint64_t n, uint32_t max_len, void *stream) {
+  if (!c || n > 0xffffffffull) return -EINVAL;
+  if (n == 0) return 0;
+  if (!d_frames || (!d_off && stride == 0 && n > 1) || (!d_len && fixed_len > 65535))
+    return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  pptk_rx_dev_batch b;
+  memset(&b, 0, sizeof(b));
+  b.d_frames = d_frames;
+  b.d_off = d_off;
+  b.d_len = d_len;
+  b.stride = stride;
+  b.fixed_len = fixed_len;
+  b.max_len = max_len;
+  b.n = n;
+  uint32_t mmax = 15;
+  if (!d_off) {
+    const uint64_t p = (uint64_t)(uintptr_t)d_frames;
+    const uint64_t gg = gcd64(stride % 16 ? stride % 16 : 16, 16);
+    mmax = (uint32_t)((p % gg) + 16 - gg);
+  }
+  const uint32_t maxlen = d_len ? (max_len ? max_len : 65535u) : fixed_len;
+  int variant = pick_variant(maxlen + mmax);
+  const int fv = forced_variant(c);
+  if (fv >= 0) variant = fv;
+  RxKArgs a = batch_args(c, &b);
+  a.frames_w = d_frames;
+  a.tune = pick_tune(c, variant, d_off || d_len) & ~(uint32_t)PPTK_RX_TUNE_NT_LOADS;
+  return hip_err(launch_rx(variant, a, grid_for(c, variant, n), (hipStream_t)stream));
+}
+
 int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
                                uint32_t *d_perm, void *d_scratch, void *stream) {
   int rc = check_batch(c, b);
@@ -290,7 +323,7 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
 }
 
 int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
-  if (!c || variant < -1 || variant >= RX_NVARIANTS || flags < -1 || flags > 255) return -EINVAL;
+  if (!c || variant < -1 || variant >= RX_NVARIANTS || flags < -1 || flags > 0xffff) return -EINVAL;
   c->forced_variant = variant;
   c->forced_flags = flags;
   return 0;

@@ -26,6 +26,7 @@ struct RxKArgs {
   uint32_t bucket4, bucket6;  // 1 = compute src_bucket for that family
   uint32_t tune;         // A/B knobs (PPTK_RX_TUNE): bit0 nt frame loads, bit1 no LDS record staging
   const void *zero;      // >= 16 zeroed device bytes (owned by the context)
+  uint8_t *frames_w;     // tx batches: frames (writable) whose checksums are set
   // Derived by launch_rx for the GATHER kernels: branch-free descriptor
   // loads.  An absent array is read at index 0 of `zero` (msk = 0) and its
   // arithmetic stand-in (identity, i * stride_g, fixed_g) is added instead.

@@ -433,11 +433,19 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
   uint8_t *wimg = lds + wv * WAVE * IMG_STRIDE;
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
   const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+  // Tile order: strided over the grid (default), or, with tune bit 8
+  // (experiment), a contiguous block of tiles per wave, so that one wave's
+  // successive record flushes are adjacent in memory.
+  const bool blocked = a.tune & 256u;
+  const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
+  const uint64_t per = (ntiles + nwaves - 1) / nwaves;
+  const uint64_t step = blocked ? 1 : nwaves;
+  const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
 
-  uint64_t tile = (uint64_t)blockIdx.x * WPB + wv;
+  uint64_t tile = blocked ? wid * per : wid;
   Desc dc = load_desc<GATHER>(a, tile, lane);
-  Desc dn = load_desc<GATHER>(a, tile + nwaves, lane);
-  uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * nwaves, lane);
+  Desc dn = load_desc<GATHER>(a, tile + step, lane);
+  uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * step, lane);
   // prologue: the first D rounds of the first tile, in slots 0 .. D-1
   Buf<S> b[D + 1];
   // (issued strictly in slot order: the loop-header wait is computed from
@@ -449,13 +457,13 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  while (tile < ntiles) {
+  while (tile < tend) {
     uint32_t my_sum = 0;
     // Descriptors run ahead in two stages so that no wait on them ever has
     // to drain the chunk loads in flight: the index (perm) of tile + 3 nwaves
     // is loaded here, the dependent offset/length of tile + 2 nwaves (whose
     // index arrived during the previous tile) before the last round group.
-    const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * nwaves, lane);
+    const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
     // ---- streaming rounds: team g sums frame g*T + r over [team_start, len).
     // Fixed-slot ring of D + 1 rounds: round r lives in slot r % (D + 1); a
     // group of D + 1 rounds is unrolled so every slot index is a constant and
@@ -556,6 +564,16 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
           ipc = finish16(hs);
           if (ipc == 0)
             flags |= PPTK_RX_F_IP_OK;
+          if (a.frames_w) {
+            // tx: ip_set_hdr_cksum_calc (iphdr/ipcksum.h:101-111) -- the sum
+            // with the field zeroed is hs - field; the version nibble makes
+            // it positive, so the mod-0xffff residue is exact
+            const uint32_t fld = v.le32((int)l3 + 8) >> 16;
+            const uint32_t nc = finish16(fold16(hs) + (0xffffu - fld));
+            uint8_t *fw = a.frames_w + dc.base + l3 + 10;
+            fw[0] = (uint8_t)(nc >> 8);
+            fw[1] = (uint8_t)nc;
+          }
         }
         uint32_t ports = 0, l4c = 0;
         if (flags & PPTK_RX_F_L4) {
@@ -578,27 +596,41 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
           l4c = finish16(ps + rsum);
           if (l4c == 0)
             flags |= PPTK_RX_F_L4_OK;
+          if (a.frames_w) {
+            // tx: tcp/udp(6)_set_cksum_calc (iphdr/ipcksum.h:127-211) -- the
+            // region sum minus the transmitted field (an even offset of the
+            // region, so one of its words); the pseudo-header keeps the
+            // total positive
+            const int f = (int)rs + (proto == 6 ? 16 : 6);
+            const uint32_t fld = v.u8(f) | (v.u8(f + 1) << 8);
+            const uint32_t nc = finish16(ps + fold16(rsum + (0xffffu - fld)));
+            uint8_t *fw = a.frames_w + dc.base + f;
+            fw[0] = (uint8_t)(nc >> 8);
+            fw[1] = (uint8_t)nc;
+          }
           if (proto == 17 && (v.le32((int)rs + 4) >> 16) == 0)
             flags |= PPTK_RX_F_UDP_ZERO;
         }
-        Sip sh(a.k0, a.k1);
-        sh.block((uint64_t)s0 | ((uint64_t)s1 << 32));
-        sh.block((uint64_t)s2 | ((uint64_t)s3 << 32));
-        sh.block((uint64_t)d0 | ((uint64_t)d1 << 32));
-        sh.block((uint64_t)d2 | ((uint64_t)d3 << 32));
-        sh.block((uint64_t)ports | ((uint64_t)proto << 32));
-        fh = sh.finish(40ull << 56);
         uint32_t bucket = 0;
-        if (!v6 && a.bucket4) {
-          const uint32_t host = __builtin_bswap32(s0) & a.mask4;
-          Sip bh(a.k0, a.k1);
-          bh.block((uint64_t)host);
-          bucket = (uint32_t)bh.finish(8ull << 56) & a.hash_mask;
-        } else if (v6 && a.bucket6) {
-          Sip bh(a.k0, a.k1);
-          bh.block(((uint64_t)s0 | ((uint64_t)s1 << 32)) & a.mask6_0);
-          bh.block(((uint64_t)s2 | ((uint64_t)s3 << 32)) & a.mask6_1);
-          bucket = (uint32_t)bh.finish(16ull << 56) & a.hash_mask;
+        if (a.recs || a.recs32 || a.hash) {   // tx batches need no hashes
+          Sip sh(a.k0, a.k1);
+          sh.block((uint64_t)s0 | ((uint64_t)s1 << 32));
+          sh.block((uint64_t)s2 | ((uint64_t)s3 << 32));
+          sh.block((uint64_t)d0 | ((uint64_t)d1 << 32));
+          sh.block((uint64_t)d2 | ((uint64_t)d3 << 32));
+          sh.block((uint64_t)ports | ((uint64_t)proto << 32));
+          fh = sh.finish(40ull << 56);
+          if (!v6 && a.bucket4) {
+            const uint32_t host = __builtin_bswap32(s0) & a.mask4;
+            Sip bh(a.k0, a.k1);
+            bh.block((uint64_t)host);
+            bucket = (uint32_t)bh.finish(8ull << 56) & a.hash_mask;
+          } else if (v6 && a.bucket6) {
+            Sip bh(a.k0, a.k1);
+            bh.block(((uint64_t)s0 | ((uint64_t)s1 << 32)) & a.mask6_0);
+            bh.block(((uint64_t)s2 | ((uint64_t)s3 << 32)) & a.mask6_1);
+            bucket = (uint32_t)bh.finish(16ull << 56) & a.hash_mask;
+          }
         }
         w[0] = (uint32_t)fh;
         w[1] = (uint32_t)(fh >> 32);
@@ -627,7 +659,9 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
         r2 = (u32x4){w[8], w[9], w[10], w[11]};
         r3 = (u32x4){w[12], w[13], w[14], w[15]};
       }
-      if (!stage) {  // permuted order: records scatter, store per lane
+      if (!a.recs && !a.recs32) {
+        // tx batch: no records
+      } else if (!stage) {  // permuted order: records scatter, store per lane
         u32x4 *dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + (uint64_t)dc.idx * 32u
                                    : (uint8_t *)a.recs + (uint64_t)dc.idx * 64u);
         dst[0] = r0; dst[1] = r1;
@@ -640,7 +674,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
         if (!c32) { st[2] = r2; st[3] = r3; }
       }
     }
-    if (stage && !(a.tune & 8u)) {   // tune bit 3 (diagnostics only): no record stores
+    if (stage && !(a.tune & 8u) && (a.recs || a.recs32)) {   // tune bit 3: diagnostics, no stores
       // identity order: the tile's 64 records are one contiguous 4 KB run
       // (2 KB compact); each store instruction writes 1 KB contiguously
       // instead of 64 scattered 16-byte pieces
@@ -674,7 +708,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
       }
       __builtin_amdgcn_wave_barrier();
     }
-    tile += nwaves;
+    tile += step;
     dc = dn;
     dn = d2;
     idx2 = idx3;

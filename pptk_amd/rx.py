@@ -45,7 +45,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
-           "pptk_rx_tokens_refill_device",
+           "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
@@ -76,6 +76,10 @@ def lib(path=None):
         L.pptk_rx_bin_scratch_bytes.restype = ctypes.c_size_t
         L.pptk_rx_bin_device.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp]
         L.pptk_rx_bin_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_tx_cksum_device"):         # absent from older A/B builds
+            L.pptk_tx_cksum_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
+                                               ctypes.c_uint64, ctypes.c_uint32, vp]
+            L.pptk_tx_cksum_device.restype = ctypes.c_int
         if hasattr(L, "pptk_rx_permit_device"):        # absent from older A/B builds
             L.pptk_rx_permit_scratch_bytes.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
             L.pptk_rx_permit_scratch_bytes.restype = ctypes.c_size_t
@@ -221,6 +225,17 @@ class RxContext:
                                                   initial, ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_tokens_refill_device failed ({rc})")
+
+    def tx_cksum_device(self, frames, n, off=None, lens=None, stride=0, fixed_len=0, max_len=0,
+                        stream=None):
+        """Tx side: set the checksums of the frames in `frames` (torch uint8
+        CUDA tensor) in place, asynchronously."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = self._L.pptk_tx_cksum_device(self._ctx, _dp(frames), _dp(off), _dp(lens), stride,
+                                          fixed_len, n, max_len, ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_tx_cksum_device failed ({rc})")
 
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""

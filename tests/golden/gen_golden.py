@@ -9,6 +9,10 @@ holds only frames (inputs) and the 64-byte records (outputs).
 
     python tests/golden/gen_golden.py [set ...]     (default: every set)
 
+tx.npz holds tx-side cases: frames with scrambled checksum fields and the
+same frames after the reference's ip_set_hdr_cksum_calc /
+tcp/udp(6)_set_cksum_calc (oracle/refgen.c ref_tx_batch).
+
 permit.npz additionally holds rate-limiter cases: token arrays before/after
 and per-frame verdicts of the reference's ip_permitted / ipv6_permitted
 called once per subject frame in frame order (oracle/refgen.c
@@ -79,11 +83,54 @@ def gen_permit(ref):
     return out
 
 
+def scramble_cksums(z, rng):
+    """Copy of z's buffer with random bytes in the IPv4 header and TCP/UDP
+    checksum fields of every frame the record composition parses."""
+    from pptk_amd.records import F_IPV6, F_L4, F_MALFORMED, F_PARSED, as_records
+    buf = z["buf"].copy()
+    rec = as_records(z["recs"])
+    for i, o in enumerate(z["off"]):
+        r, f = rec[i], int(o)
+        fl = int(r["flags"])
+        if not fl & F_PARSED or fl & F_MALFORMED:
+            continue
+        if not fl & F_IPV6:
+            p = f + int(r["l3_off"]) + 10
+            buf[p:p + 2] = rng.integers(0, 256, 2)
+        if fl & F_L4:
+            p = f + int(r["l4_off"]) + (16 if int(r["proto"]) == 6 else 6)
+            buf[p:p + 2] = rng.integers(0, 256, 2)
+    return buf
+
+
+def gen_tx(ref):
+    """Tx-side fixtures over the golden sets: random bytes in every parsed
+    frame's checksum fields (inputs), and the reference's
+    *_set_cksum_calc result.  Stored as byte positions into the set's buffer
+    with the scrambled and the expected bytes (the setters change nothing
+    else, which the tests check)."""
+    rng = np.random.default_rng(0x7C)
+    out = {}
+    for name in ("edge", "fuzz", "cmix", "c64"):
+        z = dict(np.load(os.path.join(HERE, f"{name}.npz")))
+        buf_in = scramble_cksums(z, rng)
+        buf_out = ref.tx_batch(buf_in, z["off"], z["len"])
+        pos = np.nonzero((buf_in != z["buf"]) | (buf_out != buf_in))[0]
+        out[f"{name}_pos"] = pos.astype(np.uint64)
+        out[f"{name}_in"] = buf_in[pos]
+        out[f"{name}_out"] = buf_out[pos]
+    return out
+
+
 def main():
     build()
     ref = Reference()
     opts = make_opts(KEY, BITS4, BITS6, HASH_SIZE)
-    want = set(sys.argv[1:]) or set(SETS) | {"permit"}
+    want = set(sys.argv[1:]) or set(SETS) | {"permit", "tx"}
+    if "tx" in want:
+        path = os.path.join(HERE, "tx.npz")
+        np.savez_compressed(path, **gen_tx(ref))
+        print(f"tx -> {os.path.getsize(path)} B")
     if "permit" in want:
         path = os.path.join(HERE, "permit.npz")
         np.savez_compressed(path, **gen_permit(ref))

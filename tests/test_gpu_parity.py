@@ -86,7 +86,7 @@ def test_every_forced_variant(name, dev):
     z = load_golden(name)
     ctx = _ctx(z)
     for v in range(lib().pptk_rx_variant_count()):
-        ctx.set_tuning(v, v % 4)
+        ctx.set_tuning(v, (v % 4) | (256 if v % 2 else 0))   # 256: blocked tile order
         for shift in (0, 5):
             got = _run(ctx, z, dev, shift=shift)
             d = diff_records(got, z["recs"])
