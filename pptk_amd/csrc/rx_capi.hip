@@ -289,7 +289,9 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
   if (fv >= 0) variant = fv;
   RxKArgs a = batch_args(c, &b);
   a.frames_w = d_frames;
-  a.tune = pick_tune(c, variant, d_off || d_len) & ~(uint32_t)PPTK_RX_TUNE_NT_LOADS;
+  a.tune = c->forced_flags >= 0 ? (uint32_t)c->forced_flags
+                                : pick_tune(c, variant, d_off || d_len) &
+                                      ~(uint32_t)PPTK_RX_TUNE_NT_LOADS;
   return hip_err(launch_rx(variant, a, grid_for(c, variant, n), (hipStream_t)stream));
 }
 

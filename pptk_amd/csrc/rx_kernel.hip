@@ -401,6 +401,23 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
   return b;
 }
 
+// Tx: store the checksum fields txp[k] (frame offsets, -1 = none) with
+// values txv[k], network byte order.  Each field is a 2-byte write into a
+// line this wave read long before, so every field costs the memory a whole
+// write granule; writing 16/32/64-byte granules around the fields from the
+// patched LDS image instead was measured no faster, so plain
+// byte stores it is.
+__device__ __forceinline__ void tx_store(const RxKArgs &a, uint64_t base, const int txp[2],
+                                         const uint32_t txv[2]) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (txp[k] < 0) continue;
+    uint8_t *fw = a.frames_w + base + txp[k];
+    fw[0] = (uint8_t)(txv[k] >> 8);
+    fw[1] = (uint8_t)txv[k];
+  }
+}
+
 // Waves per SIMD the register allocator must leave room for: the streaming
 // variants keep D = 3 rounds of S chunks in registers (D * S * 4 VGPRs) and
 // need 2 waves/SIMD; the small-frame variants 4.
@@ -550,6 +567,8 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
       } else if (flags & PPTK_RX_F_PARSED) {
         const bool v6 = flags & PPTK_RX_F_IPV6;
         uint32_t s0, s1 = 0, s2 = 0, s3 = 0, d0, d1 = 0, d2 = 0, d3 = 0;
+        int txp[2] = {-1, -1};          // tx: frame offsets of the fields to set
+        uint32_t txv[2] = {0, 0};
         uint32_t ipc = 0;
         if (v6) {
           s0 = v.le32(l3 + 8);  s1 = v.le32(l3 + 12); s2 = v.le32(l3 + 16); s3 = v.le32(l3 + 20);
@@ -569,10 +588,8 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
             // with the field zeroed is hs - field; the version nibble makes
             // it positive, so the mod-0xffff residue is exact
             const uint32_t fld = v.le32((int)l3 + 8) >> 16;
-            const uint32_t nc = finish16(fold16(hs) + (0xffffu - fld));
-            uint8_t *fw = a.frames_w + dc.base + l3 + 10;
-            fw[0] = (uint8_t)(nc >> 8);
-            fw[1] = (uint8_t)nc;
+            txp[0] = (int)l3 + 10;
+            txv[0] = finish16(fold16(hs) + (0xffffu - fld));
           }
         }
         uint32_t ports = 0, l4c = 0;
@@ -603,14 +620,14 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
             // total positive
             const int f = (int)rs + (proto == 6 ? 16 : 6);
             const uint32_t fld = v.u8(f) | (v.u8(f + 1) << 8);
-            const uint32_t nc = finish16(ps + fold16(rsum + (0xffffu - fld)));
-            uint8_t *fw = a.frames_w + dc.base + f;
-            fw[0] = (uint8_t)(nc >> 8);
-            fw[1] = (uint8_t)nc;
+            txp[1] = f;
+            txv[1] = finish16(ps + fold16(rsum + (0xffffu - fld)));
           }
           if (proto == 17 && (v.le32((int)rs + 4) >> 16) == 0)
             flags |= PPTK_RX_F_UDP_ZERO;
         }
+        if (a.frames_w && !(a.tune & 512u))   // bit 9: diagnostics, no tx writes
+          tx_store(a, dc.base, txp, txv);
         uint32_t bucket = 0;
         if (a.recs || a.recs32 || a.hash) {   // tx batches need no hashes
           Sip sh(a.k0, a.k1);

@@ -53,7 +53,7 @@ def _tx(ctx, z, buf, dev, shift, stride=None):
 
 
 @pytest.mark.parametrize("name", SETS)
-@pytest.mark.parametrize("shift", [0, 3, 8])
+@pytest.mark.parametrize("shift", [0, 3, 8, 64])
 def test_tx_matches_reference(name, shift, dev):
     z, buf_in, buf_out = _case(name)
     big, frames = _tx(_ctx(), z, buf_in, dev, shift)
@@ -78,7 +78,7 @@ def test_tx_every_variant(dev):
     ctx = _ctx()
     for v in range(lib().pptk_rx_variant_count()):
         ctx.set_tuning(v, v % 4)
-        _, frames = _tx(ctx, z, buf_in, dev, 1)
+        _, frames = _tx(ctx, z, buf_in, dev, 0 if v % 2 else 1)
         got = frames[:buf_in.size].cpu().numpy()
         assert np.array_equal(got, buf_out), f"variant {v}"
 
