@@ -230,6 +230,10 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint6
 #define PPTK_RX_TUNE_BLOCKED 0x100   /* contiguous tiles per wavefront */
 int pptk_rx_set_tuning(struct pptk_rx_ctx *ctx, int variant, int flags);
 int pptk_rx_variant_count(void);
+/* The kernel variant the last device batch of this context launched (the
+ * automatic or forced choice after eligibility checks; -1 before the first
+ * batch).  Diagnostics for tests and benchmarks. */
+int pptk_rx_last_variant(const struct pptk_rx_ctx *ctx);
 
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);

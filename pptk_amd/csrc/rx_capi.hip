@@ -51,6 +51,7 @@ struct pptk_rx_ctx {
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
   int forced_flags = -1;
+  int last_variant = -1;
   RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch)
   std::vector<RxRing> rings;
 };
@@ -177,7 +178,8 @@ static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
   }
   if (c->forced_flags >= 0) return (uint32_t)c->forced_flags;
   if (tune >= 0) return (uint32_t)tune;
-  const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2;
+  const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2 ||
+                     variant == RX_L4;
   return (small || gather) ? PPTK_RX_TUNE_NT_STORES
                            : (PPTK_RX_TUNE_NT_STORES | PPTK_RX_TUNE_NT_LOADS);
 }
@@ -252,11 +254,16 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
     mmax = (uint32_t)((p % gg) + 16 - gg);
   }
   const uint32_t maxlen = b->d_len ? (b->max_len ? b->max_len : 65535u) : b->fixed_len;
-  int variant = pick_variant(maxlen + mmax);
+  // the lane kernel takes fixed-stride batches of small frames that all
+  // start on a 16-byte boundary (mmax == 0: aligned buffer and stride)
+  const bool lane_ok = !b->d_off && !b->d_len && !b->d_perm && mmax == 0 && b->fixed_len <= 64;
+  int variant = lane_ok ? RX_L4 : pick_variant(maxlen + mmax);
   const int fv = forced_variant(c);
   if (fv >= 0) variant = fv;
+  if (variant == RX_L4 && !lane_ok) variant = pick_variant(maxlen + mmax);
   RxKArgs a = batch_args(c, b);
   a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm);
+  c->last_variant = variant;
   return hip_err(launch_rx(variant, a, grid_for(c, variant, b->n), (hipStream_t)stream));
 }
 
@@ -286,9 +293,10 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
   const uint32_t maxlen = d_len ? (max_len ? max_len : 65535u) : fixed_len;
   int variant = pick_variant(maxlen + mmax);
   const int fv = forced_variant(c);
-  if (fv >= 0) variant = fv;
+  if (fv >= 0 && fv != RX_L4) variant = fv;   // the lane kernel has no tx mode
   RxKArgs a = batch_args(c, &b);
   a.frames_w = d_frames;
+  c->last_variant = variant;
   a.tune = c->forced_flags >= 0 ? (uint32_t)c->forced_flags
                                 : pick_tune(c, variant, d_off || d_len) &
                                       ~(uint32_t)PPTK_RX_TUNE_NT_LOADS;
@@ -313,7 +321,7 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
     // the group holding max_len also takes every group above it (all empty
     // when the hint is right; a wrong hint costs speed, never results)
     const bool last = g == kGroups - 1 || kGroupMaxLen[g] >= maxlen;
-    const int variant = fv >= 0 ? fv : kGroupVariant[g];
+    const int variant = fv >= 0 && fv != RX_L4 ? fv : kGroupVariant[g];
     a.range_lo = tab + g;
     a.range_hi = tab + (last ? kGroups : g + 1);
     a.tune = pick_tune(c, variant, true);
@@ -332,6 +340,8 @@ int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
 }
 
 int pptk_rx_variant_count(void) { return RX_NVARIANTS; }
+
+int pptk_rx_last_variant(const struct pptk_rx_ctx *c) { return c ? c->last_variant : -1; }
 
 size_t pptk_rx_permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
   if (hash_size == 0 || (hash_size & (hash_size - 1)) || n > 0xffffffffull) return 0;

@@ -47,6 +47,7 @@ enum RxVariant {
   RX_T16S7L, RX_T32S4L,   // chunk grid on 128-byte lines
   RX_T32S3D7, RX_T16S6D1, // prefetch-depth experiments
   RX_T8S2, RX_T16S4,      // length-group shapes (256 and 1024 bytes)
+  RX_L4,                  // lane kernel: fixed stride, 16-byte aligned frames <= 64 bytes
   RX_NVARIANTS
 };
 

@@ -418,6 +418,280 @@ __device__ __forceinline__ void tx_store(const RxKArgs &a, uint64_t base, const 
   }
 }
 
+// The 16 record words of struct pptk_rx_rec (include/pptk_rx.h) of one frame,
+// before the compact projection.
+struct LaneRec {
+  uint32_t w[16];
+  uint64_t fh;
+  uint32_t flags;
+};
+
+// The per-frame part of the transform for a frame in any layout: structural
+// parse, IPv4 header checksum, L4 checksum from the team sum `my_sum` of the
+// frame bytes [team_start_of(v.m), len), flow hash, bucket hash, and (tx
+// batches) the checksum stores.  DESIGN.md "Record semantics" steps 1-9.
+__device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &v, uint32_t len,
+                                             uint64_t base, uint32_t my_sum, LaneRec &o) {
+  const int m = v.m;
+  const Parse p = parse_frame(v, len);
+  uint32_t flags = p.flags;
+  const uint32_t l3 = p.l3, rs = p.rs, re = p.re, proto = p.proto;
+  uint32_t *w = o.w;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = 0;
+  uint64_t fh = 0;
+  if (flags & PPTK_RX_F_MALFORMED) {
+    flags &= PPTK_RX_F_MALFORMED | PPTK_RX_F_VLAN | PPTK_RX_F_IPV6;
+  } else if (flags & PPTK_RX_F_PARSED) {
+    const bool v6 = flags & PPTK_RX_F_IPV6;
+    uint32_t s0, s1 = 0, s2 = 0, s3 = 0, d0, d1 = 0, d2 = 0, d3 = 0;
+    int txp[2] = {-1, -1};          // tx: frame offsets of the fields to set
+    uint32_t txv[2] = {0, 0};
+    uint32_t ipc = 0;
+    if (v6) {
+      s0 = v.le32(l3 + 8);  s1 = v.le32(l3 + 12); s2 = v.le32(l3 + 16); s3 = v.le32(l3 + 20);
+      d0 = v.le32(l3 + 24); d1 = v.le32(l3 + 28); d2 = v.le32(l3 + 32); d3 = v.le32(l3 + 36);
+    } else {
+      s0 = v.le32(l3 + 12);
+      d0 = v.le32(l3 + 16);
+      // ip_hdr_cksum_calc over ihl = rs - l3 bytes (frame-relative pairing)
+      uint32_t hs = 0;
+      for (uint32_t k = l3; k < rs; k += 4)
+        hs = dot16(v.le32((int)k), hs);
+      ipc = finish16(hs);
+      if (ipc == 0)
+        flags |= PPTK_RX_F_IP_OK;
+      if (a.frames_w) {
+        // tx: ip_set_hdr_cksum_calc (iphdr/ipcksum.h:101-111) -- the sum
+        // with the field zeroed is hs - field; the version nibble makes
+        // it positive, so the mod-0xffff residue is exact
+        const uint32_t fld = v.le32((int)l3 + 8) >> 16;
+        txp[0] = (int)l3 + 10;
+        txv[0] = finish16(fold16(hs) + (0xffffu - fld));
+      }
+    }
+    uint32_t ports = 0, l4c = 0;
+    if (flags & PPTK_RX_F_L4) {
+      ports = v.le32((int)rs);
+      const uint32_t l4len = re - rs;
+      uint32_t ps = dot16(s0, 0);
+      ps = dot16(s1, ps); ps = dot16(s2, ps); ps = dot16(s3, ps);
+      ps = dot16(d0, ps); ps = dot16(d1, ps); ps = dot16(d2, ps); ps = dot16(d3, ps);
+      ps += bswap16(proto) + bswap16(l4len);   // > 0: proto is 6 or 17
+      // region [rs, re) = [ts, len) - [ts, rs) - [re, len), mod 0xffff
+      const int ts = team_start_of(m);
+      uint32_t rsum = fold16(my_sum);
+      if ((int)rs > ts)
+        rsum += 0xffffu - fold16(sum_abs(v, ts, (int)rs));
+      if (re < len)
+        rsum += 0xffffu - fold16(sum_abs(v, (int)re, (int)len));
+      rsum = fold16(rsum);
+      if ((m + (int)rs) & 1)
+        rsum = bswap16(rsum);   // region starts at an odd address
+      l4c = finish16(ps + rsum);
+      if (l4c == 0)
+        flags |= PPTK_RX_F_L4_OK;
+      if (a.frames_w) {
+        // tx: tcp/udp(6)_set_cksum_calc (iphdr/ipcksum.h:127-211) -- the
+        // region sum minus the transmitted field (an even offset of the
+        // region, so one of its words); the pseudo-header keeps the
+        // total positive
+        const int f = (int)rs + (proto == 6 ? 16 : 6);
+        const uint32_t fld = v.u8(f) | (v.u8(f + 1) << 8);
+        txp[1] = f;
+        txv[1] = finish16(ps + fold16(rsum + (0xffffu - fld)));
+      }
+      if (proto == 17 && (v.le32((int)rs + 4) >> 16) == 0)
+        flags |= PPTK_RX_F_UDP_ZERO;
+    }
+    if (a.frames_w && !(a.tune & 512u))   // bit 9: diagnostics, no tx writes
+      tx_store(a, base, txp, txv);
+    uint32_t bucket = 0;
+    if (a.recs || a.recs32 || a.hash) {   // tx batches need no hashes
+      Sip sh(a.k0, a.k1);
+      sh.block((uint64_t)s0 | ((uint64_t)s1 << 32));
+      sh.block((uint64_t)s2 | ((uint64_t)s3 << 32));
+      sh.block((uint64_t)d0 | ((uint64_t)d1 << 32));
+      sh.block((uint64_t)d2 | ((uint64_t)d3 << 32));
+      sh.block((uint64_t)ports | ((uint64_t)proto << 32));
+      fh = sh.finish(40ull << 56);
+      if (!v6 && a.bucket4) {
+        const uint32_t host = __builtin_bswap32(s0) & a.mask4;
+        Sip bh(a.k0, a.k1);
+        bh.block((uint64_t)host);
+        bucket = (uint32_t)bh.finish(8ull << 56) & a.hash_mask;
+      } else if (v6 && a.bucket6) {
+        Sip bh(a.k0, a.k1);
+        bh.block(((uint64_t)s0 | ((uint64_t)s1 << 32)) & a.mask6_0);
+        bh.block(((uint64_t)s2 | ((uint64_t)s3 << 32)) & a.mask6_1);
+        bucket = (uint32_t)bh.finish(16ull << 56) & a.hash_mask;
+      }
+    }
+    w[0] = (uint32_t)fh;
+    w[1] = (uint32_t)(fh >> 32);
+    w[2] = s0; w[3] = s1; w[4] = s2; w[5] = s3;
+    w[6] = d0; w[7] = d1; w[8] = d2; w[9] = d3;
+    w[10] = bswap16(ports & 0xffffu) | (bswap16(ports >> 16) << 16);
+    w[11] = ipc | (l4c << 16);
+    w[12] = rs | ((re - rs) << 16);
+    w[13] = proto << 8;
+    w[14] = bucket;
+  }
+  w[13] |= l3 | (flags << 16);
+  w[15] = p.et | (p.ver << 16);
+  o.fh = fh;
+  o.flags = flags;
+}
+
+// The common case parsed from registers: frame bytes 0..63 as little-endian
+// dwords d[0..15] (frame start 16-byte aligned, bytes >= len arbitrary), an
+// untagged IPv4 frame with a 20-byte header that is not a fragment and lies
+// within the frame.  Returns false for every other frame (lane_generic
+// handles it); otherwise fills the same words lane_generic would: the fixed
+// offsets are Ethernet 14 + IPv4 20, so L4 starts at 34 (an even address:
+// no byte swap) and the team-start correction disappears.
+__device__ __forceinline__ bool lane_fast(const RxKArgs &a, const uint32_t d[16], uint32_t len,
+                                          LaneRec &o) {
+  const uint32_t tl = bswap16(d[4] & 0xffffu);            // ip_total_len
+  // ethertype 0x0800 (bytes 12-13), version 4 + IHL 5 (byte 14), no MF /
+  // offset (bytes 20-21), 20 <= tl, 14 + tl <= len
+  if ((d[3] & 0x00ffffffu) != 0x00450008u || (d[5] & 0xff3fu) != 0u || tl < 20u ||
+      tl + 14u > len)
+    return false;
+  const uint32_t proto = d[5] >> 24;
+  const uint32_t re = 14u + tl, l4len = tl - 20u;
+  uint32_t flags = PPTK_RX_F_PARSED;
+  // ip_hdr_cksum_calc over bytes 14..33
+  uint32_t hs = dot16(d[3] & 0xffff0000u, 0);
+  hs = dot16(d[4], hs); hs = dot16(d[5], hs); hs = dot16(d[6], hs); hs = dot16(d[7], hs);
+  hs = dot16(d[8] & 0xffffu, hs);
+  const uint32_t ipc = finish16(hs);
+  if (ipc == 0) flags |= PPTK_RX_F_IP_OK;
+  const uint32_t s0 = __builtin_amdgcn_alignbyte(d[7], d[6], 2u);   // bytes 26..29
+  const uint32_t d0 = __builtin_amdgcn_alignbyte(d[8], d[7], 2u);   // bytes 30..33
+  uint32_t ports = 0, l4c = 0;
+  if ((proto == 6u && l4len >= 20u) || (proto == 17u && l4len >= 8u)) {
+    flags |= PPTK_RX_F_L4;
+    ports = __builtin_amdgcn_alignbyte(d[9], d[8], 2u);            // bytes 34..37
+    uint32_t ps = dot16(s0, 0);
+    ps = dot16(d0, ps);
+    ps += bswap16(proto) + bswap16(l4len);
+    uint32_t rsum;
+    if (re >= 64u) {      // region [34, 64)
+      rsum = dot16(d[8] & 0xffff0000u, 0);
+#pragma unroll
+      for (int k = 9; k < 16; ++k) rsum = dot16(d[k], rsum);
+    } else {              // Ethernet padding or a shorter frame: [34, re)
+      rsum = 0;
+#pragma unroll
+      for (int k = 8; k < 16; ++k)
+        rsum = dot16(d[k] & bmask(min(max(34 - 4 * k, 0), 4), min(max((int)re - 4 * k, 0), 4)),
+                     rsum);
+    }
+    l4c = finish16(ps + rsum);
+    if (l4c == 0) flags |= PPTK_RX_F_L4_OK;
+    if (proto == 17u && (d[10] & 0xffffu) == 0u) flags |= PPTK_RX_F_UDP_ZERO;
+  }
+  Sip sh(a.k0, a.k1);
+  sh.block((uint64_t)s0);
+  sh.block(0);
+  sh.block((uint64_t)d0);
+  sh.block(0);
+  sh.block((uint64_t)ports | ((uint64_t)proto << 32));
+  const uint64_t fh = sh.finish(40ull << 56);
+  uint32_t bucket = 0;
+  if (a.bucket4) {
+    Sip bh(a.k0, a.k1);
+    bh.block((uint64_t)(__builtin_bswap32(s0) & a.mask4));
+    bucket = (uint32_t)bh.finish(8ull << 56) & a.hash_mask;
+  }
+  uint32_t *w = o.w;
+  w[0] = (uint32_t)fh;
+  w[1] = (uint32_t)(fh >> 32);
+  w[2] = s0; w[3] = 0; w[4] = 0; w[5] = 0;
+  w[6] = d0; w[7] = 0; w[8] = 0; w[9] = 0;
+  w[10] = bswap16(ports & 0xffffu) | (bswap16(ports >> 16) << 16);
+  w[11] = ipc | (l4c << 16);
+  w[12] = 34u | (l4len << 16);
+  w[13] = 14u | (proto << 8) | (flags << 16);
+  w[14] = bucket;
+  w[15] = 0x0800u | (4u << 16);
+  o.fh = fh;
+  o.flags = flags;
+  return true;
+}
+
+// Record of frame `idx`: the optional dense flow-hash word, then the record
+// (64 bytes, or the 32-byte compact projection) either parked in the lane's
+// LDS slot `st` for flush_records (batch order) or stored directly
+// (permuted order: records scatter).
+__device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, uint32_t idx,
+                                            u32x4 *st, bool stage) {
+  const uint32_t *w = o.w;
+  if (a.hash)
+    a.hash[idx] = o.fh;
+  if (!a.recs && !a.recs32)
+    return;   // tx batch: no records
+  const bool c32 = a.recs32 != nullptr;   // compact 32-byte records
+  u32x4 r0, r1, r2, r3;
+  if (c32) {   // struct pptk_rx_rec32: a projection of the same words
+    const bool v6 = o.flags & PPTK_RX_F_IPV6;
+    r0 = (u32x4){w[0], w[1], v6 ? 0u : w[2], v6 ? 0u : w[6]};
+    r1 = (u32x4){w[10], (w[13] >> 16) | (((w[13] >> 8) & 0xffu) << 16) | (w[13] << 24),
+                 w[12], w[14]};
+    r2 = r3 = (u32x4){0u, 0u, 0u, 0u};
+  } else {
+    r0 = (u32x4){w[0], w[1], w[2], w[3]};
+    r1 = (u32x4){w[4], w[5], w[6], w[7]};
+    r2 = (u32x4){w[8], w[9], w[10], w[11]};
+    r3 = (u32x4){w[12], w[13], w[14], w[15]};
+  }
+  u32x4 *dst = st;
+  if (!stage)
+    dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + (uint64_t)idx * 32u
+                        : (uint8_t *)a.recs + (uint64_t)idx * 64u);
+  dst[0] = r0; dst[1] = r1;
+  if (!c32) { dst[2] = r2; dst[3] = r3; }
+}
+
+// Batch order: the tile's 64 records, parked in the wave's LDS at an 80-byte
+// pitch, are one contiguous 4 KB run (2 KB compact) in memory; each store
+// instruction writes 1 KB contiguously instead of 64 scattered 16-byte
+// pieces.
+__device__ __forceinline__ void flush_records(const RxKArgs &a, const uint8_t *wimg, uint64_t tile,
+                                              int lane) {
+  const bool c32 = a.recs32 != nullptr;
+  __builtin_amdgcn_wave_barrier();
+  const u32x4 *st = (const u32x4 *)wimg;
+  u32x4 *dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + tile * (uint64_t)WAVE * 32u
+                             : (uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
+  const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
+  const int lg = c32 ? 1 : 2;                 // log2 16-byte pieces per record
+  int kmax = c32 ? 2 : 4;
+  if (a.tune & 128u) kmax >>= 1;              // bit 7: diagnostics, half the bytes
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = k * WAVE + lane;   // 16-byte piece e of the tile's records
+    const int r = e >> lg;
+    if ((uint64_t)r < nrec && k < kmax) {
+      const u32x4 val = st[r * 5 + (e & ((1 << lg) - 1))];
+      if (a.tune & 64u) {            // bit 6: write-through, drop from L2 (sc1)
+        uint64_t *d8 = (uint64_t *)(dst + e);
+        __hip_atomic_store(d8, (uint64_t)val.x | ((uint64_t)val.y << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d8 + 1, (uint64_t)val.z | ((uint64_t)val.w << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      } else if (a.tune & 32u) {     // bit 5: non-temporal stores
+        asm volatile("" ::: "memory");
+        __builtin_nontemporal_store(val, dst + e);
+      } else {
+        dst[e] = val;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Waves per SIMD the register allocator must leave room for: the streaming
 // variants keep D = 3 rounds of S chunks in registers (D * S * 4 VGPRs) and
 // need 2 waves/SIMD; the small-frame variants 4.
@@ -541,7 +815,6 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
 
     // ---- lane phase: frame `lane` -> record (parsed once per frame)
     const bool stage = !(GATHER && a.perm) && !(a.tune & 2u);
-    const bool c32 = a.recs32 != nullptr;   // compact 32-byte records
     // tune bit 4 (diagnostics only, output invalid): skip the lane phase
     if (dc.idx != 0xffffffffu && !(a.tune & 16u)) {
       const int m = (int)(dc.base & 15);
@@ -555,180 +828,95 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
         }
       }
       const FrameView v = {wimg + lane * IMG_STRIDE, a.frames + dc.base, m, 16 * IMGC - m};
-      const Parse p = parse_frame(v, dc.len);
-      uint32_t flags = p.flags;
-      const uint32_t l3 = p.l3, rs = p.rs, re = p.re, proto = p.proto;
-      uint32_t w[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = 0;
-      uint64_t fh = 0;
-      if (flags & PPTK_RX_F_MALFORMED) {
-        flags &= PPTK_RX_F_MALFORMED | PPTK_RX_F_VLAN | PPTK_RX_F_IPV6;
-      } else if (flags & PPTK_RX_F_PARSED) {
-        const bool v6 = flags & PPTK_RX_F_IPV6;
-        uint32_t s0, s1 = 0, s2 = 0, s3 = 0, d0, d1 = 0, d2 = 0, d3 = 0;
-        int txp[2] = {-1, -1};          // tx: frame offsets of the fields to set
-        uint32_t txv[2] = {0, 0};
-        uint32_t ipc = 0;
-        if (v6) {
-          s0 = v.le32(l3 + 8);  s1 = v.le32(l3 + 12); s2 = v.le32(l3 + 16); s3 = v.le32(l3 + 20);
-          d0 = v.le32(l3 + 24); d1 = v.le32(l3 + 28); d2 = v.le32(l3 + 32); d3 = v.le32(l3 + 36);
-        } else {
-          s0 = v.le32(l3 + 12);
-          d0 = v.le32(l3 + 16);
-          // ip_hdr_cksum_calc over ihl = rs - l3 bytes (frame-relative pairing)
-          uint32_t hs = 0;
-          for (uint32_t k = l3; k < rs; k += 4)
-            hs = dot16(v.le32((int)k), hs);
-          ipc = finish16(hs);
-          if (ipc == 0)
-            flags |= PPTK_RX_F_IP_OK;
-          if (a.frames_w) {
-            // tx: ip_set_hdr_cksum_calc (iphdr/ipcksum.h:101-111) -- the sum
-            // with the field zeroed is hs - field; the version nibble makes
-            // it positive, so the mod-0xffff residue is exact
-            const uint32_t fld = v.le32((int)l3 + 8) >> 16;
-            txp[0] = (int)l3 + 10;
-            txv[0] = finish16(fold16(hs) + (0xffffu - fld));
-          }
-        }
-        uint32_t ports = 0, l4c = 0;
-        if (flags & PPTK_RX_F_L4) {
-          ports = v.le32((int)rs);
-          const uint32_t l4len = re - rs;
-          uint32_t ps = dot16(s0, 0);
-          ps = dot16(s1, ps); ps = dot16(s2, ps); ps = dot16(s3, ps);
-          ps = dot16(d0, ps); ps = dot16(d1, ps); ps = dot16(d2, ps); ps = dot16(d3, ps);
-          ps += bswap16(proto) + bswap16(l4len);   // > 0: proto is 6 or 17
-          // region [rs, re) = [ts, len) - [ts, rs) - [re, len), mod 0xffff
-          const int ts = team_start_of(m);
-          uint32_t rsum = fold16(my_sum);
-          if ((int)rs > ts)
-            rsum += 0xffffu - fold16(sum_abs(v, ts, (int)rs));
-          if (re < dc.len)
-            rsum += 0xffffu - fold16(sum_abs(v, (int)re, (int)dc.len));
-          rsum = fold16(rsum);
-          if ((m + (int)rs) & 1)
-            rsum = bswap16(rsum);   // region starts at an odd address
-          l4c = finish16(ps + rsum);
-          if (l4c == 0)
-            flags |= PPTK_RX_F_L4_OK;
-          if (a.frames_w) {
-            // tx: tcp/udp(6)_set_cksum_calc (iphdr/ipcksum.h:127-211) -- the
-            // region sum minus the transmitted field (an even offset of the
-            // region, so one of its words); the pseudo-header keeps the
-            // total positive
-            const int f = (int)rs + (proto == 6 ? 16 : 6);
-            const uint32_t fld = v.u8(f) | (v.u8(f + 1) << 8);
-            txp[1] = f;
-            txv[1] = finish16(ps + fold16(rsum + (0xffffu - fld)));
-          }
-          if (proto == 17 && (v.le32((int)rs + 4) >> 16) == 0)
-            flags |= PPTK_RX_F_UDP_ZERO;
-        }
-        if (a.frames_w && !(a.tune & 512u))   // bit 9: diagnostics, no tx writes
-          tx_store(a, dc.base, txp, txv);
-        uint32_t bucket = 0;
-        if (a.recs || a.recs32 || a.hash) {   // tx batches need no hashes
-          Sip sh(a.k0, a.k1);
-          sh.block((uint64_t)s0 | ((uint64_t)s1 << 32));
-          sh.block((uint64_t)s2 | ((uint64_t)s3 << 32));
-          sh.block((uint64_t)d0 | ((uint64_t)d1 << 32));
-          sh.block((uint64_t)d2 | ((uint64_t)d3 << 32));
-          sh.block((uint64_t)ports | ((uint64_t)proto << 32));
-          fh = sh.finish(40ull << 56);
-          if (!v6 && a.bucket4) {
-            const uint32_t host = __builtin_bswap32(s0) & a.mask4;
-            Sip bh(a.k0, a.k1);
-            bh.block((uint64_t)host);
-            bucket = (uint32_t)bh.finish(8ull << 56) & a.hash_mask;
-          } else if (v6 && a.bucket6) {
-            Sip bh(a.k0, a.k1);
-            bh.block(((uint64_t)s0 | ((uint64_t)s1 << 32)) & a.mask6_0);
-            bh.block(((uint64_t)s2 | ((uint64_t)s3 << 32)) & a.mask6_1);
-            bucket = (uint32_t)bh.finish(16ull << 56) & a.hash_mask;
-          }
-        }
-        w[0] = (uint32_t)fh;
-        w[1] = (uint32_t)(fh >> 32);
-        w[2] = s0; w[3] = s1; w[4] = s2; w[5] = s3;
-        w[6] = d0; w[7] = d1; w[8] = d2; w[9] = d3;
-        w[10] = bswap16(ports & 0xffffu) | (bswap16(ports >> 16) << 16);
-        w[11] = ipc | (l4c << 16);
-        w[12] = rs | ((re - rs) << 16);
-        w[13] = proto << 8;
-        w[14] = bucket;
-      }
-      w[13] |= l3 | (flags << 16);
-      w[15] = p.et | (p.ver << 16);
-      if (a.hash)
-        a.hash[dc.idx] = fh;
-      u32x4 r0, r1, r2, r3;
-      if (c32) {   // struct pptk_rx_rec32: a projection of the same words
-        const bool v6 = flags & PPTK_RX_F_IPV6;
-        r0 = (u32x4){w[0], w[1], v6 ? 0u : w[2], v6 ? 0u : w[6]};
-        r1 = (u32x4){w[10], (w[13] >> 16) | (((w[13] >> 8) & 0xffu) << 16) | (w[13] << 24),
-                     w[12], w[14]};
-        r2 = r3 = (u32x4){0u, 0u, 0u, 0u};
-      } else {
-        r0 = (u32x4){w[0], w[1], w[2], w[3]};
-        r1 = (u32x4){w[4], w[5], w[6], w[7]};
-        r2 = (u32x4){w[8], w[9], w[10], w[11]};
-        r3 = (u32x4){w[12], w[13], w[14], w[15]};
-      }
-      if (!a.recs && !a.recs32) {
-        // tx batch: no records
-      } else if (!stage) {  // permuted order: records scatter, store per lane
-        u32x4 *dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + (uint64_t)dc.idx * 32u
-                                   : (uint8_t *)a.recs + (uint64_t)dc.idx * 64u);
-        dst[0] = r0; dst[1] = r1;
-        if (!c32) { dst[2] = r2; dst[3] = r3; }
-      } else {
-        // park the record in LDS (every lane's image reads are behind us in
-        // program order) for the coalesced store below
-        u32x4 *st = (u32x4 *)wimg + lane * 5;   // 80-byte pitch
-        st[0] = r0; st[1] = r1;
-        if (!c32) { st[2] = r2; st[3] = r3; }
-      }
+      LaneRec o;
+      lane_generic(a, v, dc.len, dc.base, my_sum, o);
+      // park the record in LDS (every lane's image reads are behind us in
+      // program order) for the coalesced store below
+      emit_record(a, o, dc.idx, (u32x4 *)wimg + lane * 5, stage);
     }
-    if (stage && !(a.tune & 8u) && (a.recs || a.recs32)) {   // tune bit 3: diagnostics, no stores
-      // identity order: the tile's 64 records are one contiguous 4 KB run
-      // (2 KB compact); each store instruction writes 1 KB contiguously
-      // instead of 64 scattered 16-byte pieces
-      __builtin_amdgcn_wave_barrier();
-      const u32x4 *st = (const u32x4 *)wimg;
-      u32x4 *dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + tile * (uint64_t)WAVE * 32u
-                                 : (uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
-      const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
-      const int lg = c32 ? 1 : 2;                 // log2 16-byte pieces per record
-      int kmax = c32 ? 2 : 4;
-      if (a.tune & 128u) kmax >>= 1;              // bit 7: diagnostics, half the bytes
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = k * WAVE + lane;   // 16-byte piece e of the tile's records
-        const int r = e >> lg;
-        if ((uint64_t)r < nrec && k < kmax) {
-          const u32x4 val = st[r * 5 + (e & ((1 << lg) - 1))];
-          if (a.tune & 64u) {            // bit 6: write-through, drop from L2 (sc1)
-            uint64_t *d8 = (uint64_t *)(dst + e);
-            __hip_atomic_store(d8, (uint64_t)val.x | ((uint64_t)val.y << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(d8 + 1, (uint64_t)val.z | ((uint64_t)val.w << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          } else if (a.tune & 32u) {     // bit 5: non-temporal stores
-            asm volatile("" ::: "memory");
-            __builtin_nontemporal_store(val, dst + e);
-          } else {
-            dst[e] = val;
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
+    if (stage && !(a.tune & 8u) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
+      flush_records(a, wimg, tile, lane);
     tile += step;
     dc = dn;
     dn = d2;
     idx2 = idx3;
+  }
+}
+
+// Lane kernel (RX_L4): frames of at most 64 bytes at a fixed stride, every
+// frame start 16-byte aligned (the host checks the buffer address and the
+// stride).  Small frames need no team streaming: lane q loads its own frame
+// as four 16-byte chunks (a wave's four loads cover the tile's 4 KB exactly;
+// each line is fetched once and served to its lanes from the caches), the
+// common IPv4 case is parsed from registers at fixed offsets (lane_fast),
+// anything else goes through the LDS image and lane_generic.  The next tile's
+// chunks are in flight while a tile is processed (two register sets used in
+// turn, so no in-flight load destination is ever copied).
+constexpr int LSLOT = 80;   // LDS bytes per lane: 64-byte frame image, then the record
+
+template <bool NT>
+__device__ __forceinline__ void lane_load(const RxKArgs &a, uint64_t tile, int lane, uint32_t nch,
+                                          u32x4 c[4]) {
+  uint64_t i = tile * WAVE + lane;
+  i = i < a.n ? i : a.n - 1;   // past-the-end lanes re-read the last frame (no record)
+  const u32x4 *p = (const u32x4 *)(a.frames + i * a.stride);
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    c[s] = ldc<NT>(p + min((uint32_t)s, nch - 1));   // chunks past the frame: masked at use
+}
+
+template <bool NT>
+__device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int lane, uint32_t nch,
+                                          const u32x4 c[4], uint8_t *wimg) {
+  const uint64_t i = tile * WAVE + lane;
+  uint8_t *slot = wimg + lane * LSLOT;
+  if (i < a.n && !(a.tune & 16u)) {
+    const uint32_t len = a.fixed_len;
+    uint32_t d[16];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bool in = (uint32_t)s < nch;
+      d[4 * s + 0] = in ? c[s].x : 0u;
+      d[4 * s + 1] = in ? c[s].y : 0u;
+      d[4 * s + 2] = in ? c[s].z : 0u;
+      d[4 * s + 3] = in ? c[s].w : 0u;
+    }
+    LaneRec o;
+    if (!lane_fast(a, d, len, o)) {
+      u32x4 *img = (u32x4 *)slot;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        img[s] = (u32x4){d[4 * s], d[4 * s + 1], d[4 * s + 2], d[4 * s + 3]};
+      // team-round equivalent: the sum of [team_start_of(0) = 32, len)
+      uint32_t ms = sum_chunk_from(img[2], 32, 32, (int)len, 0u);
+      ms = sum_chunk_from(img[3], 48, 32, (int)len, ms);
+      const FrameView v = {slot, a.frames + i * a.stride, 0, 64};
+      lane_generic(a, v, len, i * a.stride, ms, o);
+    }
+    emit_record(a, o, (uint32_t)i, (u32x4 *)slot, true);
+  }
+  if (!(a.tune & 8u) && (a.recs || a.recs32))
+    flush_records(a, wimg, tile, lane);
+}
+
+template <bool NT>
+__global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * LSLOT];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = threadIdx.x / WAVE;
+  uint8_t *wimg = lds + wv * WAVE * LSLOT;
+  const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
+  const uint64_t step = (uint64_t)gridDim.x * WPB;
+  const uint32_t nch = (a.fixed_len + 15u) >> 4;   // 1..4, uniform
+  uint64_t tile = (uint64_t)blockIdx.x * WPB + wv;
+  u32x4 c0[4], c1[4];
+  lane_load<NT>(a, tile, lane, nch, c0);
+  while (tile < ntiles) {
+    lane_load<NT>(a, tile + step, lane, nch, c1);
+    lane_tile<NT>(a, tile, lane, nch, c0, wimg);
+    tile += step;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c0[s] = c1[s];
   }
 }
 
@@ -785,6 +973,12 @@ int blocks_per_cu() {
 }  // namespace
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s) {
+  if (variant == RX_L4) {
+    const dim3 gd(grid), bd(WAVE * WPB);
+    if (a.tune & 1u) hipLaunchKernelGGL(rx_kernel_lane<true>, gd, bd, 0, s, a);
+    else hipLaunchKernelGGL(rx_kernel_lane<false>, gd, bd, 0, s, a);
+    return hipGetLastError();
+  }
   switch (variant) {
 #define X(name, T, S, D, AL) \
   case name: return launch_variant<T, S, D, AL>(a, grid, s);
@@ -795,6 +989,13 @@ hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s) {
 }
 
 int rx_variant_blocks_per_cu(int variant) {
+  if (variant == RX_L4) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel_lane<false>, WAVE * WPB, 0) !=
+        hipSuccess)
+      return 1;
+    return nb > 0 ? nb : 1;
+  }
   switch (variant) {
 #define X(name, T, S, D, AL) \
   case name: return blocks_per_cu<T, S, D, AL>();

@@ -43,12 +43,17 @@ assert ctypes.sizeof(RxOpts) == 36
 EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_batch", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
-           "pptk_rx_variant_count", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
+           "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
+
+# Kernel variants, in the order of enum RxVariant (pptk_amd/csrc/rx_internal.h).
+VARIANTS = ("T4S1", "T4S2", "T16S2", "T16S6", "T32S3", "T64S2", "T16S7L", "T32S4L",
+            "T32S3D7", "T16S6D1", "T8S2", "T16S4", "L4")
+RX_L4 = VARIANTS.index("L4")
 
 _libs = {}
 
@@ -96,6 +101,8 @@ def lib(path=None):
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
         L.pptk_rx_variant_count.restype = ctypes.c_int
+        L.pptk_rx_last_variant.argtypes = [vp]
+        L.pptk_rx_last_variant.restype = ctypes.c_int
         L.pptk_rx_register_ring.argtypes = [vp, vp, ctypes.c_size_t]
         L.pptk_rx_register_ring.restype = ctypes.c_int
         L.pptk_rx_unregister_ring.argtypes = [vp, vp]
@@ -141,6 +148,10 @@ class RxContext:
         rc = self._L.pptk_rx_set_tuning(self._ctx, variant, flags)
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_set_tuning({variant}, {flags}) failed")
+
+    def last_variant(self):
+        """Kernel variant of the last device batch (-1: none yet)."""
+        return self._L.pptk_rx_last_variant(self._ctx)
 
     def close(self):
         if self._ctx:

@@ -315,3 +315,91 @@ def test_empty_and_single(dev):
         got = _run(ctx, one, dev)
         d = diff_records(got, z["recs"][i:i + 1])
         assert not d, f"frame {i}: {d}"
+
+
+def _small_fixed_batches():
+    """Every golden frame of at most 64 bytes, grouped by length (a fixed-stride
+    batch has one length), with the records the reference produced."""
+    groups = {}
+    for name in GOLDEN_SETS:
+        z = load_golden(name)
+        for i in np.flatnonzero(z["len"] <= 64):
+            L = int(z["len"][i])
+            fr = z["buf"][int(z["off"][i]):int(z["off"][i]) + L]
+            groups.setdefault(L, ([], []))
+            groups[L][0].append(fr)
+            groups[L][1].append(z["recs"][i])
+    return groups
+
+
+@pytest.mark.parametrize("stride_kind", ["tight", "64", "96"])
+@pytest.mark.parametrize("compact", [False, True])
+def test_lane_kernel(stride_kind, compact, dev):
+    """RX_L4 (lane kernel: fixed stride, 16-byte aligned frames <= 64 B) on
+    every golden frame that short -- VLAN, IPv6, malformed, fragments, padded
+    and odd-length frames (the generic per-lane path) and plain IPv4 (the
+    register fast path) -- bit-exact, with the flow-hash array."""
+    from pptk_amd.rx import RX_L4
+    zk = load_golden("edge")
+    ctx = _ctx(zk)
+    groups = _small_fixed_batches()
+    assert len(groups) > 20
+    for L, (frs, recs) in sorted(groups.items()):
+        stride = {"tight": max(16, (L + 15) // 16 * 16), "64": 64, "96": 96}[stride_kind]
+        n = len(frs)
+        buf = np.zeros(n * stride + 16, np.uint8)
+        for k, fr in enumerate(frs):
+            buf[k * stride:k * stride + L] = fr
+            buf[k * stride + L:(k + 1) * stride] = 0xA5   # garbage after the frame
+        want = np.array(recs)
+        frames = torch.from_numpy(buf).to(dev)
+        h = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        got = ctx.batch_device(frames, n, stride=stride, fixed_len=L, hash_out=h,
+                               compact=compact)
+        torch.cuda.synchronize()
+        assert ctx.last_variant() == RX_L4, f"len {L}: lane kernel not selected"
+        got = got.cpu().numpy().reshape(-1)
+        if compact:
+            d = diff_records(got, to_rec32(want), dtype=REC32_DTYPE)
+        else:
+            d = diff_records(got, want)
+        assert not d, f"len {L} stride {stride}: {d}"
+        w = as_records(want)
+        hh = h.cpu().numpy().view(np.uint64)
+        assert np.array_equal(hh, np.where(w["flags"] & F_PARSED, w["flow_hash"], 0)), L
+
+
+def test_lane_kernel_large_batch(dev):
+    """Many tiles per wave (the prefetch loop), a ragged last tile, every 7th
+    frame corrupted, against the oracle; misaligned buffers fall back to the
+    team kernels with the same results."""
+    import framegen
+    from oracle.oracle import Oracle, make_opts
+    from pptk_amd.rx import RX_L4, RxContext
+    rng = np.random.default_rng(5)
+    n = 300_001
+    base = framegen.frame_v4(rng, 17, 64)
+    buf = np.tile(np.frombuffer(base, np.uint8), n).copy()
+    # vary addresses / ports / payload so every record differs
+    rnd = rng.integers(0, 256, size=(n, 64), dtype=np.uint8)
+    v = buf.reshape(n, 64)
+    v[:, 26:38] = rnd[:, 26:38]
+    v[:, 42:64] = rnd[:, 42:64]
+    v[::7, 50] ^= 0x5A                               # corrupt the UDP checksum of some
+    v[::11, 0] = 0                                   # (L2 bytes are not covered)
+    off = np.arange(n, dtype=np.uint64) * 64
+    lens = np.full(n, 64, np.uint16)
+    key = bytes(range(1, 17))
+    want = Oracle().rx_batch(buf, off, lens, opts=make_opts(key, 24, 48, 1 << 12))
+    ctx = RxContext(0, key, 24, 48, 1 << 12)
+    big = torch.zeros(buf.size + 64, dtype=torch.uint8, device=dev)
+    big[:buf.size] = torch.from_numpy(buf).to(dev)
+    for shift, lane in ((0, True), (16, True), (8, False)):
+        fr = big[shift:]
+        if shift:
+            fr[:buf.size] = torch.from_numpy(buf).to(dev)
+        got = ctx.batch_device(fr, n, stride=64, fixed_len=64)
+        torch.cuda.synchronize()
+        assert (ctx.last_variant() == RX_L4) == lane
+        d = diff_records(got.cpu().numpy().reshape(-1), want)
+        assert not d, f"shift {shift}: {d}"
