@@ -39,6 +39,13 @@ constexpr int IMG_CHUNKS = 8;     // 16-byte chunks parked in LDS per frame
 constexpr int IMG_STRIDE = 144;   // LDS bytes per frame slot (9 x 16: no b128 bank conflicts)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Explicit address spaces for every pointer the per-frame code dereferences:
+// a pointer the compiler cannot place becomes a FLAT access, which counts in
+// both vmcnt and lgkmcnt and may complete out of order, so every later wait
+// on the streaming loads degrades to vmcnt(0) -- a drain of the prefetch.
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t dot16(uint32_t w, uint32_t acc) {
@@ -105,17 +112,27 @@ struct Sip {
   }
 };
 
+// A value loaded from global memory on a rare path, made ready before the
+// paths join: the empty asm consumes it, so its vmcnt wait sits inside the
+// rare branch.  Consumed after the join instead, the wait would be a
+// vmcnt(0) on the common path -- a drain of the prefetched rounds.
+__device__ __forceinline__ uint32_t settle(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // A frame as seen by a lane: bytes [0, lim) from the LDS image (frame byte k
 // at img[m + k], image = aligned 16-byte chunks from floor16(frame start)),
 // everything else straight from global memory.
 struct FrameView {
-  const uint8_t *img;
-  const uint8_t *g;
+  const LDS_AS uint8_t *img;
+  const GLB_AS uint8_t *g;
   int m;
   int lim;
 
   __device__ __forceinline__ uint32_t u8(int k) const {
-    return k < lim ? (uint32_t)img[m + k] : (uint32_t)g[k];
+    if (k < lim) return (uint32_t)img[m + k];
+    return settle((uint32_t)g[k]);
   }
   __device__ __forceinline__ uint32_t be16(int k) const {
     return (u8(k) << 8) | u8(k + 1);
@@ -124,11 +141,11 @@ struct FrameView {
   __device__ __forceinline__ uint32_t le32(int k) const {
     if (k + 4 <= lim) {
       const int a = m + k;
-      const uint32_t *p = (const uint32_t *)(img + (a & ~3));
+      const LDS_AS uint32_t *p = (const LDS_AS uint32_t *)(img + (a & ~3));
       return __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(a & 3));
     }
-    return (uint32_t)g[k] | ((uint32_t)g[k + 1] << 8) | ((uint32_t)g[k + 2] << 16) |
-           ((uint32_t)g[k + 3] << 24);
+    return settle((uint32_t)g[k] | ((uint32_t)g[k + 1] << 8) | ((uint32_t)g[k + 2] << 16) |
+                  ((uint32_t)g[k + 3] << 24));
   }
 };
 
@@ -295,12 +312,12 @@ __device__ uint32_t sum_abs(const FrameView &v, int a, int b) {
   if (a < hi_img) {
     const int lo_o = v.m + a, hi_o = v.m + hi_img;
     for (int d = lo_o & ~3; d < hi_o; d += 4) {
-      const uint32_t w = *(const uint32_t *)(v.img + d);
+      const uint32_t w = *(const LDS_AS uint32_t *)(v.img + d);
       s = dot16(w & bmask(min(max(lo_o - d, 0), 4), min(max(hi_o - d, 0), 4)), s);
     }
   }
   for (int k = max(a, v.lim); k < b; ++k)
-    s += (uint32_t)v.g[k] << (((v.m + k) & 1) * 8);
+    s += settle((uint32_t)v.g[k]) << (((v.m + k) & 1) * 8);
   return s;
 }
 
@@ -626,7 +643,7 @@ __device__ __forceinline__ bool lane_fast(const RxKArgs &a, const uint32_t d[16]
 // LDS slot `st` for flush_records (batch order) or stored directly
 // (permuted order: records scatter).
 __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, uint32_t idx,
-                                            u32x4 *st, bool stage) {
+                                            LDS_AS u32x4 *st, bool stage) {
   const uint32_t *w = o.w;
   if (a.hash)
     a.hash[idx] = o.fh;
@@ -646,25 +663,31 @@ __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, 
     r2 = (u32x4){w[8], w[9], w[10], w[11]};
     r3 = (u32x4){w[12], w[13], w[14], w[15]};
   }
-  u32x4 *dst = st;
-  if (!stage)
-    dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + (uint64_t)idx * 32u
-                        : (uint8_t *)a.recs + (uint64_t)idx * 64u);
-  dst[0] = r0; dst[1] = r1;
-  if (!c32) { dst[2] = r2; dst[3] = r3; }
+  if (stage) {
+    st[0] = r0; st[1] = r1;
+    if (!c32) { st[2] = r2; st[3] = r3; }
+  } else {
+    GLB_AS u32x4 *dst = (GLB_AS u32x4 *)(c32 ? (GLB_AS uint8_t *)a.recs32 + (uint64_t)idx * 32u
+                                             : (GLB_AS uint8_t *)a.recs + (uint64_t)idx * 64u);
+    dst[0] = r0; dst[1] = r1;
+    if (!c32) { dst[2] = r2; dst[3] = r3; }
+  }
 }
 
 // Batch order: the tile's 64 records, parked in the wave's LDS at an 80-byte
 // pitch, are one contiguous 4 KB run (2 KB compact) in memory; each store
 // instruction writes 1 KB contiguously instead of 64 scattered 16-byte
 // pieces.
-__device__ __forceinline__ void flush_records(const RxKArgs &a, const uint8_t *wimg, uint64_t tile,
+__device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uint8_t *wimg, uint64_t tile,
                                               int lane) {
+#ifdef PPTK_RX_EXP_NO_FLUSH
+  return;
+#endif
   const bool c32 = a.recs32 != nullptr;
   __builtin_amdgcn_wave_barrier();
-  const u32x4 *st = (const u32x4 *)wimg;
-  u32x4 *dst = (u32x4 *)(c32 ? (uint8_t *)a.recs32 + tile * (uint64_t)WAVE * 32u
-                             : (uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
+  const LDS_AS u32x4 *st = (const LDS_AS u32x4 *)wimg;
+  GLB_AS u32x4 *dst = (GLB_AS u32x4 *)(c32 ? (GLB_AS uint8_t *)a.recs32 + tile * (uint64_t)WAVE * 32u
+                                           : (GLB_AS uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
   const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
   const int lg = c32 ? 1 : 2;                 // log2 16-byte pieces per record
   int kmax = c32 ? 2 : 4;
@@ -676,7 +699,7 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const uint8_t *w
     if ((uint64_t)r < nrec && k < kmax) {
       const u32x4 val = st[r * 5 + (e & ((1 << lg) - 1))];
       if (a.tune & 64u) {            // bit 6: write-through, drop from L2 (sc1)
-        uint64_t *d8 = (uint64_t *)(dst + e);
+        GLB_AS uint64_t *d8 = (GLB_AS uint64_t *)(dst + e);
         __hip_atomic_store(d8, (uint64_t)val.x | ((uint64_t)val.y << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(d8 + 1, (uint64_t)val.z | ((uint64_t)val.w << 32), __ATOMIC_RELAXED,
@@ -721,7 +744,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const int g = lane / T, j = lane % T;
-  uint8_t *wimg = lds + wv * WAVE * IMG_STRIDE;
+  LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * IMG_STRIDE;
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
   const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
   // Tile order: strided over the grid (default), or, with tune bit 8
@@ -773,13 +796,13 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
         const int m = (int)(cb.pb & ALM);       // frame start inside its first chunk row
         const int c_img = m >> 4;                  // first chunk holding frame bytes
         const int nch = (m + (int)cb.pl + 15) >> 4;
-        uint8_t *img = wimg + q * IMG_STRIDE;
+        LDS_AS uint8_t *img = wimg + q * IMG_STRIDE;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           if (s * T < IMGC + (int)(ALM >> 4)) {
             const int ci = s * T + j - c_img;      // image = 16-byte chunks from floor16(frame)
             if (ci >= 0 && ci < IMGC)
-              *(u32x4 *)(img + 16 * ci) = cb.v[s];
+              *(LDS_AS u32x4 *)(img + 16 * ci) = cb.v[s];
           }
         }
         uint32_t acc = 0;
@@ -824,15 +847,16 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
         if (nch > S * T) {
           const u32x4 *c0 = (const u32x4 *)(a.frames + (dc.base - (uint64_t)ma));
           for (int c = S * T; c < nch; ++c)
-            my_sum = sum_chunk_from(ldc<NT>(c0 + c), 16 * c - ma, 0, (int)dc.len, my_sum);
+            my_sum = settle(sum_chunk_from(ldc<NT>(c0 + c), 16 * c - ma, 0, (int)dc.len, my_sum));
         }
       }
-      const FrameView v = {wimg + lane * IMG_STRIDE, a.frames + dc.base, m, 16 * IMGC - m};
+      const FrameView v = {wimg + lane * IMG_STRIDE, (const GLB_AS uint8_t *)a.frames + dc.base, m,
+                           16 * IMGC - m};
       LaneRec o;
       lane_generic(a, v, dc.len, dc.base, my_sum, o);
       // park the record in LDS (every lane's image reads are behind us in
       // program order) for the coalesced store below
-      emit_record(a, o, dc.idx, (u32x4 *)wimg + lane * 5, stage);
+      emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
     }
     if (stage && !(a.tune & 8u) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
       flush_records(a, wimg, tile, lane);
@@ -867,9 +891,9 @@ __device__ __forceinline__ void lane_load(const RxKArgs &a, uint64_t tile, int l
 
 template <bool NT>
 __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int lane, uint32_t nch,
-                                          const u32x4 c[4], uint8_t *wimg) {
+                                          const u32x4 c[4], LDS_AS uint8_t *wimg) {
   const uint64_t i = tile * WAVE + lane;
-  uint8_t *slot = wimg + lane * LSLOT;
+  LDS_AS uint8_t *slot = wimg + lane * LSLOT;
   if (i < a.n && !(a.tune & 16u)) {
     const uint32_t len = a.fixed_len;
     uint32_t d[16];
@@ -883,17 +907,17 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
     }
     LaneRec o;
     if (!lane_fast(a, d, len, o)) {
-      u32x4 *img = (u32x4 *)slot;
+      LDS_AS u32x4 *img = (LDS_AS u32x4 *)slot;
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         img[s] = (u32x4){d[4 * s], d[4 * s + 1], d[4 * s + 2], d[4 * s + 3]};
       // team-round equivalent: the sum of [team_start_of(0) = 32, len)
       uint32_t ms = sum_chunk_from(img[2], 32, 32, (int)len, 0u);
       ms = sum_chunk_from(img[3], 48, 32, (int)len, ms);
-      const FrameView v = {slot, a.frames + i * a.stride, 0, 64};
+      const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + i * a.stride, 0, 64};
       lane_generic(a, v, len, i * a.stride, ms, o);
     }
-    emit_record(a, o, (uint32_t)i, (u32x4 *)slot, true);
+    emit_record(a, o, (uint32_t)i, (LDS_AS u32x4 *)slot, true);
   }
   if (!(a.tune & 8u) && (a.recs || a.recs32))
     flush_records(a, wimg, tile, lane);
@@ -904,7 +928,7 @@ __global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * LSLOT];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
-  uint8_t *wimg = lds + wv * WAVE * LSLOT;
+  LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * LSLOT;
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
   const uint64_t step = (uint64_t)gridDim.x * WPB;
   const uint32_t nch = (a.fixed_len + 15u) >> 4;   // 1..4, uniform

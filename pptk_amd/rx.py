@@ -101,8 +101,9 @@ def lib(path=None):
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
         L.pptk_rx_variant_count.restype = ctypes.c_int
-        L.pptk_rx_last_variant.argtypes = [vp]
-        L.pptk_rx_last_variant.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_last_variant"):   # (absent from older A/B builds)
+            L.pptk_rx_last_variant.argtypes = [vp]
+            L.pptk_rx_last_variant.restype = ctypes.c_int
         L.pptk_rx_register_ring.argtypes = [vp, vp, ctypes.c_size_t]
         L.pptk_rx_register_ring.restype = ctypes.c_int
         L.pptk_rx_unregister_ring.argtypes = [vp, vp]
