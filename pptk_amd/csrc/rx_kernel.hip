@@ -276,12 +276,22 @@ __device__ __forceinline__ uint32_t sum_chunk(u32x4 c, int o, int rs, int re, ui
   return acc;
 }
 
-// Team-round chunk sum: whole chunks from the team's first chunk on (no head
-// masking), only bytes past the frame end masked.  `o` = frame offset.
+// Team-round chunk sum: every chunk that starts in [start, len) is summed
+// whole -- no byte masking at either end, so every lane runs the same four
+// dot2 ops whatever its frame's length.  The chunk holding the frame's last
+// byte therefore also adds the bytes [len, end of that chunk), which the
+// owning lane subtracts once per frame (tail_past_end).  `o` = frame offset.
+//
+// MASKED instead masks the bytes past the end inside the chunk (no
+// correction needed): the choice for fixed-stride batches, whose frames all
+// end in the same one or two chunk slots of a round, so the masking runs on
+// few slots -- cheaper there than the per-frame correction, whose extra load
+// of the last chunk costs C1500 5 %.
+template <bool MASKED = false>
 __device__ __forceinline__ uint32_t sum_chunk_from(u32x4 c, int o, int start, int len,
                                                    uint32_t acc) {
   uint32_t t;
-  if (o + 16 <= len) {
+  if (!MASKED || o + 16 <= len) {
     t = dot16(c.x, 0);
     t = dot16(c.y, t);
     t = dot16(c.z, t);
@@ -292,7 +302,27 @@ __device__ __forceinline__ uint32_t sum_chunk_from(u32x4 c, int o, int start, in
     for (int d = 0; d < 4; ++d)
       t = dot16(c[d] & bmask(0, min(max(len - (o + 4 * d), 0), 4)), t);
   }
-  return o >= start ? acc + t : acc;
+  return (o >= start && o < len) ? acc + t : acc;
+}
+
+// Frame offset of the aligned 16-byte chunk holding the last byte of a frame
+// of `len` bytes that starts at `m` inside its chunk (len >= 1).
+__device__ __forceinline__ int last_chunk_off(int m, int len) {
+  return ((m + len - 1) & ~15) - m;
+}
+
+// What sum_chunk_from over-counted for this frame: the bytes past its end
+// in its last chunk `tc`, if that chunk was summed (it starts at or after
+// the team start ts); absolute pairing, like the team sums.
+__device__ __forceinline__ uint32_t tail_past_end(u32x4 tc, int m, int len, int ts) {
+  const int e = (m + len) & 15;   // first byte past the end inside the chunk
+  if (len <= 0 || e == 0 || last_chunk_off(m, len) < ts)
+    return 0;
+  uint32_t t = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+    t = dot16(tc[d] & bmask(min(max(e - 4 * d, 0), 4), 4), t);
+  return t;
 }
 
 // First chunk boundary (frame offset) at or after byte 18 of a frame whose
@@ -448,7 +478,8 @@ struct LaneRec {
 // frame bytes [team_start_of(v.m), len), flow hash, bucket hash, and (tx
 // batches) the checksum stores.  DESIGN.md "Record semantics" steps 1-9.
 __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &v, uint32_t len,
-                                             uint64_t base, uint32_t my_sum, LaneRec &o) {
+                                             uint64_t base, uint32_t my_sum, u32x4 tailc,
+                                             LaneRec &o) {
   const int m = v.m;
   const Parse p = parse_frame(v, len);
   uint32_t flags = p.flags;
@@ -495,9 +526,11 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
       ps = dot16(s1, ps); ps = dot16(s2, ps); ps = dot16(s3, ps);
       ps = dot16(d0, ps); ps = dot16(d1, ps); ps = dot16(d2, ps); ps = dot16(d3, ps);
       ps += bswap16(proto) + bswap16(l4len);   // > 0: proto is 6 or 17
-      // region [rs, re) = [ts, len) - [ts, rs) - [re, len), mod 0xffff
+      // region [rs, re) = [ts, L16) - [ts, rs) - [re, len) - [len, L16), mod
+      // 0xffff, where the team sum covered [ts, L16): L16 = the end of the
+      // chunk holding the last byte
       const int ts = team_start_of(m);
-      uint32_t rsum = fold16(my_sum);
+      uint32_t rsum = fold16(my_sum) + (0xffffu - fold16(tail_past_end(tailc, m, (int)len, ts)));
       if ((int)rs > ts)
         rsum += 0xffffu - fold16(sum_abs(v, ts, (int)rs));
       if (re < len)
@@ -720,12 +753,17 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
 // need 2 waves/SIMD; the small-frame variants 4.
 template <int T, int S>
 constexpr int min_waves_per_simd() { return S * T >= 32 ? 2 : 4; }
+#ifndef PPTK_RX_D1_WAVES
+#define PPTK_RX_D1_WAVES 3
+#endif
+template <int T, int S, int D>
+constexpr int min_waves() { return D == 1 && S * T >= 32 ? PPTK_RX_D1_WAVES : min_waves_per_simd<T, S>(); }
 
 // D = rounds in flight; (D + 1) must divide T so that the prefetch ring is
 // back in its starting registers at the tile boundary (no moves of in-flight
 // load destinations, which would force vmcnt waits).
 template <int T, int S, int D, int AL, bool NT, bool GATHER>
-__global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_kernel(RxKArgs a) {
+__global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(RxKArgs a) {
   if constexpr (GATHER) {
     // length-group launch (pptk_rx_batch_device_mixed): this launch owns
     // positions [*range_lo, *range_hi) of the binned order, known on the
@@ -778,6 +816,13 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
     // is loaded here, the dependent offset/length of tile + 2 nwaves (whose
     // index arrived during the previous tile) before the last round group.
     const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
+    // the chunk holding the last byte of this lane's frame (for the
+    // over-count correction of the unmasked team sums); issued before this
+    // tile's rounds so that waiting for it never drains them
+    u32x4 tailc = (u32x4){0u, 0u, 0u, 0u};   // (masked sums: nothing to correct)
+    if constexpr (GATHER)
+      tailc = *(const u32x4 *)(a.frames + ((dc.base + (uint64_t)max(dc.len, 1u) - 1u) &
+                                           ~(uint64_t)15));
     // ---- streaming rounds: team g sums frame g*T + r over [team_start, len).
     // Fixed-slot ring of D + 1 rounds: round r lives in slot r % (D + 1); a
     // group of D + 1 rounds is unrolled so every slot index is a constant and
@@ -810,12 +855,12 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           const int c = s * T + j;
-          acc = sum_chunk_from(cb.v[s], 16 * c - m, ts, (int)cb.pl, acc);
+          acc = sum_chunk_from<!GATHER>(cb.v[s], 16 * c - m, ts, (int)cb.pl, acc);
         }
         if (!UNROLL && nch > S * T) {  // frames longer than the staged chunks
           const u32x4 *c0 = (const u32x4 *)(a.frames + (cb.pb - (uint64_t)m));
           for (int c = S * T + j; c < nch; c += T)
-            acc = sum_chunk_from(ldc<NT>(c0 + c), 16 * c - m, ts, (int)cb.pl, acc);
+            acc = sum_chunk_from<!GATHER>(ldc<NT>(c0 + c), 16 * c - m, ts, (int)cb.pl, acc);
         }
         acc = team_sum<T>(acc);
         if (j == r)
@@ -847,13 +892,14 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves_per_simd<T, S>())) void rx_k
         if (nch > S * T) {
           const u32x4 *c0 = (const u32x4 *)(a.frames + (dc.base - (uint64_t)ma));
           for (int c = S * T; c < nch; ++c)
-            my_sum = settle(sum_chunk_from(ldc<NT>(c0 + c), 16 * c - ma, 0, (int)dc.len, my_sum));
+            my_sum = settle(sum_chunk_from<!GATHER>(ldc<NT>(c0 + c), 16 * c - ma, 0, (int)dc.len,
+                                                    my_sum));
         }
       }
       const FrameView v = {wimg + lane * IMG_STRIDE, (const GLB_AS uint8_t *)a.frames + dc.base, m,
                            16 * IMGC - m};
       LaneRec o;
-      lane_generic(a, v, dc.len, dc.base, my_sum, o);
+      lane_generic(a, v, dc.len, dc.base, my_sum, tailc, o);
       // park the record in LDS (every lane's image reads are behind us in
       // program order) for the coalesced store below
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
@@ -915,7 +961,9 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
       uint32_t ms = sum_chunk_from(img[2], 32, 32, (int)len, 0u);
       ms = sum_chunk_from(img[3], 48, 32, (int)len, ms);
       const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + i * a.stride, 0, 64};
-      lane_generic(a, v, len, i * a.stride, ms, o);
+      const uint32_t lc = len ? (len - 1u) >> 4 : 0u;   // chunk holding the last byte
+      const u32x4 tailc = lc == 0 ? c[0] : lc == 1 ? c[1] : lc == 2 ? c[2] : c[3];
+      lane_generic(a, v, len, i * a.stride, ms, tailc, o);
     }
     emit_record(a, o, (uint32_t)i, (LDS_AS u32x4 *)slot, true);
   }
