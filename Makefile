@@ -58,3 +58,8 @@ tools/libmembench.so: tools/membench.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
 all: tools/libmembench.so
+
+tools/librwmix.so: tools/rwmix.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
+
+all: tools/librwmix.so

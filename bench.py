@@ -442,6 +442,20 @@ def main():
     if not args.no_membench:
         from tools.membench import measure
         box = measure(prim["_batch"]["frames"])
+        b = prim["_batch"]
+        if "stride" in b and "off" not in b:
+            # the speed of light of this launch's traffic mix: the same frame
+            # bytes read in the same 64-frame tiles, 4 KB of records written
+            # per tile, nothing computed (tools/rwmix.hip)
+            from tools.rwmix import mix_ms
+            rb = 64 * b["stride"]
+            ntiles = n // 64
+            if rb % 16 == 0:
+                ms = mix_ms(b["frames"], rb, ntiles, prim["_recs"], 4096,
+                            nt=1 if primary_cfg == "c1500" else 0)
+                box["mix_ms"] = round(ms, 4)
+                box["mix_desc"] = (f"{ntiles} tiles x {rb} B read + 4096 B written, "
+                                   "grid-strided, no compute")
         log(f"[rank {rank}] box HBM: {box}")
 
     bytes_per_launch = prim["bytes"]
@@ -458,6 +472,11 @@ def main():
                 "traffic_source": tsrc,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_ms": round(kernel_ms, 4)}
+    if box and "mix_ms" in box:
+        # fraction of this GPU's speed of light for the same read/write mix
+        # (a trivial kernel moving the same bytes, tools/rwmix.hip)
+        roofline["mix_sol_ms"] = box["mix_ms"]
+        roofline["mix_sol_frac"] = round(box["mix_ms"] / kernel_ms, 4)
 
     # the same batch with compact 32-byte records (struct pptk_rx_rec32)
     rec32 = None

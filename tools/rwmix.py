@@ -1,0 +1,88 @@
+"""BENCH TOOLING: read/write mix microbenchmark (tools/rwmix.hip).
+
+    python tools/rwmix.py            -> one JSON line: ms per setting
+
+Reads 24 GiB worth of tiles (a 6 GiB buffer read 4 times over would hit
+the caches differently, so the buffer is the full 24 GiB) and writes 1/24
+of that, in bursts of wb bytes per rb-byte tile, for several burst sizes at
+the same read:write ratio; plus read-only and write-only references."""
+import ctypes
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _lib():
+    L = ctypes.CDLL(os.path.join(HERE, "librwmix.so"))
+    vp = ctypes.c_void_p
+    L.rwmix_run.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                            ctypes.c_int, ctypes.c_int, vp, vp]
+    return L
+
+
+def mix_ms(inp, rb, ntiles, out, wb, nt=1, reps=8):
+    """Median ms of the trivial stream over the same bytes as an rx launch:
+    ntiles tiles of rb bytes read from torch uint8 CUDA tensor `inp` (only
+    read), wb bytes written per tile into `out` -- the speed of light of
+    that read/write mix on this GPU (no parsing, no hashing, no sums)."""
+    import torch
+    assert rb % 16 == 0 and wb % 16 == 0
+    assert inp.numel() >= ntiles * rb and out.numel() >= ntiles * wb
+    L = _lib()
+    dev = inp.device
+    sink = torch.zeros(64, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    grid = torch.cuda.get_device_properties(dev).multi_processor_count * 2
+    ts = []
+    for k in range(reps + 2):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        L.rwmix_run(inp.data_ptr(), out.data_ptr(), ntiles, rb, wb, nt, grid, sink.data_ptr(),
+                    ctypes.c_void_p(s.cuda_stream))
+        b.record()
+        torch.cuda.synchronize(dev)
+        if k >= 2:
+            ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    import torch
+    L = _lib()
+    vp = ctypes.c_void_p
+    dev = torch.device("cuda", 0)
+    total = 24 * 1024 ** 3
+    inp = torch.empty(total, dtype=torch.uint8, device=dev)
+    inp.fill_(1)
+    out = torch.empty(total // 24 + (1 << 20), dtype=torch.uint8, device=dev)
+    sink = torch.zeros(64, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    settings = [(96 << 10, 0), (96 << 10, 4 << 10), (192 << 10, 8 << 10), (384 << 10, 16 << 10),
+                (768 << 10, 32 << 10), (1536 << 10, 64 << 10), (48 << 10, 2 << 10)]
+    res = {}
+    for rounds in range(3):
+        for nt in (1, 0):
+            for grid_mult in (2,):
+                for rb, wb in settings:
+                    ntiles = total // rb
+                    key = f"rb{rb >> 10}k_wb{wb >> 10}k_nt{nt}"
+                    ts = []
+                    for k in range(4):
+                        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        a.record()
+                        L.rwmix_run(inp.data_ptr(), out.data_ptr(), ntiles, rb, wb, nt,
+                                    ncu * grid_mult, sink.data_ptr(), vp(s.cuda_stream))
+                        b.record()
+                        torch.cuda.synchronize()
+                        if k:
+                            ts.append(a.elapsed_time(b))
+                    res.setdefault(key, []).extend(ts)
+    out_ = {k: round(sorted(v)[len(v) // 2], 4) for k, v in res.items()}
+    print(json.dumps(out_))
+
+
+if __name__ == "__main__":
+    main()
