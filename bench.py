@@ -324,6 +324,41 @@ def tx_bench(ctx, b, n, dev, steps, warmup):
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
 
 
+def rewrite_bench(ctx, n, dev, rank, steps, warmup):
+    """Header rewrite with incremental checksum updates (SURVEY 8(f) row 4,
+    pptk_tx_rewrite_device) of a C64 batch in place: TTL decrement + new
+    source/destination + new ports on every frame (a NAT + forwarding step;
+    each frame is read once, 14 bytes of it written)."""
+    import torch
+    from pptk_amd.records import REWRITE_DTYPE
+    from tools.synth import make_batch
+    b = make_batch("c64", n, dev, first=rank * n)
+    rw = np.zeros(1, REWRITE_DTYPE)
+    rw["ops"], rw["src"], rw["dst"], rw["sport"], rw["dport"] = 0x1F, 0xC0A80A01, 0x0A000002, 4242, 443
+    rw_t = torch.from_numpy(rw.view(np.uint8).copy()).to(dev)
+    assert warmup + steps < 64          # the synthetic TTL is 64: stays > 0
+    kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
+    for _ in range(warmup):
+        ctx.tx_rewrite_device(b["frames"], n, rw_t, **kw)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for a, z in ev:
+        a.record()
+        ctx.tx_rewrite_device(b["frames"], n, rw_t, **kw)
+        z.record()
+    torch.cuda.synchronize(dev)
+    ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
+    ach = b["bytes"] / (ms * 1e-3) / 1e9
+    del b
+    torch.cuda.empty_cache()
+    return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "kernel_ms": round(ms, 4),
+            "workload": "C64 frames, TTL-1 + src/dst/ports rewritten in place, "
+                        "checksums updated incrementally (RFC 1624)",
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
+
+
 def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
     """Batched ip_permitted over the records of a C64
     batch: buckets of the /24 source prefixes in 2^16 buckets, every IPv4
@@ -519,10 +554,13 @@ def main():
             del r["_batch"], r["_recs"]
             torch.cuda.empty_cache()
 
-    permit = None
+    permit = rewrite = None
     if not args.no_secondary and args.only is None:
         permit = permit_bench(n, dev, ws, rank, args.steps, args.warmup)
         log(f"[rank {rank}] permit: {permit}")
+        if args.steps + args.warmup < 64:
+            rewrite = rewrite_bench(ctx, n, dev, rank, args.steps, args.warmup)
+            log(f"[rank {rank}] rewrite: {rewrite}")
 
     if rank == 0:
         line = {
@@ -553,6 +591,7 @@ def main():
             "secondary": secondary,
             "permit": permit,
             "tx": tx,
+            "rewrite": rewrite,
         }
         print(json.dumps(line), flush=True)
     if ws > 1:

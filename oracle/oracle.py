@@ -58,6 +58,24 @@ def _tx(fn, buf, off, lens, stride, fixed_len, n):
     return out
 
 
+def _rewrite(fn, buf, rw, off, lens, stride, fixed_len, n):
+    from pptk_amd.records import REWRITE_DTYPE
+    out = np.array(buf, dtype=np.uint8, copy=True)
+    rw = np.ascontiguousarray(rw, dtype=REWRITE_DTYPE)
+    off = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    lens = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    if n is None:
+        n = len(off) if off is not None else len(buf) // stride
+    status = np.zeros(n, dtype=np.uint8)
+    fn(_ptr(out), _ptr(off), _ptr(lens), ctypes.c_uint64(stride), ctypes.c_uint32(fixed_len),
+       ctypes.c_size_t(n), _ptr(rw), ctypes.c_uint64(len(rw)), _ptr(status))
+    return out, status
+
+
+_RW_ARGS = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t, _vp,
+            ctypes.c_uint64, _vp]
+
+
 class _Lib:
     prefix = ""
 
@@ -113,6 +131,12 @@ class Oracle(_Lib):
         L.orc_cksum_loop.restype = ctypes.c_uint32
         L.orc_cksum_loop.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint64]
         L.orc_tx_batch.restype = None
+        L.orc_rewrite_batch.restype = None
+        L.orc_rewrite_batch.argtypes = _RW_ARGS
+        L.orc_update_cksum16.restype = ctypes.c_uint16
+        L.orc_update_cksum16.argtypes = [ctypes.c_uint16] * 3
+        L.orc_update_cksum32.restype = ctypes.c_uint16
+        L.orc_update_cksum32.argtypes = [ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32]
         L.orc_tx_batch.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_size_t]
         L.orc_permit_batch.restype = None
@@ -139,6 +163,17 @@ class Oracle(_Lib):
     def tx_batch(self, buf, off=None, lens=None, stride=0, fixed_len=0, n=None):
         """Tx-side checksum setting; returns an updated copy of buf."""
         return _tx(self.lib.orc_tx_batch, buf, off, lens, stride, fixed_len, n)
+
+    def rewrite_batch(self, buf, rw, off=None, lens=None, stride=0, fixed_len=0, n=None):
+        """Header rewrite with incremental checksum updates (REWRITE_DTYPE
+        entries, 1 or n); returns (updated copy of buf, status per frame)."""
+        return _rewrite(self.lib.orc_rewrite_batch, buf, rw, off, lens, stride, fixed_len, n)
+
+    def update_cksum16(self, c, old, new):
+        return self.lib.orc_update_cksum16(c, old, new)
+
+    def update_cksum32(self, c, old, new):
+        return self.lib.orc_update_cksum32(c, old, new)
 
     def cksum(self, data):
         b = bytes(data)
@@ -202,6 +237,12 @@ class Reference(_Lib):
         L.ref_cksum_loop.restype = ctypes.c_uint32
         L.ref_cksum_loop.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint64]
         L.ref_tx_batch.restype = None
+        L.ref_rewrite_batch.restype = None
+        L.ref_rewrite_batch.argtypes = _RW_ARGS
+        L.ref_update_cksum16.restype = ctypes.c_uint16
+        L.ref_update_cksum16.argtypes = [ctypes.c_uint16] * 3
+        L.ref_update_cksum32.restype = ctypes.c_uint16
+        L.ref_update_cksum32.argtypes = [ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32]
         L.ref_tx_batch.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_size_t]
         L.ref_permit_batch.restype = None
@@ -226,6 +267,17 @@ class Reference(_Lib):
         """The reference's *_set_cksum_calc on every parsed frame; returns an
         updated copy of buf."""
         return _tx(self.lib.ref_tx_batch, buf, off, lens, stride, fixed_len, n)
+
+    def rewrite_batch(self, buf, rw, off=None, lens=None, stride=0, fixed_len=0, n=None):
+        """The reference's incremental-update functions (iphdr/ipcksum.h:
+        213-393) as pptk_tx_rewrite_device composes them."""
+        return _rewrite(self.lib.ref_rewrite_batch, buf, rw, off, lens, stride, fixed_len, n)
+
+    def update_cksum16(self, c, old, new):
+        return self.lib.ref_update_cksum16(c, old, new)
+
+    def update_cksum32(self, c, old, new):
+        return self.lib.ref_update_cksum32(c, old, new)
 
     def tokens_refill(self, hash_size, batch_size, initial, add, k, tokens):
         """The reference's batch_timer_fn for timer k (buckets

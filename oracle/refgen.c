@@ -17,6 +17,8 @@
  *   udp6_cksum_calc, ip_cksum_feed, ip_cksum_postprocess  (iphdr/ipcksum.*)
  *   siphash_buf, siphash64                         (misc/siphash.h)
  *   ip_permitted, ipv6_permitted                   (iphash/iphash.c)
+ *   ip_update_cksum16/32, ip_decr_ttl_cksum_update, ip_set_src/dst_cksum_update,
+ *   tcp/udp_set_src/dst_port_cksum_update, ip_ttl   (iphdr/ipcksum.h, iphdr.h)
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -489,4 +491,71 @@ void ref_tx_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64
         udp_set_cksum_calc(ip, ip_hdr_len(ip), l4, r.l4_len);
     }
   }
+}
+
+/* ---- header rewrite: the reference's own incremental-update functions
+ * (iphdr/ipcksum.h:213-393), called in the order and under the conditions
+ * pptk_tx_rewrite_device defines (include/pptk_rx.h): on frames the record
+ * composition parses as IPv4; L4 follow-ups only with an L4 header (proto
+ * passed as 0 otherwise, which makes ip_set_src/dst_cksum_update touch the
+ * IP header alone); TTL 0 under DECR_TTL skipped (the reference abort()s). */
+void ref_rewrite_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                       uint32_t fixed_len, size_t n, const struct pptk_rewrite *rw,
+                       uint64_t rw_count, uint8_t *status)
+{
+  struct ref_opts o;
+  size_t i;
+  memset(&o, 0, sizeof(o));
+  for (i = 0; i < n; i++) {
+    uint8_t *f = buf + (off ? off[i] : i * stride);
+    const uint32_t flen = len ? len[i] : fixed_len;
+    const struct pptk_rewrite *w = &rw[rw_count == 1 ? 0 : i];
+    struct pptk_rx_rec r;
+    uint8_t *ip, *l4, st = 0;
+    int l4ok;
+    ref_rx_one(f, flen, &o, &r, 0);
+    if ((r.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED | PPTK_RX_F_IPV6)) != PPTK_RX_F_PARSED)
+      goto done;
+    ip = f + r.l3_off;
+    l4 = f + r.l4_off;
+    l4ok = (r.flags & PPTK_RX_F_L4) != 0;
+    if ((w->ops & PPTK_RW_DECR_TTL) && ip_ttl(ip) == 0) {
+      st = PPTK_RW_ST_TTL_ZERO;
+      goto done;
+    }
+    st = PPTK_RW_ST_IP | (l4ok ? PPTK_RW_ST_L4 : 0);
+    if (w->ops & PPTK_RW_DECR_TTL) {
+      if (!ip_decr_ttl_cksum_update(ip))
+        st |= PPTK_RW_ST_EXPIRED;
+    }
+    if (w->ops & PPTK_RW_SRC)
+      ip_set_src_cksum_update(ip, ip_hdr_len(ip), l4ok ? r.proto : 0, l4, r.l4_len, w->src);
+    if (w->ops & PPTK_RW_DST)
+      ip_set_dst_cksum_update(ip, ip_hdr_len(ip), l4ok ? r.proto : 0, l4, r.l4_len, w->dst);
+    if (l4ok && (w->ops & PPTK_RW_SPORT)) {
+      if (r.proto == 6)
+        tcp_set_src_port_cksum_update(l4, r.l4_len, w->sport);
+      else
+        udp_set_src_port_cksum_update(l4, r.l4_len, w->sport);
+    }
+    if (l4ok && (w->ops & PPTK_RW_DPORT)) {
+      if (r.proto == 6)
+        tcp_set_dst_port_cksum_update(l4, r.l4_len, w->dport);
+      else
+        udp_set_dst_port_cksum_update(l4, r.l4_len, w->dport);
+    }
+done:
+    if (status)
+      status[i] = st;
+  }
+}
+
+uint16_t ref_update_cksum16(uint16_t c, uint16_t o, uint16_t nw)
+{
+  return ip_update_cksum16(c, o, nw);
+}
+
+uint16_t ref_update_cksum32(uint16_t c, uint32_t o, uint32_t nw)
+{
+  return (uint16_t)ip_update_cksum32(c, o, nw);
 }

@@ -540,3 +540,123 @@ void orc_tx_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64
     }
   }
 }
+
+/* ---- header rewrite with incremental checksum update
+ * (include/pptk_rx.h pptk_tx_rewrite_device; reference iphdr/ipcksum.h:
+ * 213-393).  ip_update_cksum16 (:213-226): RFC 1624 eqn. 3 on host-order
+ * values of big-endian fields, folded with end-around carry. */
+uint16_t orc_update_cksum16(uint16_t cksum, uint16_t old16, uint16_t new16)
+{
+  uint32_t s = (uint16_t)~cksum;
+  s += (uint16_t)~old16;
+  s += new16;
+  while (s >> 16)
+    s = (s & 0xffff) + (s >> 16);
+  return (uint16_t)~s;
+}
+
+/* ip_update_cksum32 (:228-236): high half first, then low half */
+uint16_t orc_update_cksum32(uint16_t cksum, uint32_t old32, uint32_t new32)
+{
+  return orc_update_cksum16(orc_update_cksum16(cksum, (uint16_t)(old32 >> 16),
+                                               (uint16_t)(new32 >> 16)),
+                            (uint16_t)old32, (uint16_t)new32);
+}
+
+static uint32_t be32_at(const uint8_t *p)
+{
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+static void put_be32(uint8_t *p, uint32_t v)
+{
+  p[0] = (uint8_t)(v >> 24);
+  p[1] = (uint8_t)(v >> 16);
+  p[2] = (uint8_t)(v >> 8);
+  p[3] = (uint8_t)v;
+}
+
+/* L4 checksum follow-up of an address change: TCP always, UDP only when the
+ * transmitted checksum is not 0 (ip_set_src_cksum_update :245-260) */
+static void l4_addr_update(uint8_t *l4, uint8_t proto, uint32_t old32, uint32_t new32)
+{
+  if (proto == 6) {
+    put_be16(l4 + 16, orc_update_cksum32(be16_at(l4 + 16), old32, new32));
+  } else if (proto == 17) {
+    const uint16_t c = be16_at(l4 + 6);
+    if (c != 0)
+      put_be16(l4 + 6, orc_update_cksum32(c, old32, new32));
+  }
+}
+
+/* port write with checksum update: tcp_set_*_port_cksum_update (:263-281)
+ * and udp_set_*_port_cksum_update (:323-347; a 0 checksum stays 0) */
+static void l4_port_update(uint8_t *l4, uint8_t proto, int at, uint16_t port)
+{
+  const uint16_t old = be16_at(l4 + at);
+  if (proto == 6) {
+    put_be16(l4 + 16, orc_update_cksum16(be16_at(l4 + 16), old, port));
+  } else {
+    const uint16_t c = be16_at(l4 + 6);
+    if (c != 0)
+      put_be16(l4 + 6, orc_update_cksum16(c, old, port));
+  }
+  put_be16(l4 + at, port);
+}
+
+void orc_rewrite_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                       uint32_t fixed_len, size_t n, const struct pptk_rewrite *rw,
+                       uint64_t rw_count, uint8_t *status)
+{
+  struct orc_opts o;
+  size_t i;
+  memset(&o, 0, sizeof(o));
+  for (i = 0; i < n; i++) {
+    uint8_t *f = buf + (off ? off[i] : i * stride);
+    const uint32_t flen = len ? len[i] : fixed_len;
+    const struct pptk_rewrite *w = &rw[rw_count == 1 ? 0 : i];
+    struct pptk_rx_rec r;
+    uint8_t *ip, *l4, st = 0;
+    int l4ok;
+    orc_rx_one(f, flen, &o, &r);
+    if ((r.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED | PPTK_RX_F_IPV6)) != PPTK_RX_F_PARSED)
+      goto done;
+    ip = f + r.l3_off;
+    l4 = f + r.l4_off;
+    l4ok = (r.flags & PPTK_RX_F_L4) != 0;
+    if ((w->ops & PPTK_RW_DECR_TTL) && ip[8] == 0) {
+      st = PPTK_RW_ST_TTL_ZERO;   /* the reference abort()s (:382-385) */
+      goto done;
+    }
+    st = PPTK_RW_ST_IP | (l4ok ? PPTK_RW_ST_L4 : 0);
+    if (w->ops & PPTK_RW_DECR_TTL) {   /* ip_decr_ttl_cksum_update :374-393 */
+      const uint16_t old = (uint16_t)((ip[8] << 8) | ip[9]);
+      const uint16_t nw = (uint16_t)(((ip[8] - 1) << 8) | ip[9]);
+      put_be16(ip + 10, orc_update_cksum16(be16_at(ip + 10), old, nw));
+      ip[8] = (uint8_t)(ip[8] - 1);
+      if (ip[8] == 0)
+        st |= PPTK_RW_ST_EXPIRED;
+    }
+    if (w->ops & PPTK_RW_SRC) {        /* ip_set_src_cksum_update :238-261 */
+      const uint32_t old = be32_at(ip + 12);
+      put_be16(ip + 10, orc_update_cksum32(be16_at(ip + 10), old, w->src));
+      if (l4ok)
+        l4_addr_update(l4, r.proto, old, w->src);
+      put_be32(ip + 12, w->src);
+    }
+    if (w->ops & PPTK_RW_DST) {        /* ip_set_dst_cksum_update :349-372 */
+      const uint32_t old = be32_at(ip + 16);
+      put_be16(ip + 10, orc_update_cksum32(be16_at(ip + 10), old, w->dst));
+      if (l4ok)
+        l4_addr_update(l4, r.proto, old, w->dst);
+      put_be32(ip + 16, w->dst);
+    }
+    if (l4ok && (w->ops & PPTK_RW_SPORT))
+      l4_port_update(l4, r.proto, 0, w->sport);
+    if (l4ok && (w->ops & PPTK_RW_DPORT))
+      l4_port_update(l4, r.proto, 2, w->dport);
+done:
+    if (status)
+      status[i] = st;
+  }
+}

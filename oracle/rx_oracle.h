@@ -48,5 +48,10 @@ void orc_tx_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64
                   uint32_t fixed_len, size_t n);
 void orc_tokens_refill(uint32_t *tokens, uint32_t start, uint32_t end,
                        uint32_t add, uint32_t initial);
+uint16_t orc_update_cksum16(uint16_t cksum, uint16_t old16, uint16_t new16);
+uint16_t orc_update_cksum32(uint16_t cksum, uint32_t old32, uint32_t new32);
+void orc_rewrite_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                       uint32_t fixed_len, size_t n, const struct pptk_rewrite *rw,
+                       uint64_t rw_count, uint8_t *status);
 
 #endif

@@ -303,6 +303,32 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
   return hip_err(launch_rx(variant, a, grid_for(c, variant, n), (hipStream_t)stream));
 }
 
+int pptk_tx_rewrite_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,
+                           const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
+                           uint64_t n, const struct pptk_rewrite *d_rw, uint64_t rw_count,
+                           uint8_t *d_status, void *stream) {
+  if (!c || n > 0xffffffffull) return -EINVAL;
+  if (n == 0) return 0;
+  if (!d_frames || !d_rw || (rw_count != 1 && rw_count != n) ||
+      (!d_off && stride == 0 && n > 1) || (!d_len && fixed_len > 65535))
+    return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  RxKArgs a = c->tmpl;
+  a.frames = d_frames;
+  a.frames_w = d_frames;
+  a.off = d_off;
+  a.len = d_len;
+  a.stride = stride;
+  a.fixed_len = fixed_len;
+  a.n = n;
+  a.rw = d_rw;
+  a.rw_one = rw_count == 1 ? 1u : 0u;
+  a.rw_status = d_status;
+  const uint64_t blocks = (n + 255) / 256;
+  const int grid = (int)std::min<uint64_t>(blocks, (uint64_t)c->ncu * 8);
+  return hip_err(launch_rewrite(a, grid, (hipStream_t)stream));
+}
+
 int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
                                uint32_t *d_perm, void *d_scratch, void *stream) {
   int rc = check_batch(c, b);

@@ -37,6 +37,10 @@ struct RxKArgs {
   uint64_t stride_g;
   // nullable (GATHER + perm): process perm[*range_lo .. *range_hi) only
   const uint32_t *range_lo, *range_hi;
+  // header rewrite (pptk_tx_rewrite_device): rw[rw_one ? 0 : i], status
+  const pptk_rewrite *rw;
+  uint32_t rw_one;
+  uint8_t *rw_status;
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S
@@ -61,6 +65,7 @@ constexpr int kGroupVariant[kGroups] = {RX_T4S2, RX_T8S2, RX_T16S2, RX_T16S4, RX
                                         RX_T64S2};
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
+hipError_t launch_rewrite(const RxKArgs &a, int grid, hipStream_t s);
 int rx_variant_blocks_per_cu(int variant);
 
 // Stable counting sort of 0..n-1 into kGroups length groups.  After it,

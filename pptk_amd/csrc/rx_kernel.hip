@@ -992,6 +992,104 @@ __global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
   }
 }
 
+// Header rewrite with incremental checksum updates (pptk_tx_rewrite_device,
+// reference iphdr/ipcksum.h:213-393).  Only the first 128 bytes of a frame
+// matter (Ethernet, the IPv4 header, the first 18 bytes of TCP/UDP), so one
+// lane per frame loads its frame's first eight aligned chunks (clamped to
+// the frame) into its LDS slot, parses it exactly as the receive transform
+// does, folds the requested changes into the transmitted checksums with
+// RFC 1624 updates, and stores the changed fields.
+__device__ __forceinline__ uint32_t upd16(uint32_t ck, uint32_t o, uint32_t nw) {
+  // ip_update_cksum16 (iphdr/ipcksum.h:213-226)
+  uint32_t s = (~ck & 0xffffu) + (~o & 0xffffu) + nw;
+  s = fold16(s);
+  return ~s & 0xffffu;
+}
+__device__ __forceinline__ uint32_t upd32(uint32_t ck, uint32_t o, uint32_t nw) {
+  // ip_update_cksum32 (:228-236): high halves, then low halves
+  return upd16(upd16(ck, o >> 16, nw >> 16), o & 0xffffu, nw & 0xffffu);
+}
+
+__device__ __forceinline__ void put_be(GLB_AS uint8_t *p, uint32_t v, int nbytes) {
+  for (int k = 0; k < nbytes; ++k)
+    p[k] = (uint8_t)(v >> (8 * (nbytes - 1 - k)));
+}
+
+constexpr int RW_SLOT = 128;
+
+__global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[256 * RW_SLOT];
+  LDS_AS uint8_t *slot = (LDS_AS uint8_t *)lds + threadIdx.x * RW_SLOT;
+  const uint64_t step = (uint64_t)gridDim.x * 256u;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += step) {
+    const uint64_t base = a.off ? a.off[i] : i * a.stride;
+    const uint32_t len = a.len ? a.len[i] : a.fixed_len;
+    const int m = (int)(base & 15);
+    const int nch = max((m + (int)len + 15) >> 4, 1);
+    const u32x4 *c0 = (const u32x4 *)(a.frames + (base - (uint64_t)m));
+#pragma unroll
+    for (int c = 0; c < RW_SLOT / 16; ++c)
+      ((LDS_AS u32x4 *)slot)[c] = c0[min(c, nch - 1)];
+    const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + base, m, RW_SLOT - m};
+    const Parse p = parse_frame(v, len);
+    uint32_t st = 0;
+    if ((p.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED | PPTK_RX_F_IPV6)) == PPTK_RX_F_PARSED) {
+      const pptk_rewrite w = a.rw[a.rw_one ? 0 : i];
+      const int l3 = (int)p.l3, l4 = (int)p.rs;
+      const bool l4ok = p.flags & PPTK_RX_F_L4;
+      const uint32_t proto = p.proto;
+      uint32_t ttl = v.u8(l3 + 8);
+      if ((w.ops & PPTK_RW_DECR_TTL) && ttl == 0) {
+        st = PPTK_RW_ST_TTL_ZERO;   // the reference abort()s (:382-385)
+      } else {
+        st = PPTK_RW_ST_IP | (l4ok ? PPTK_RW_ST_L4 : 0u);
+        GLB_AS uint8_t *f = (GLB_AS uint8_t *)a.frames_w + base;
+        const int cko = proto == 6 ? 16 : 6;          // TCP / UDP checksum field
+        uint32_t ipc = v.be16(l3 + 10);
+        uint32_t l4c = l4ok ? v.be16(l4 + cko) : 0u;
+        bool l4c_w = false;
+        if (w.ops & PPTK_RW_DECR_TTL) {   // ip_decr_ttl_cksum_update (:374-393)
+          ipc = upd16(ipc, (ttl << 8) | proto, ((ttl - 1) << 8) | proto);
+          ttl -= 1;
+          f[l3 + 8] = (uint8_t)ttl;
+          if (ttl == 0) st |= PPTK_RW_ST_EXPIRED;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {    // ip_set_src/dst_cksum_update (:238-261, :349-372)
+          const uint32_t op = k == 0 ? PPTK_RW_SRC : PPTK_RW_DST;
+          if (!(w.ops & op)) continue;
+          const uint32_t nw = k == 0 ? w.src : w.dst;
+          const uint32_t old = __builtin_bswap32(v.le32(l3 + 12 + 4 * k));
+          ipc = upd32(ipc, old, nw);
+          if (l4ok && (proto == 6 || l4c != 0)) {   // UDP: a 0 checksum stays 0
+            l4c = upd32(l4c, old, nw);
+            l4c_w = true;
+          }
+          put_be(f + l3 + 12 + 4 * k, nw, 4);
+        }
+        if (l4ok) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {  // tcp/udp_set_src/dst_port_cksum_update (:263-347)
+            const uint32_t op = k == 0 ? PPTK_RW_SPORT : PPTK_RW_DPORT;
+            if (!(w.ops & op)) continue;
+            const uint32_t nw = k == 0 ? w.sport : w.dport;
+            if (proto == 6 || l4c != 0) {
+              l4c = upd16(l4c, v.be16(l4 + 2 * k), nw);
+              l4c_w = true;
+            }
+            put_be(f + l4 + 2 * k, nw, 2);
+          }
+        }
+        if (w.ops & (PPTK_RW_DECR_TTL | PPTK_RW_SRC | PPTK_RW_DST))
+          put_be(f + l3 + 10, ipc, 2);
+        if (l4c_w)
+          put_be(f + l4 + cko, l4c, 2);
+      }
+    }
+    if (a.rw_status) a.rw_status[i] = (uint8_t)st;
+  }
+}
+
 template <int T, int S, int D, int AL>
 hipError_t launch_variant(const RxKArgs &a0, int grid, hipStream_t s) {
   const dim3 gd(grid), bd(WAVE * WPB);
@@ -1058,6 +1156,11 @@ hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s) {
 #undef X
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_rewrite(const RxKArgs &a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(rx_rewrite_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 int rx_variant_blocks_per_cu(int variant) {

@@ -23,6 +23,14 @@ REC_DTYPE = np.dtype([
 ])
 assert REC_DTYPE.itemsize == 64
 
+# struct pptk_rewrite (pptk_tx_rewrite_device): ops, new src/dst (host
+# order), new ports (host order)
+REWRITE_DTYPE = np.dtype([("ops", "<u4"), ("src", "<u4"), ("dst", "<u4"),
+                          ("sport", "<u2"), ("dport", "<u2")])
+assert REWRITE_DTYPE.itemsize == 16
+RW_DECR_TTL, RW_SRC, RW_DST, RW_SPORT, RW_DPORT = 0x1, 0x2, 0x4, 0x8, 0x10
+RW_ST_IP, RW_ST_L4, RW_ST_TTL_ZERO, RW_ST_EXPIRED = 0x1, 0x2, 0x4, 0x8
+
 REC32_DTYPE = np.dtype([
     ("flow_hash", "<u8"),
     ("src4", "u1", 4),

@@ -45,7 +45,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
-           "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device",
+           "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_rewrite_device",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
@@ -85,6 +85,10 @@ def lib(path=None):
             L.pptk_tx_cksum_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
                                                ctypes.c_uint64, ctypes.c_uint32, vp]
             L.pptk_tx_cksum_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_tx_rewrite_device"):       # absent from older A/B builds
+            L.pptk_tx_rewrite_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
+                                                 ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp]
+            L.pptk_tx_rewrite_device.restype = ctypes.c_int
         if hasattr(L, "pptk_rx_permit_device"):        # absent from older A/B builds
             L.pptk_rx_permit_scratch_bytes.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
             L.pptk_rx_permit_scratch_bytes.restype = ctypes.c_size_t
@@ -248,6 +252,21 @@ class RxContext:
                                           fixed_len, n, max_len, ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise OSError(-rc, f"pptk_tx_cksum_device failed ({rc})")
+
+    def tx_rewrite_device(self, frames, n, rw, off=None, lens=None, stride=0, fixed_len=0,
+                          status=None, stream=None):
+        """Header rewrite with incremental checksum updates, in place and
+        asynchronously.  rw: torch uint8 CUDA tensor of 1 or n struct
+        pptk_rewrite entries (16 bytes each, records.REWRITE_DTYPE);
+        status: optional torch uint8 CUDA tensor of n PPTK_RW_ST_* bytes."""
+        import torch
+        count = rw.numel() // 16
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = self._L.pptk_tx_rewrite_device(self._ctx, _dp(frames), _dp(off), _dp(lens), stride,
+                                            fixed_len, n, _dp(rw), count, _dp(status),
+                                            ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_tx_rewrite_device failed ({rc})")
 
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""

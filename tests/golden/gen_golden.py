@@ -13,6 +13,13 @@ tx.npz holds tx-side cases: frames with scrambled checksum fields and the
 same frames after the reference's ip_set_hdr_cksum_calc /
 tcp/udp(6)_set_cksum_calc (oracle/refgen.c ref_tx_batch).
 
+rewrite.npz holds header-rewrite cases (pptk_tx_rewrite_device): per
+golden set, frames with some IPv4 TTLs set to 0 or 1 and some UDP checksums
+to 0 (inputs), random per-frame rewrite entries (ops, new addresses and
+ports), and the frames after the reference's ip_decr_ttl_cksum_update /
+ip_set_src/dst_cksum_update / tcp/udp_set_src/dst_port_cksum_update
+(oracle/refgen.c ref_rewrite_batch) with the per-frame status.
+
 permit.npz additionally holds rate-limiter cases: token arrays before/after
 and per-frame verdicts of the reference's ip_permitted / ipv6_permitted
 called once per subject frame in frame order (oracle/refgen.c
@@ -122,11 +129,69 @@ def gen_tx(ref):
     return out
 
 
+def rewrite_inputs(z, rng):
+    """Copy of z's buffer with the TTL of ~1/4 of the parsed IPv4 frames set
+    to 0 or 1 and the checksum of ~1/4 of the UDP frames set to 0."""
+    from pptk_amd.records import F_IPV6, F_L4, F_MALFORMED, F_PARSED, as_records
+    buf = z["buf"].copy()
+    rec = as_records(z["recs"])
+    for i, o in enumerate(z["off"]):
+        r, f = rec[i], int(o)
+        fl = int(r["flags"])
+        if not fl & F_PARSED or fl & (F_MALFORMED | F_IPV6):
+            continue
+        if rng.random() < 0.25:
+            buf[f + int(r["l3_off"]) + 8] = rng.integers(0, 2)
+        if fl & F_L4 and int(r["proto"]) == 17 and rng.random() < 0.25:
+            p = f + int(r["l4_off"]) + 6
+            buf[p:p + 2] = 0
+    return buf
+
+
+def random_rewrites(n, rng):
+    from pptk_amd.records import REWRITE_DTYPE
+    rw = np.zeros(n, REWRITE_DTYPE)
+    rw["ops"] = rng.integers(0, 32, n)
+    rw["src"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    rw["dst"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    rw["sport"] = rng.integers(0, 65536, n)
+    rw["dport"] = rng.integers(0, 65536, n)
+    return rw
+
+
+def gen_rewrite(ref):
+    """Header-rewrite fixtures over the golden sets (positions into the set's
+    buffer with input and expected bytes, the rewrite entries, the status);
+    for c64 also one shared rewrite entry for every frame ("c64_one")."""
+    rng = np.random.default_rng(0x5E7)
+    out = {}
+    cases = [("edge", "edge", None), ("fuzz", "fuzz", None), ("cmix", "cmix", None),
+             ("c64", "c64", None), ("c64_one", "c64", 1)]
+    for tag, name, count in cases:
+        z = dict(np.load(os.path.join(HERE, f"{name}.npz")))
+        buf_in = rewrite_inputs(z, rng)
+        rw = random_rewrites(count or len(z["off"]), rng)
+        if count == 1:
+            rw["ops"] = 0x1F
+        buf_out, status = ref.rewrite_batch(buf_in, rw, z["off"], z["len"])
+        pos = np.nonzero((buf_in != z["buf"]) | (buf_out != buf_in))[0]
+        out[f"{tag}_pos"] = pos.astype(np.uint64)
+        out[f"{tag}_in"] = buf_in[pos]
+        out[f"{tag}_out"] = buf_out[pos]
+        out[f"{tag}_rw"] = rw.view(np.uint8).reshape(-1, 16)
+        out[f"{tag}_status"] = status
+    return out
+
+
 def main():
     build()
     ref = Reference()
     opts = make_opts(KEY, BITS4, BITS6, HASH_SIZE)
-    want = set(sys.argv[1:]) or set(SETS) | {"permit", "tx"}
+    want = set(sys.argv[1:]) or set(SETS) | {"permit", "tx", "rewrite"}
+    if "rewrite" in want:
+        path = os.path.join(HERE, "rewrite.npz")
+        np.savez_compressed(path, **gen_rewrite(ref))
+        print(f"rewrite -> {os.path.getsize(path)} B")
     if "tx" in want:
         path = os.path.join(HERE, "tx.npz")
         np.savez_compressed(path, **gen_tx(ref))
