@@ -171,4 +171,20 @@ static inline uint16_t udp_dst_port(const void *l4) { return hdr_get16n(PPTK_AT(
 static inline uint16_t udp_total_len(const void *l4) { return hdr_get16n(PPTK_AT(l4, 4)); }
 static inline uint16_t udp_cksum(const void *l4) { return hdr_get16n(PPTK_AT(l4, 6)); }
 
+/* ---- setters used by the tx side and the incremental updates:
+ * iphdr.h:1152-1156 (ttl), 1253-1257 (hdr cksum), 1271-1281 (src/dst),
+ * 1315-1325, 1387-1391 (tcp), 1405-1415, 1435-1439 (udp); host-order values
+ * stored big-endian. */
+#define PPTK_W(p, k) ((unsigned char *)(p) + (k))
+static inline void ip_set_ttl(void *pkt, uint8_t ttl) { *PPTK_W(pkt, 8) = ttl; }
+static inline void ip_set_hdr_cksum(void *pkt, uint16_t c) { hdr_set16n(PPTK_W(pkt, 10), c); }
+static inline void ip_set_src(void *pkt, uint32_t src) { hdr_set32n(PPTK_W(pkt, 12), src); }
+static inline void ip_set_dst(void *pkt, uint32_t dst) { hdr_set32n(PPTK_W(pkt, 16), dst); }
+static inline void tcp_set_src_port(void *l4, uint16_t p) { hdr_set16n(PPTK_W(l4, 0), p); }
+static inline void tcp_set_dst_port(void *l4, uint16_t p) { hdr_set16n(PPTK_W(l4, 2), p); }
+static inline void tcp_set_cksum(void *l4, uint16_t c) { hdr_set16n(PPTK_W(l4, 16), c); }
+static inline void udp_set_src_port(void *l4, uint16_t p) { hdr_set16n(PPTK_W(l4, 0), p); }
+static inline void udp_set_dst_port(void *l4, uint16_t p) { hdr_set16n(PPTK_W(l4, 2), p); }
+static inline void udp_set_cksum(void *l4, uint16_t c) { hdr_set16n(PPTK_W(l4, 6), c); }
+
 #endif

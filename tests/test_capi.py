@@ -174,3 +174,89 @@ def test_example_rx_loop_runs(tmp_path):
                          timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "20000 frames" in out.stdout and "19995 verified, 5 failed" in out.stdout
+
+
+@pytest.fixture(scope="module")
+def kept_inline(tmp_path_factory):
+    """tests/c/kept_inline.c: the kept inline setters / incremental updates
+    of include/ipcksum.h wrapped as exported functions (built with gcc)."""
+    import ctypes
+    so = str(tmp_path_factory.mktemp("kept") / "libkept.so")
+    libdir = os.path.join(ROOT, "pptk_amd")
+    subprocess.check_call(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Werror", "-fPIC",
+                           "-shared", "-I", INCLUDE, os.path.join(ROOT, "tests", "c", "kept_inline.c"),
+                           "-L", libdir, "-lpptkrx", f"-Wl,-rpath,{libdir}", "-o", so])
+    L = ctypes.CDLL(so)
+    u16, u32, vp = ctypes.c_uint16, ctypes.c_uint32, ctypes.c_void_p
+    L.kept_update16.argtypes, L.kept_update16.restype = [u16, u16, u16], u16
+    L.kept_update32.argtypes, L.kept_update32.restype = [u16, u32, u32], u16
+    L.kept_rewrite.argtypes = [vp] + [ctypes.c_int] * 4 + [u32, u32, u32, u16, u16]
+    L.kept_set_cksums.argtypes = [vp] + [ctypes.c_int] * 5 + [u16]
+    L.kept_set_cksums.restype = None
+    return L
+
+
+def test_kept_update_helpers(kept_inline, oracle_lib):
+    rng = np.random.default_rng(3)
+    for _ in range(20000):
+        c, a, b = (int(x) for x in rng.integers(0, 65536, 3))
+        assert kept_inline.kept_update16(c, a, b) == oracle_lib.update_cksum16(c, a, b)
+        a32, b32 = (int(x) for x in rng.integers(0, 2 ** 32, 2))
+        assert kept_inline.kept_update32(c, a32, b32) == oracle_lib.update_cksum32(c, a32, b32)
+
+
+def test_kept_update_helpers_vs_reference(kept_inline, reference_lib):
+    rng = np.random.default_rng(4)
+    for _ in range(20000):
+        c, a, b = (int(x) for x in rng.integers(0, 65536, 3))
+        assert kept_inline.kept_update16(c, a, b) == reference_lib.update_cksum16(c, a, b)
+
+
+@pytest.mark.parametrize("tag,name", [("edge", "edge"), ("fuzz", "fuzz"), ("cmix", "cmix")])
+def test_kept_rewrite_functions_match_fixture(kept_inline, tag, name):
+    """The kept per-frame *_cksum_update functions, applied frame by frame
+    as pptk_tx_rewrite_device composes them, give the reference's bytes."""
+    import ctypes
+    from pptk_amd.records import (F_L4, F_PARSED, RW_ST_TTL_ZERO, as_records)
+    from test_oracle import rewrite_case
+    z, buf_in, buf_out, rw, status = rewrite_case(tag, name)
+    recs = as_records(z["recs"])
+    buf = buf_in.copy()
+    n_done = 0
+    for i, o in enumerate(z["off"]):
+        if status[i] == 0 or status[i] & RW_ST_TTL_ZERO:
+            continue
+        r, w = recs[i], rw[i]
+        L = int(z["len"][i])
+        fr = (ctypes.c_uint8 * L).from_buffer(buf, int(o))
+        kept_inline.kept_rewrite(fr, int(r["l3_off"]), int(r["l4_off"]), int(r["proto"]),
+                                 int(bool(r["flags"] & F_L4)), int(w["ops"]), int(w["src"]),
+                                 int(w["dst"]), int(w["sport"]), int(w["dport"]))
+        assert r["flags"] & F_PARSED
+        n_done += 1
+    assert n_done > 50
+    assert np.array_equal(buf, buf_out), int((buf != buf_out).sum())
+
+
+@pytest.mark.parametrize("name", ["edge", "fuzz", "cmix"])
+def test_kept_tx_setters_match_fixture(kept_inline, name):
+    import ctypes
+    from pptk_amd.records import F_IPV6, F_L4, F_MALFORMED, F_PARSED, as_records
+    z = load_golden(name)
+    t = load_golden("tx")
+    pos = t[f"{name}_pos"].astype(np.int64)
+    buf = z["buf"].copy()
+    buf[pos] = t[f"{name}_in"]
+    want = buf.copy()
+    want[pos] = t[f"{name}_out"]
+    recs = as_records(z["recs"])
+    for i, o in enumerate(z["off"]):
+        r = recs[i]
+        fl = int(r["flags"])
+        if not fl & F_PARSED or fl & F_MALFORMED:
+            continue
+        L = int(z["len"][i])
+        fr = (ctypes.c_uint8 * L).from_buffer(buf, int(o))
+        kept_inline.kept_set_cksums(fr, int(r["l3_off"]), int(r["l4_off"]), int(bool(fl & F_IPV6)),
+                                    int(r["proto"]), int(bool(fl & F_L4)), int(r["l4_len"]))
+    assert np.array_equal(buf, want), int((buf != want).sum())
