@@ -1010,12 +1010,58 @@ __device__ __forceinline__ uint32_t upd32(uint32_t ck, uint32_t o, uint32_t nw) 
   return upd16(upd16(ck, o >> 16, nw >> 16), o & 0xffffu, nw & 0xffffu);
 }
 
-__device__ __forceinline__ void put_be(GLB_AS uint8_t *p, uint32_t v, int nbytes) {
-  for (int k = 0; k < nbytes; ++k)
-    p[k] = (uint8_t)(v >> (8 * (nbytes - 1 - k)));
-}
+// Field writes of one frame: patched into the lane's LDS image (and marked
+// in `touched`) where the image holds the byte, stored directly otherwise;
+// flush() then writes back every image chunk that lies inside the frame
+// whole -- whole 16-byte chunks instead of a dozen scattered byte stores per
+// frame: C64 0.77 -> 0.58 ms, C1500 1.47 -> 1.24 ms, CMIX 1.28 -> 1.15 ms
+// (in-process A/B, tools/ab_rewrite.py) -- and only the touched bytes of
+// chunks that reach outside it (those bytes may be a neighbour's).
+template <int SLOT>
+struct FieldWriter {
+  LDS_AS uint8_t *img;
+  GLB_AS uint8_t *f;     // frame start
+  int m;
+  uint64_t touched = 0;  // image byte positions patched
 
-constexpr int RW_SLOT = 128;
+  __device__ __forceinline__ void put(int k, uint32_t v, int nbytes) {
+    for (int b = 0; b < nbytes; ++b) {
+      const uint8_t x = (uint8_t)(v >> (8 * (nbytes - 1 - b)));
+      const int pos = m + k + b;
+      if (pos < SLOT) {
+        img[pos] = x;
+        touched |= 1ull << pos;
+      } else {
+        f[k + b] = x;
+      }
+    }
+  }
+  __device__ __forceinline__ void flush(uint32_t len) {
+    if (!touched) return;
+    GLB_AS uint8_t *row = f - m;
+#pragma unroll
+    for (int c = 0; c < SLOT / 16; ++c) {
+      const int fo = 16 * c - m;                    // frame offset of the chunk
+      if (fo >= 0 && fo + 16 <= (int)len) {
+        *(GLB_AS u32x4 *)(row + 16 * c) = ((const LDS_AS u32x4 *)img)[c];
+      } else {
+        uint32_t t = (uint32_t)(touched >> (16 * c)) & 0xffffu;
+        while (t) {
+          const int b = __builtin_ctz(t);
+          row[16 * c + b] = img[16 * c + b];
+          t &= t - 1;
+        }
+      }
+    }
+  }
+};
+
+// The lane's image holds the frame's first four aligned chunks, 64 - m
+// frame bytes: every field of an IPv4 frame with a 20-byte header lies in
+// the first 52 bytes (56 behind a VLAN tag), so the image covers it when the
+// frame starts at most 12 (8) bytes into its chunk; fields past the image
+// come from global memory through the FrameView rare path.
+constexpr int RW_SLOT = 64;
 
 __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[256 * RW_SLOT];
@@ -1043,7 +1089,7 @@ __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
         st = PPTK_RW_ST_TTL_ZERO;   // the reference abort()s (:382-385)
       } else {
         st = PPTK_RW_ST_IP | (l4ok ? PPTK_RW_ST_L4 : 0u);
-        GLB_AS uint8_t *f = (GLB_AS uint8_t *)a.frames_w + base;
+        FieldWriter<RW_SLOT> fw{slot, (GLB_AS uint8_t *)a.frames_w + base, m};
         const int cko = proto == 6 ? 16 : 6;          // TCP / UDP checksum field
         uint32_t ipc = v.be16(l3 + 10);
         uint32_t l4c = l4ok ? v.be16(l4 + cko) : 0u;
@@ -1051,7 +1097,7 @@ __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
         if (w.ops & PPTK_RW_DECR_TTL) {   // ip_decr_ttl_cksum_update (:374-393)
           ipc = upd16(ipc, (ttl << 8) | proto, ((ttl - 1) << 8) | proto);
           ttl -= 1;
-          f[l3 + 8] = (uint8_t)ttl;
+          fw.put(l3 + 8, ttl, 1);
           if (ttl == 0) st |= PPTK_RW_ST_EXPIRED;
         }
 #pragma unroll
@@ -1065,7 +1111,7 @@ __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
             l4c = upd32(l4c, old, nw);
             l4c_w = true;
           }
-          put_be(f + l3 + 12 + 4 * k, nw, 4);
+          fw.put(l3 + 12 + 4 * k, nw, 4);
         }
         if (l4ok) {
 #pragma unroll
@@ -1077,13 +1123,14 @@ __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
               l4c = upd16(l4c, v.be16(l4 + 2 * k), nw);
               l4c_w = true;
             }
-            put_be(f + l4 + 2 * k, nw, 2);
+            fw.put(l4 + 2 * k, nw, 2);
           }
         }
         if (w.ops & (PPTK_RW_DECR_TTL | PPTK_RW_SRC | PPTK_RW_DST))
-          put_be(f + l3 + 10, ipc, 2);
+          fw.put(l3 + 10, ipc, 2);
         if (l4c_w)
-          put_be(f + l4 + cko, l4c, 2);
+          fw.put(l4 + cko, l4c, 2);
+        fw.flush(len);
       }
     }
     if (a.rw_status) a.rw_status[i] = (uint8_t)st;
