@@ -496,16 +496,24 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
     int txp[2] = {-1, -1};          // tx: frame offsets of the fields to set
     uint32_t txv[2] = {0, 0};
     uint32_t ipc = 0;
+    // [ts, rs): the header bytes between the team start (18 <= ts <= 33) and
+    // the L4 start (>= 34), absolute pairing; the L4 correction subtracts
+    // them, and for IPv4 they are most of the header sum
+    const int ts = team_start_of(m);
+    const uint32_t s_tr = sum_abs(v, ts, (int)rs);
     if (v6) {
       s0 = v.le32(l3 + 8);  s1 = v.le32(l3 + 12); s2 = v.le32(l3 + 16); s3 = v.le32(l3 + 20);
       d0 = v.le32(l3 + 24); d1 = v.le32(l3 + 28); d2 = v.le32(l3 + 32); d3 = v.le32(l3 + 36);
     } else {
       s0 = v.le32(l3 + 12);
       d0 = v.le32(l3 + 16);
-      // ip_hdr_cksum_calc over ihl = rs - l3 bytes (frame-relative pairing)
-      uint32_t hs = 0;
-      for (uint32_t k = l3; k < rs; k += 4)
-        hs = dot16(v.le32((int)k), hs);
+      // ip_hdr_cksum_calc over ihl = rs - l3 bytes: [l3, ts) + [ts, rs), a
+      // sum of sums (no subtraction, so exactly 0 only for all-zero bytes);
+      // absolute pairing, byte-swapped to the header's own pairing when the
+      // header starts at an odd address (RFC 1071 2.(B))
+      uint32_t hs = fold16(sum_abs(v, (int)l3, ts) + s_tr);
+      if ((m + (int)l3) & 1)
+        hs = bswap16(hs);
       ipc = finish16(hs);
       if (ipc == 0)
         flags |= PPTK_RX_F_IP_OK;
@@ -529,10 +537,8 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
       // region [rs, re) = [ts, L16) - [ts, rs) - [re, len) - [len, L16), mod
       // 0xffff, where the team sum covered [ts, L16): L16 = the end of the
       // chunk holding the last byte
-      const int ts = team_start_of(m);
       uint32_t rsum = fold16(my_sum) + (0xffffu - fold16(tail_past_end(tailc, m, (int)len, ts)));
-      if ((int)rs > ts)
-        rsum += 0xffffu - fold16(sum_abs(v, ts, (int)rs));
+      rsum += 0xffffu - fold16(s_tr);
       if (re < len)
         rsum += 0xffffu - fold16(sum_abs(v, (int)re, (int)len));
       rsum = fold16(rsum);
