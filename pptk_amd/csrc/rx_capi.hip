@@ -11,6 +11,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -35,6 +39,74 @@ struct RxSlot {
   bool busy = false;
 };
 
+// The context's host worker threads (opts.gather_threads - 1 of them, started
+// on the first host batch and kept): parallel_for(n, f) runs f(0..n-1)
+// across them and the calling thread and returns when all are done.  The
+// staged path's frame gather and record copy-out use it; starting threads
+// per chunk instead cost more than the copies for small frames.
+class WorkerPool {
+ public:
+  explicit WorkerPool(size_t nworkers) {
+    for (size_t t = 0; t < nworkers; ++t) th_.emplace_back([this] { loop(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread &t : th_) t.join();
+  }
+  size_t size() const { return th_.size() + 1; }
+  void parallel_for(size_t n, const std::function<void(size_t)> &f) {
+    if (n == 0) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &f;
+      n_ = n;
+      next_.store(0);
+      left_ = n;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [this] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const size_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      (*job_)(i);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--left_ == 0) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)> *job_ = nullptr;
+  size_t n_ = 0, left_ = 0;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 // A host rx ring registered for zero-copy reads (hipHostRegister, mapped).
 struct RxRing {
   uint8_t *host;
@@ -54,6 +126,7 @@ struct pptk_rx_ctx {
   int last_variant = -1;
   RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch)
   std::vector<RxRing> rings;
+  WorkerPool *pool = nullptr;   // started by the first host batch
 };
 
 static int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -150,6 +223,7 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   free_staging(c);
+  delete c->pool;
   (void)hipFree(c->d_zero);
   for (const RxRing &r : c->rings) (void)hipHostUnregister(r.host);
   delete c;
@@ -439,12 +513,36 @@ static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {
   return 0;
 }
 
+// The context's worker pool (nullptr with gather_threads <= 1).
+static WorkerPool *pool_of(pptk_rx_ctx *c) {
+  const size_t nth = std::max<size_t>(1, std::min<size_t>(c->opts.gather_threads, 64));
+  if (nth > 1 && !c->pool) c->pool = new (std::nothrow) WorkerPool(nth - 1);
+  return c->pool;
+}
+
+// Copy n bytes, split over the pool when it pays (a few MB and up).
+static void copy_out(WorkerPool *pool, void *dst, const void *src, size_t n) {
+  constexpr size_t kPiece = 1u << 20;
+#ifdef PPTK_RX_SERIAL_COPYOUT
+  pool = nullptr;
+#endif
+  if (!pool || n < 2 * kPiece) {
+    memcpy(dst, src, n);
+    return;
+  }
+  const size_t parts = (n + kPiece - 1) / kPiece;
+  pool->parallel_for(parts, [&](size_t i) {
+    const size_t lo = i * kPiece, hi = std::min(n, lo + kPiece);
+    memcpy((uint8_t *)dst + lo, (const uint8_t *)src + lo, hi - lo);
+  });
+}
+
 // Wait for the slot's chunk and hand its records to the caller.
-static int retire(RxSlot &sl) {
+static int retire(RxSlot &sl, WorkerPool *pool) {
   if (!sl.busy) return 0;
   sl.busy = false;
   if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
-  memcpy(sl.out, sl.h_recs, sl.count * 64);
+  copy_out(pool, sl.out, sl.h_recs, sl.count * 64);
   return 0;
 }
 
@@ -504,6 +602,7 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   const RxRing *ring = ring_of(c, pkts, num);
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
   const size_t chunk_bytes = chunk * ((maxf + 15) & ~15u);
+  WorkerPool *pool = pool_of(c);
   int rc = 0;
   // Double-buffered: while chunk k runs on one slot's stream (H2D, kernel,
   // D2H), the host gathers chunk k+1 into the other slot.  In a registered
@@ -512,7 +611,7 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   size_t k = 0;
   for (size_t first = 0; first < (size_t)num && rc == 0; first += chunk, ++k) {
     RxSlot &sl = c->slot[k & 1];
-    if ((rc = retire(sl)) != 0) break;
+    if ((rc = retire(sl, pool)) != 0) break;
     const size_t cnt = std::min(chunk, (size_t)num - first);
     if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes)) != 0) break;
     // descriptors (and staging offsets) first, serially; then the frame
@@ -539,16 +638,12 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
         for (size_t i = lo; i < hi; ++i)
           if (sl.h_len[i]) memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
       };
-      const size_t nth = std::max<size_t>(1, std::min<size_t>(c->opts.gather_threads, 64));
-      if (nth == 1 || cnt < 1024) {
+      if (!pool || cnt < 1024) {
         gather(0, cnt);
       } else {
-        std::vector<std::thread> th;
-        th.reserve(nth - 1);
-        for (size_t t = 1; t < nth; ++t)
-          th.emplace_back(gather, cnt * t / nth, cnt * (t + 1) / nth);
-        gather(0, cnt / nth);
-        for (std::thread &x : th) x.join();
+        // pieces of ~256 frames, taken by the workers in turn
+        const size_t parts = std::min<size_t>((cnt + 255) / 256, 64 * pool->size());
+        pool->parallel_for(parts, [&](size_t t) { gather(cnt * t / parts, cnt * (t + 1) / parts); });
       }
     }
     hipStream_t s = sl.stream;
@@ -579,7 +674,7 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   }
   // drain (also on error: nothing may still read the caller's buffers)
   for (RxSlot &sl : c->slot) {
-    const int r2 = retire(sl);
+    const int r2 = retire(sl, pool);
     if (rc == 0) rc = r2;
   }
   return rc;

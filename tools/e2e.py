@@ -39,7 +39,11 @@ def main():
         pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
                            np.full(n, b["fixed_len"], np.uint16))
         res = {}
-        for mode in ("staged", "ring"):
+        for mode in os.environ.get("E2E_MODES", "staged,ring").split(","):
+            if os.environ.get("E2E_FRESH") and res:    # one context per mode
+                ctx.close()
+                ctx = RxContext(0, bytes(range(1, 17)), max_batch=chunk, max_frame=1518,
+                                gather_threads=gt)
             if mode == "ring":
                 ctx.register_ring(ring)
             got = ctx.batch_host(pkts)          # warm-up (allocations)
@@ -55,6 +59,7 @@ def main():
             if mode == "ring":
                 ctx.unregister_ring(ring)
         out[cfg] = res
+        ctx.close()
         del b, ref
         torch.cuda.empty_cache()
     print(json.dumps(out))
