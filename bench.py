@@ -37,6 +37,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def dist_on(ws):
+    """A process group exists: N > 1, or PPTK_BENCH_FORCE_DIST=1 (a one-rank
+    RCCL group, to exercise the all-gather path on a one-GPU box)."""
+    return ws > 1 or os.environ.get("PPTK_BENCH_FORCE_DIST") == "1"
+
+
 def dist_setup(ngpus):
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -44,9 +50,12 @@ def dist_setup(ngpus):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if ws > 1:
+    if dist_on(ws):
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(ws))
         dist.init_process_group("nccl", device_id=dev)
     return ws, rank, dev
 
@@ -55,13 +64,13 @@ def barrier(ws, dev):
     import torch
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
-    if ws > 1:
+    if dist_on(ws):
         import torch.distributed as dist
         dist.barrier()
 
 
 def max_over_ranks(x, ws, dev):
-    if ws == 1:
+    if not dist_on(ws):
         return x
     import torch
     import torch.distributed as dist
@@ -71,7 +80,7 @@ def max_over_ranks(x, ws, dev):
 
 
 def sum_over_ranks(x, ws, dev):
-    if ws == 1:
+    if not dist_on(ws):
         return x
     import torch
     import torch.distributed as dist
@@ -90,7 +99,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     b = batch if batch is not None else make_batch(cfg, n, dev, first=rank * n)
     torch.cuda.synchronize(dev)
     recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
-    hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)] if (gather and ws > 1) else None
+    hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)] if (gather and dist_on(ws)) else None
     if "off" in b:
         # mixed sizes: per-frame offset/length arrays, frames in batch order
         # (measured faster than length-binned order, whose per-frame record
@@ -99,7 +108,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     else:
         kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
     gout = None
-    if gather and ws > 1:
+    if gather and dist_on(ws):
         gout = torch.empty(n * ws, dtype=torch.int64, device=dev)
 
     work = [None]
@@ -464,7 +473,7 @@ def main():
                       args.settle)
     log(f"[rank {rank}] {primary_cfg}: {prim['mpkts']:.1f} Mpkts/s, kernel {prim['kernel_ms']:.3f} ms")
     nog = gat = None
-    if ws > 1:
+    if dist_on(ws):
         # same launches without the collective: the kernel-only duration the
         # roofline uses, and the rate "without the gather" 
         nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False,
@@ -579,7 +588,7 @@ def main():
             "config": {"workload": f"{primary_cfg.upper()}: {n} frames per GPU"
                                    + (" x 1500 B IPv4/TCP" if primary_cfg == "c1500" else ""),
                        "frames_per_gpu": n, "global_frames": n * ws,
-                       "parallelism": f"shard{ws}" + ("+allgather(flow_hash)" if ws > 1 else ""),
+                       "parallelism": f"shard{ws}" + ("+allgather(flow_hash)" if dist_on(ws) else ""),
                        "key": "01..10"},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -594,7 +603,7 @@ def main():
             "rewrite": rewrite,
         }
         print(json.dumps(line), flush=True)
-    if ws > 1:
+    if dist_on(ws):
         import torch.distributed as dist
         dist.destroy_process_group()
 
