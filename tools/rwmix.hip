@@ -9,7 +9,12 @@
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool NT>
+// INDEP: the burst stores a value that does not depend on the tile's loads
+// (so the stores need not wait for them): separates the memory's cost of the
+// writes from the wait the dependent stores put on the read stream.
+// WRAP: the bursts go to a 32 MiB window reused over and over (they stay in
+// the caches; not a real output, an experiment on where the write cost is).
+template <bool NT, bool INDEP = false, bool WRAP = false, bool NTST = true, uint32_t WIN = 32u << 20>
 __global__ __launch_bounds__(256) void rw_kernel(const u32x4 *in, u32x4 *out, uint64_t ntiles,
                                                  uint32_t rb16, uint32_t wb16, uint32_t *sink) {
   const int lane = threadIdx.x & 63;
@@ -28,10 +33,11 @@ __global__ __launch_bounds__(256) void rw_kernel(const u32x4 *in, u32x4 *out, ui
       for (int u = 0; u < 8; ++u) acc ^= v[u];
     }
     for (; k < rb16; k += 64) acc ^= p[k];
-    u32x4 *q = out + t * (uint64_t)wb16;
+    u32x4 *q = out + (WRAP ? (t * (uint64_t)wb16) & (WIN / 16 - 1) : t * (uint64_t)wb16);
+    const u32x4 val = INDEP ? u32x4{(uint32_t)t, (uint32_t)lane, 0u, 0u} : acc;
     for (uint32_t e = lane; e < wb16; e += 64) {
-      if (NT) __builtin_nontemporal_store(acc, q + e);
-      else q[e] = acc;
+      if (NT && NTST) __builtin_nontemporal_store(val, q + e);
+      else q[e] = val;
     }
   }
   const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
@@ -40,7 +46,19 @@ __global__ __launch_bounds__(256) void rw_kernel(const u32x4 *in, u32x4 *out, ui
 
 extern "C" int rwmix_run(const void *in, void *out, uint64_t ntiles, uint32_t rb, uint32_t wb,
                          int nt, int grid, uint32_t *sink, void *stream) {
-  if (nt)
+  if (nt == 13)
+    hipLaunchKernelGGL((rw_kernel<true, false, true, false, (1u << 20)>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4 *)in, (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else if (nt == 9)
+    hipLaunchKernelGGL((rw_kernel<true, false, false, false>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4 *)in, (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else if (nt == 5)
+    hipLaunchKernelGGL((rw_kernel<true, false, true>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4 *)in, (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else if (nt == 3)
+    hipLaunchKernelGGL((rw_kernel<true, true>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4 *)in, (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else if (nt)
     hipLaunchKernelGGL(rw_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                        (const u32x4 *)in, (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
   else

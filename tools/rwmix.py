@@ -5,7 +5,11 @@
 Reads 24 GiB worth of tiles (a 6 GiB buffer read 4 times over would hit
 the caches differently, so the buffer is the full 24 GiB) and writes 1/24
 of that, in bursts of wb bytes per rb-byte tile, for several burst sizes at
-the same read:write ratio; plus read-only and write-only references."""
+the same read:write ratio; plus a read-only reference.  Store modes (the
+`nt` key, see rwmix.hip): 1 = non-temporal loads and stores (the rx
+kernel's policy), 3 = stores independent of the loads, 5 = stores into a
+reused 32 MiB window, 9 = ordinary (write-back) stores, 13 = ordinary stores
+into a reused 1 MiB window (they never leave L2)."""
 import ctypes
 import json
 import os
@@ -60,15 +64,14 @@ def main():
     sink = torch.zeros(64, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    settings = [(96 << 10, 0), (96 << 10, 4 << 10), (192 << 10, 8 << 10), (384 << 10, 16 << 10),
-                (768 << 10, 32 << 10), (1536 << 10, 64 << 10), (48 << 10, 2 << 10)]
+    settings = [(96 << 10, 0), (96 << 10, 4 << 10), (1536 << 10, 64 << 10)]
     res = {}
-    for rounds in range(3):
-        for nt in (1, 0):
+    for rounds in range(2):
+        for nt in (1, 5, 9, 13):
             for grid_mult in (2,):
                 for rb, wb in settings:
                     ntiles = total // rb
-                    key = f"rb{rb >> 10}k_wb{wb >> 10}k_nt{nt}"
+                    key = f"rb{rb >> 10}k_wb{wb >> 10}k_nt{nt}_g{grid_mult}"
                     ts = []
                     for k in range(4):
                         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
