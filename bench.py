@@ -368,6 +368,51 @@ def rewrite_bench(ctx, n, dev, rank, steps, warmup):
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
 
 
+def mss_bench(ctx, n, dev, steps, warmup, stride=80):
+    """TCP MSS clamping (pptk_tcp_mss_clamp_device) of n IPv4 SYNs in place,
+    each carrying a typical SYN option list (MSS 1460, SACK-permitted,
+    timestamps, NOP, window scale: 74-byte frames in 80-byte slots); every
+    timed launch clamps to a lower value than the one before, so every frame
+    is parsed, walked and written (4 bytes) in every launch."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import framegen
+    rng = np.random.default_rng(0x355)
+    opts = (b"\x02\x04\x05\xb4" + b"\x04\x02" + b"\x08\x0a" + bytes(8) + b"\x01"
+            + b"\x03\x03\x07")
+    f = framegen.frame_tcp_opts(rng, opts=opts, payload=b"")
+    slot = np.zeros(stride, np.uint8)
+    slot[:len(f)] = np.frombuffer(f, np.uint8)
+    frames = torch.from_numpy(slot).to(dev).repeat(n)
+    kw = dict(stride=stride, fixed_len=len(f))
+    mss = 1460
+    assert warmup + steps < 400
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    for _ in range(warmup):
+        mss -= 1
+        ctx.mss_clamp_device(frames, n, mss, syn_only=True, status=st, **kw)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for a, z in ev:
+        mss -= 1
+        a.record()
+        ctx.mss_clamp_device(frames, n, mss, syn_only=True, status=st, **kw)
+        z.record()
+    torch.cuda.synchronize(dev)
+    clamped = int((st == 7).sum().item())
+    ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
+    ach = n * len(f) / (ms * 1e-3) / 1e9
+    del frames, st
+    torch.cuda.empty_cache()
+    return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "kernel_ms": round(ms, 4),
+            "workload": f"{n} IPv4 SYNs ({len(f)} B, MSS/SACK-perm/TS/NOP/WS options) in "
+                        f"{stride}-byte slots, MSS clamped in place with checksum update",
+            "clamped_every_frame": clamped == n,
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
+
+
 def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
     """Batched ip_permitted over the records of a C64
     batch: buckets of the /24 source prefixes in 2^16 buckets, every IPv4
@@ -563,10 +608,13 @@ def main():
             del r["_batch"], r["_recs"]
             torch.cuda.empty_cache()
 
-    permit = rewrite = None
+    permit = rewrite = mss = None
     if not args.no_secondary and args.only is None:
         permit = permit_bench(n, dev, ws, rank, args.steps, args.warmup)
         log(f"[rank {rank}] permit: {permit}")
+        if args.steps + args.warmup < 400:
+            mss = mss_bench(ctx, n, dev, args.steps, args.warmup)
+            log(f"[rank {rank}] mss: {mss}")
         if args.steps + args.warmup < 64:
             rewrite = rewrite_bench(ctx, n, dev, rank, args.steps, args.warmup)
             log(f"[rank {rank}] rewrite: {rewrite}")
@@ -601,6 +649,7 @@ def main():
             "permit": permit,
             "tx": tx,
             "rewrite": rewrite,
+            "mss_clamp": mss,
         }
         print(json.dumps(line), flush=True)
     if dist_on(ws):

@@ -95,32 +95,63 @@ static inline uint16_t tcp46_cksum_calc(const void *iphdr)
  * verify (ipcksum.h:101-211): zero the field, compute, store. */
 static inline void ip_set_hdr_cksum_calc(void *iphdr, uint16_t iplen)
 {
+  if (iplen < 20)
+    abort();
   ip_set_hdr_cksum(iphdr, 0);
   ip_set_hdr_cksum(iphdr, ip_hdr_cksum_calc(iphdr, iplen));
 }
 
+/* ipcksum.h:113-128: IPv6 has no header checksum (nothing to do) */
+static inline void ip46_set_hdr_cksum_calc(void *iphdr)
+{
+  if (pptk_ipver_or_die(iphdr) == 4)
+    ip_set_hdr_cksum_calc(iphdr, ip_hdr_len(iphdr));
+}
+
 static inline void tcp_set_cksum_calc(void *iphdr, uint16_t iplen, void *tcphdr, uint16_t tcplen)
 {
+  if (iplen < 20 || tcplen < 20)
+    abort();
   tcp_set_cksum(tcphdr, 0);
   tcp_set_cksum(tcphdr, tcp_cksum_calc(iphdr, iplen, tcphdr, tcplen));
 }
 
 static inline void udp_set_cksum_calc(void *iphdr, uint16_t iplen, void *udphdr, uint16_t udplen)
 {
+  if (iplen < 20 || udplen < 8)
+    abort();
   udp_set_cksum(udphdr, 0);
   udp_set_cksum(udphdr, udp_cksum_calc(iphdr, iplen, udphdr, udplen));
 }
 
 static inline void tcp6_set_cksum_calc(void *iphdr, uint16_t iplen, void *tcphdr, uint16_t tcplen)
 {
+  if (iplen < 40 || tcplen < 20)
+    abort();
   tcp_set_cksum(tcphdr, 0);
   tcp_set_cksum(tcphdr, tcp6_cksum_calc(iphdr, iplen, tcphdr, tcplen));
 }
 
 static inline void udp6_set_cksum_calc(void *iphdr, uint16_t iplen, void *udphdr, uint16_t udplen)
 {
+  if (iplen < 40 || udplen < 8)
+    abort();
   udp_set_cksum(udphdr, 0);
   udp_set_cksum(udphdr, udp6_cksum_calc(iphdr, iplen, udphdr, udplen));
+}
+
+/* ipcksum.h:160-181: TCP at the fixed header length, as tcp46_cksum_calc */
+static inline void tcp46_set_cksum_calc(void *iphdr)
+{
+  uint16_t tcplen = ip46_payload_len(iphdr);
+  uint16_t iplen = ip46_hdr_len(iphdr);
+  void *tcphdr = (unsigned char *)iphdr + iplen;
+  if (ip46_proto(iphdr) != 6)
+    abort();
+  if (ip_version(iphdr) == 4)
+    tcp_set_cksum_calc(iphdr, iplen, tcphdr, tcplen);
+  else
+    tcp6_set_cksum_calc(iphdr, iplen, tcphdr, tcplen);
 }
 
 /* ---- incremental update (RFC 1624 eqn. 3), ipcksum.h:213-236: the new
@@ -223,6 +254,179 @@ static inline int ip_decr_ttl_cksum_update(void *pkt)
                                           (uint16_t)(((ttl - 1) << 8) | proto)));
   ip_set_ttl(pkt, (uint8_t)(ttl - 1));
   return ttl - 1 > 0;
+}
+
+/* ---- TCP / ICMP field rewrites with incremental update, ipcksum.h:283-321 */
+static inline void icmp_set_echo_identifier_cksum_update(void *icmphdr, uint16_t icmplen,
+                                                         uint16_t id)
+{
+  (void)icmplen;
+  icmp_set_checksum(icmphdr, ip_update_cksum16(icmp_checksum(icmphdr),
+                                               icmp_echo_identifier(icmphdr), id));
+  icmp_set_echo_identifier(icmphdr, id);
+}
+
+static inline void tcp_set_seq_number_cksum_update(void *tcphdr, uint16_t tcplen, uint32_t seq)
+{
+  (void)tcplen;
+  tcp_set_cksum(tcphdr, (uint16_t)ip_update_cksum32(tcp_cksum(tcphdr), tcp_seq_number(tcphdr), seq));
+  tcp_set_seq_number(tcphdr, seq);
+}
+
+static inline void tcp_set_ack_number_cksum_update(void *tcphdr, uint16_t tcplen, uint32_t ack)
+{
+  (void)tcplen;
+  tcp_set_cksum(tcphdr, (uint16_t)ip_update_cksum32(tcp_cksum(tcphdr), tcp_ack_number(tcphdr), ack));
+  tcp_set_ack_number(tcphdr, ack);
+}
+
+static inline void tcp_set_window_cksum_update(void *tcphdr, uint16_t tcplen, uint16_t window)
+{
+  (void)tcplen;
+  tcp_set_cksum(tcphdr, ip_update_cksum16(tcp_cksum(tcphdr), tcp_window(tcphdr), window));
+  tcp_set_window(tcphdr, window);
+}
+
+/* ipcksum.h:395-406: clear ACK; the flags byte shares a word with the data
+ * offset (bytes 12-13) */
+static inline void tcp_set_ack_off_cksum_update(void *pkt)
+{
+  unsigned char *t = (unsigned char *)pkt;
+  uint16_t w_old = hdr_get16n(t + 12);
+  t[13] &= (unsigned char)~0x10;
+  tcp_set_cksum(pkt, ip_update_cksum16(tcp_cksum(pkt), w_old, hdr_get16n(t + 12)));
+}
+
+/* ---- TCP option rewrites, ipcksum.h:408-650.  The checksum sums 16-bit
+ * words from the start of the TCP header, so a field at an odd offset is
+ * folded in through the two words that straddle it: each straddling word is
+ * read before and after the field is written, and the updates are applied
+ * in the reference's order (one's-complement results can differ between
+ * orders only in the representation of zero, so the order is kept). */
+/* ipcksum.h:408-464: overwrite a SACK option with NOPs (kind 1); the
+ * "unaligned" form updates the two words straddling each rewritten pair
+ * (reading the byte before the option and the one after each pair). */
+static inline void tcp_disable_sack_cksum_update(void *pkt, void *sackhdr, size_t sacklen,
+                                                 int sixteen_bit_align)
+{
+  unsigned char *h = (unsigned char *)sackhdr;
+  uint16_t c = tcp_cksum(pkt);
+  size_t k = 0;
+  for (; k + 1 <= sacklen; k += 2) {
+    const int whole = k + 2 <= sacklen;   /* a pair, or the odd last byte */
+    if (sixteen_bit_align) {
+      uint16_t o = hdr_get16n(h + k);
+      uint16_t nw = whole ? 0x0101 : (uint16_t)((o & 0xff) | 0x0100);
+      c = ip_update_cksum16(c, o, nw);
+      hdr_set16n(h + k, nw);
+    } else {
+      uint16_t o1 = hdr_get16n(h + k - 1), o2 = hdr_get16n(h + k + 1);
+      uint16_t nw = whole ? 0x0101 : (uint16_t)((hdr_get16n(h + k) & 0xff) | 0x0100);
+      hdr_set16n(h + k, nw);
+      c = ip_update_cksum16(c, o1, hdr_get16n(h + k - 1));
+      c = ip_update_cksum16(c, o2, hdr_get16n(h + k + 1));
+    }
+    if (!whole)
+      break;
+  }
+  tcp_set_cksum(pkt, c);
+}
+
+/* ipcksum.h:466-489: set the MSS option's value (mssoff from
+ * tcp_parse_options) */
+static inline void tcp_set_mss_cksum_update(void *pkt, struct tcp_information *opts, uint16_t mss)
+{
+  unsigned char *t = (unsigned char *)pkt;
+  const size_t f = (size_t)opts->mssoff + 2;   /* the value field */
+  uint16_t c = tcp_cksum(pkt);
+  if (f % 2 == 0) {
+    c = ip_update_cksum16(c, hdr_get16n(t + f), mss);
+    hdr_set16n(t + f, mss);
+  } else {
+    uint16_t o1 = hdr_get16n(t + f - 1), o2 = hdr_get16n(t + f + 1);
+    hdr_set16n(t + f, mss);
+    c = ip_update_cksum16(c, o1, hdr_get16n(t + f - 1));
+    c = ip_update_cksum16(c, o2, hdr_get16n(t + f + 1));
+  }
+  tcp_set_cksum(pkt, c);
+}
+
+/* ipcksum.h:491-537: add `adjustment` to every SACK block edge (8-byte
+ * blocks from option offset 2).  In the reference's unaligned branch the
+ * block loop never advances (no `curoff += 8`, :512-535), so for a SACK
+ * option of 10 or more bytes at an odd offset it does not return; here each
+ * block is adjusted once, the evident intent (parity unpinned for that
+ * branch; the aligned branch and short unaligned options match). */
+static inline void tcp_adjust_sack_cksum_update(void *pkt, void *sackhdr, size_t sacklen,
+                                                int sixteen_bit_align, uint32_t adjustment)
+{
+  unsigned char *h = (unsigned char *)sackhdr;
+  uint16_t c = tcp_cksum(pkt);
+  size_t k;
+  for (k = 2; k + 8 <= sacklen; k += 8) {
+    const uint32_t s_new = hdr_get32n(h + k) + adjustment;
+    const uint32_t e_new = hdr_get32n(h + k + 4) + adjustment;
+    if (sixteen_bit_align) {
+      c = (uint16_t)ip_update_cksum32(c, hdr_get32n(h + k), s_new);
+      c = (uint16_t)ip_update_cksum32(c, hdr_get32n(h + k + 4), e_new);
+      hdr_set32n(h + k, s_new);
+      hdr_set32n(h + k + 4, e_new);
+    } else {
+      uint16_t o1 = hdr_get16n(h + k - 1);
+      uint32_t o2 = hdr_get32n(h + k + 1), o3 = hdr_get32n(h + k + 5);
+      hdr_set32n(h + k, s_new);
+      hdr_set32n(h + k + 4, e_new);
+      c = ip_update_cksum16(c, o1, hdr_get16n(h + k - 1));
+      c = (uint16_t)ip_update_cksum32(c, o2, hdr_get32n(h + k + 1));
+      c = (uint16_t)ip_update_cksum32(c, o3, hdr_get32n(h + k + 5));
+    }
+  }
+  tcp_set_cksum(pkt, c);
+}
+
+/* ipcksum.h:539-611: add `adjustment` to the timestamp value (field at
+ * tsoff + 2) or echo reply (tsoff + 6); nothing without a timestamp option */
+static inline void pptk_tcp_adjust_ts32(void *pkt, size_t f, uint32_t adjustment)
+{
+  unsigned char *t = (unsigned char *)pkt;
+  uint16_t c = tcp_cksum(pkt);
+  const uint32_t nw = hdr_get32n(t + f) + adjustment;
+  if (f % 2 == 0) {
+    c = (uint16_t)ip_update_cksum32(c, hdr_get32n(t + f), nw);
+    hdr_set32n(t + f, nw);
+  } else {
+    uint16_t o[3];
+    int i;
+    for (i = 0; i < 3; i++)
+      o[i] = hdr_get16n(t + f - 1 + 2 * i);
+    hdr_set32n(t + f, nw);
+    for (i = 0; i < 3; i++)
+      c = ip_update_cksum16(c, o[i], hdr_get16n(t + f - 1 + 2 * i));
+  }
+  tcp_set_cksum(pkt, c);
+}
+
+static inline void tcp_adjust_tsval_cksum_update(void *pkt, struct sack_ts_headers *hdrs,
+                                                 uint32_t adjustment)
+{
+  if (hdrs->tsoff != 0)
+    pptk_tcp_adjust_ts32(pkt, (size_t)hdrs->tsoff + 2, adjustment);
+}
+
+static inline void tcp_adjust_tsecho_cksum_update(void *pkt, struct sack_ts_headers *hdrs,
+                                                  uint32_t adjustment)
+{
+  if (hdrs->tsoff != 0)
+    pptk_tcp_adjust_ts32(pkt, (size_t)hdrs->tsoff + 6, adjustment);
+}
+
+/* ipcksum.h:613-623 */
+static inline void tcp_adjust_sack_cksum_update_2(void *pkt, struct sack_ts_headers *hdrs,
+                                                  uint32_t adjustment)
+{
+  if (hdrs->sackoff != 0)
+    tcp_adjust_sack_cksum_update(pkt, (unsigned char *)pkt + hdrs->sackoff, hdrs->sacklen,
+                                 !(hdrs->sackoff % 2), adjustment);
 }
 
 #ifdef __cplusplus

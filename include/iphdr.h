@@ -187,4 +187,79 @@ static inline void udp_set_src_port(void *l4, uint16_t p) { hdr_set16n(PPTK_W(l4
 static inline void udp_set_dst_port(void *l4, uint16_t p) { hdr_set16n(PPTK_W(l4, 2), p); }
 static inline void udp_set_cksum(void *l4, uint16_t c) { hdr_set16n(PPTK_W(l4, 6), c); }
 
+/* ---- TCP flags, sequence space, window: iphdr.h:1327-1379, 1441-1489.
+ * tcp_set_data_offset abort()s on a value that is not a multiple of 4 or
+ * exceeds 60, as the reference does (a caller contract violation). */
+static inline int tcp_ack(const void *l4) { return !!(*PPTK_AT(l4, 13) & 0x10); }
+static inline int tcp_rst(const void *l4) { return !!(*PPTK_AT(l4, 13) & 0x04); }
+static inline int tcp_syn(const void *l4) { return !!(*PPTK_AT(l4, 13) & 0x02); }
+static inline int tcp_fin(const void *l4) { return !!(*PPTK_AT(l4, 13) & 0x01); }
+static inline void tcp_set_ack_on(void *l4) { *PPTK_W(l4, 13) |= 0x10; }
+static inline void tcp_set_ack_off(void *l4) { *PPTK_W(l4, 13) &= (unsigned char)~0x10; }
+static inline void tcp_set_rst_on(void *l4) { *PPTK_W(l4, 13) |= 0x04; }
+static inline void tcp_set_syn_on(void *l4) { *PPTK_W(l4, 13) |= 0x02; }
+static inline void tcp_set_fin_on(void *l4) { *PPTK_W(l4, 13) |= 0x01; }
+static inline uint32_t tcp_seq_number(const void *l4) { return hdr_get32n(PPTK_AT(l4, 4)); }
+static inline uint32_t tcp_ack_number(const void *l4) { return hdr_get32n(PPTK_AT(l4, 8)); }
+static inline void tcp_set_seq_number(void *l4, uint32_t v) { hdr_set32n(PPTK_W(l4, 4), v); }
+static inline void tcp_set_ack_number(void *l4, uint32_t v) { hdr_set32n(PPTK_W(l4, 8), v); }
+static inline uint16_t tcp_window(const void *l4) { return hdr_get16n(PPTK_AT(l4, 14)); }
+static inline void tcp_set_window(void *l4, uint16_t v) { hdr_set16n(PPTK_W(l4, 14), v); }
+static inline void tcp_set_data_offset(void *l4, uint8_t data_off)
+{
+  if (data_off % 4 != 0 || data_off > 60)
+    abort();
+  *PPTK_W(l4, 12) = (unsigned char)((*PPTK_AT(l4, 12) & 0x0f) | ((data_off / 4) << 4));
+}
+
+/* ---- ICMP echo fields: iphdr.h:197-250 */
+static inline uint8_t icmp_type(const void *l4) { return *PPTK_AT(l4, 0); }
+static inline uint8_t icmp_code(const void *l4) { return *PPTK_AT(l4, 1); }
+static inline uint16_t icmp_checksum(const void *l4) { return hdr_get16n(PPTK_AT(l4, 2)); }
+static inline uint32_t icmp_header_data(const void *l4) { return hdr_get32n(PPTK_AT(l4, 4)); }
+static inline uint16_t icmp_echo_identifier(const void *l4) { return hdr_get16n(PPTK_AT(l4, 4)); }
+static inline void icmp_set_type(void *l4, uint8_t v) { *PPTK_W(l4, 0) = v; }
+static inline void icmp_set_code(void *l4, uint8_t v) { *PPTK_W(l4, 1) = v; }
+static inline void icmp_set_checksum(void *l4, uint16_t v) { hdr_set16n(PPTK_W(l4, 2), v); }
+static inline void icmp_set_header_data(void *l4, uint32_t v) { hdr_set32n(PPTK_W(l4, 4), v); }
+static inline void icmp_set_echo_identifier(void *l4, uint16_t v) { hdr_set16n(PPTK_W(l4, 4), v); }
+
+/* ---- TCP options: iphdr.h:1497-1545, iphdr/iphdr.c:4-246.  Offsets are
+ * from the start of the TCP header; the walks read bytes [20, data offset)
+ * of it (pptk_amd/csrc/host/tcpopt.c). */
+struct sack_ts_headers {
+  uint8_t sackoff;   /* SACK option (kind 5), 0 = none */
+  uint8_t sacklen;
+  uint8_t tsoff;     /* timestamp option (kind 8, length 10), 0 = none */
+};
+
+struct tcp_information {
+  uint8_t options_valid;
+  uint8_t wscale;
+  uint16_t mss;      /* 536 unless an MSS option is present */
+  uint8_t sack_permitted;
+  uint8_t mssoff;    /* from the beginning of the TCP header, 0 = none */
+  uint8_t ts_present;
+  uint32_t ts;
+  uint32_t tsecho;
+};
+
+void tcp_parse_options(void *pkt, struct tcp_information *info);
+void tcp_find_sack_ts_headers(void *pkt, struct sack_ts_headers *hdrs);
+void *tcp_find_sack_header(void *pkt, size_t *sacklen, int *sixteen_bit_align);
+
+static inline uint32_t tcp_tsval(const void *l4, struct sack_ts_headers *hdrs)
+{
+  if (hdrs->tsoff < 20)
+    abort();
+  return hdr_get32n(PPTK_AT(l4, hdrs->tsoff + 2));
+}
+
+static inline uint32_t tcp_tsecho(const void *l4, struct sack_ts_headers *hdrs)
+{
+  if (hdrs->tsoff < 20)
+    abort();
+  return hdr_get32n(PPTK_AT(l4, hdrs->tsoff + 6));
+}
+
 #endif

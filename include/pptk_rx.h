@@ -250,6 +250,28 @@ int pptk_tx_rewrite_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uin
                            uint64_t n, const struct pptk_rewrite *d_rw, uint64_t rw_count,
                            uint8_t *d_status, void *stream);
 
+/* TCP MSS clamping with incremental checksum update (middlebox / tunnel
+ * ingress), reference iphdr/iphdr.c:4-132 (tcp_parse_options) and
+ * iphdr/ipcksum.h:466-489 (tcp_set_mss_cksum_update): per frame with a TCP
+ * header (the receive transform's record: PPTK_RX_F_L4 and proto 6, IPv4 or
+ * IPv6, with or without a VLAN tag; with PPTK_MSS_SYN_ONLY also the SYN flag
+ * set), whose options lie inside the segment (l4_off + data offset <= L4
+ * end), tcp_parse_options is applied to the TCP header; if the option list
+ * is valid and holds an MSS option whose value exceeds `mss`, the value
+ * becomes `mss` through tcp_set_mss_cksum_update -- results identical to
+ * those two calls.  Everything else is left untouched.  d_status (nullable)
+ * receives per frame PPTK_MSS_ST_* bits.  Layout arguments as in
+ * pptk_tx_cksum_device.  Asynchronous on `stream`. */
+#define PPTK_MSS_SYN_ONLY 0x1u
+#define PPTK_MSS_ST_TCP 0x1u       /* TCP header present (and SYN if asked) */
+#define PPTK_MSS_ST_FOUND 0x2u     /* valid options with an MSS option      */
+#define PPTK_MSS_ST_CLAMPED 0x4u   /* MSS lowered to `mss`                  */
+#define PPTK_MSS_ST_BADOPT 0x8u    /* options past the segment or malformed */
+int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint64_t *d_off,
+                              const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
+                              uint64_t n, uint16_t mss, uint32_t flags, uint8_t *d_status,
+                              void *stream);
+
 /* Tuning: force kernel variant `variant` (0 .. pptk_rx_variant_count()-1)
  * and/or memory-policy flags for every later batch of this context; -1
  * restores the automatic choice (variant by frame length and alignment).

@@ -74,6 +74,20 @@ def _rewrite(fn, buf, rw, off, lens, stride, fixed_len, n):
 
 _RW_ARGS = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t, _vp,
             ctypes.c_uint64, _vp]
+_MSS_ARGS = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_uint16,
+             ctypes.c_uint32, _vp]
+
+
+def _mss(fn, buf, mss, flags, off, lens, stride, fixed_len, n):
+    out = np.array(buf, dtype=np.uint8, copy=True)
+    off = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    lens = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    if n is None:
+        n = len(off) if off is not None else len(buf) // stride
+    status = np.zeros(n, dtype=np.uint8)
+    fn(_ptr(out), _ptr(off), _ptr(lens), ctypes.c_uint64(stride), ctypes.c_uint32(fixed_len),
+       ctypes.c_size_t(n), ctypes.c_uint16(mss), ctypes.c_uint32(flags), _ptr(status))
+    return out, status
 
 
 class _Lib:
@@ -133,6 +147,8 @@ class Oracle(_Lib):
         L.orc_tx_batch.restype = None
         L.orc_rewrite_batch.restype = None
         L.orc_rewrite_batch.argtypes = _RW_ARGS
+        L.orc_mss_clamp_batch.restype = None
+        L.orc_mss_clamp_batch.argtypes = _MSS_ARGS
         L.orc_update_cksum16.restype = ctypes.c_uint16
         L.orc_update_cksum16.argtypes = [ctypes.c_uint16] * 3
         L.orc_update_cksum32.restype = ctypes.c_uint16
@@ -168,6 +184,12 @@ class Oracle(_Lib):
         """Header rewrite with incremental checksum updates (REWRITE_DTYPE
         entries, 1 or n); returns (updated copy of buf, status per frame)."""
         return _rewrite(self.lib.orc_rewrite_batch, buf, rw, off, lens, stride, fixed_len, n)
+
+    def mss_clamp_batch(self, buf, mss, flags=0, off=None, lens=None, stride=0, fixed_len=0,
+                        n=None):
+        """TCP MSS clamping; returns (updated copy of buf, status per frame)."""
+        return _mss(self.lib.orc_mss_clamp_batch, buf, mss, flags, off, lens, stride, fixed_len,
+                    n)
 
     def update_cksum16(self, c, old, new):
         return self.lib.orc_update_cksum16(c, old, new)
@@ -239,6 +261,16 @@ class Reference(_Lib):
         L.ref_tx_batch.restype = None
         L.ref_rewrite_batch.restype = None
         L.ref_rewrite_batch.argtypes = _RW_ARGS
+        L.ref_mss_clamp_batch.restype = None
+        L.ref_mss_clamp_batch.argtypes = _MSS_ARGS
+        L.ref_tcp_parse_options.restype = ctypes.c_uint32
+        L.ref_tcp_parse_options.argtypes = [_vp, _vp, _vp, _vp]
+        L.ref_tcp_find_sack_ts.restype = ctypes.c_uint32
+        L.ref_tcp_find_sack_ts.argtypes = [_vp]
+        L.ref_tcp_find_sack.restype = ctypes.c_int64
+        L.ref_tcp_find_sack.argtypes = [_vp, _vp, _vp]
+        L.ref_tcp_opt_op.restype = None
+        L.ref_tcp_opt_op.argtypes = [_vp, ctypes.c_int, ctypes.c_uint32]
         L.ref_update_cksum16.restype = ctypes.c_uint16
         L.ref_update_cksum16.argtypes = [ctypes.c_uint16] * 3
         L.ref_update_cksum32.restype = ctypes.c_uint16
@@ -272,6 +304,13 @@ class Reference(_Lib):
         """The reference's incremental-update functions (iphdr/ipcksum.h:
         213-393) as pptk_tx_rewrite_device composes them."""
         return _rewrite(self.lib.ref_rewrite_batch, buf, rw, off, lens, stride, fixed_len, n)
+
+    def mss_clamp_batch(self, buf, mss, flags=0, off=None, lens=None, stride=0, fixed_len=0,
+                        n=None):
+        """The reference's tcp_parse_options + tcp_set_mss_cksum_update as
+        pptk_tcp_mss_clamp_device composes them."""
+        return _mss(self.lib.ref_mss_clamp_batch, buf, mss, flags, off, lens, stride, fixed_len,
+                    n)
 
     def update_cksum16(self, c, old, new):
         return self.lib.ref_update_cksum16(c, old, new)

@@ -559,3 +559,123 @@ uint16_t ref_update_cksum32(uint16_t c, uint32_t o, uint32_t nw)
 {
   return (uint16_t)ip_update_cksum32(c, o, nw);
 }
+
+/* ---- MSS clamping: the reference's tcp_parse_options (iphdr/iphdr.c:4-132)
+ * and tcp_set_mss_cksum_update (iphdr/ipcksum.h:466-489), composed as
+ * pptk_tcp_mss_clamp_device defines (include/pptk_rx.h). */
+void ref_mss_clamp_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                         uint32_t fixed_len, size_t n, uint16_t mss, uint32_t flags,
+                         uint8_t *status)
+{
+  struct ref_opts o;
+  size_t i;
+  memset(&o, 0, sizeof(o));
+  for (i = 0; i < n; i++) {
+    uint8_t *f = buf + (off ? off[i] : i * stride);
+    const uint32_t flen = len ? len[i] : fixed_len;
+    struct pptk_rx_rec r;
+    struct tcp_information info;
+    uint8_t *t, st = 0;
+    ref_rx_one(f, flen, &o, &r, 0);
+    if ((r.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED | PPTK_RX_F_L4)) !=
+            (PPTK_RX_F_PARSED | PPTK_RX_F_L4) ||
+        r.proto != 6)
+      goto done;
+    t = f + r.l4_off;
+    if ((flags & PPTK_MSS_SYN_ONLY) && !tcp_syn(t))
+      goto done;
+    st = PPTK_MSS_ST_TCP;
+    if (tcp_data_offset(t) > r.l4_len) {
+      st |= PPTK_MSS_ST_BADOPT;
+      goto done;
+    }
+    tcp_parse_options(t, &info);
+    if (!info.options_valid) {
+      st |= PPTK_MSS_ST_BADOPT;
+      goto done;
+    }
+    if (info.mssoff == 0)
+      goto done;
+    st |= PPTK_MSS_ST_FOUND;
+    if (info.mss > mss) {
+      tcp_set_mss_cksum_update(t, &info, mss);
+      st |= PPTK_MSS_ST_CLAMPED;
+    }
+done:
+    if (status)
+      status[i] = st;
+  }
+}
+
+/* The kept TCP option API, one frame's TCP header at a time, for the
+ * host-API parity tests (tests/test_capi.py): parse results packed as
+ * valid | wscale<<8 | sack_perm<<16 | ts_present<<17 | mssoff<<24, mss,
+ * ts, tsecho; and the SACK/timestamp walk. */
+uint32_t ref_tcp_parse_options(uint8_t *t, uint16_t *mss, uint32_t *ts, uint32_t *tsecho)
+{
+  struct tcp_information info;
+  tcp_parse_options(t, &info);
+  *mss = info.mss;
+  *ts = info.ts;
+  *tsecho = info.tsecho;
+  return (uint32_t)info.options_valid | ((uint32_t)info.wscale << 8) |
+         ((uint32_t)info.sack_permitted << 16) | ((uint32_t)info.ts_present << 17) |
+         ((uint32_t)info.mssoff << 24);
+}
+
+uint32_t ref_tcp_find_sack_ts(uint8_t *t)
+{
+  struct sack_ts_headers h;
+  tcp_find_sack_ts_headers(t, &h);
+  return (uint32_t)h.sackoff | ((uint32_t)h.sacklen << 8) | ((uint32_t)h.tsoff << 16);
+}
+
+int64_t ref_tcp_find_sack(uint8_t *t, uint32_t *sacklen, int *align)
+{
+  size_t l = 0;
+  uint8_t *p = tcp_find_sack_header(t, &l, align);
+  *sacklen = (uint32_t)l;
+  return p ? (int64_t)(p - t) : -1;
+}
+
+/* Option rewrites on one TCP header (op: 0 set_mss(v), 1 disable_sack,
+ * 2 adjust_sack_2(v), 3 adjust_tsval(v), 4 adjust_tsecho(v), 5 ack_off,
+ * 6 seq(v), 7 ack(v), 8 window(v)); option offsets from the reference's
+ * own walks. */
+void ref_tcp_opt_op(uint8_t *t, int op, uint32_t v)
+{
+  struct tcp_information info;
+  struct sack_ts_headers h;
+  size_t sl = 0;
+  int al = 0;
+  void *sack;
+  switch (op) {
+  case 0:
+    tcp_parse_options(t, &info);
+    if (info.options_valid && info.mssoff)
+      tcp_set_mss_cksum_update(t, &info, (uint16_t)v);
+    break;
+  case 1:
+    sack = tcp_find_sack_header(t, &sl, &al);
+    if (sack)
+      tcp_disable_sack_cksum_update(t, sack, sl, al);
+    break;
+  case 2:
+    tcp_find_sack_ts_headers(t, &h);
+    tcp_adjust_sack_cksum_update_2(t, &h, v);
+    break;
+  case 3:
+    tcp_find_sack_ts_headers(t, &h);
+    tcp_adjust_tsval_cksum_update(t, &h, v);
+    break;
+  case 4:
+    tcp_find_sack_ts_headers(t, &h);
+    tcp_adjust_tsecho_cksum_update(t, &h, v);
+    break;
+  case 5: tcp_set_ack_off_cksum_update(t); break;
+  case 6: tcp_set_seq_number_cksum_update(t, 0, v); break;
+  case 7: tcp_set_ack_number_cksum_update(t, 0, v); break;
+  case 8: tcp_set_window_cksum_update(t, 0, (uint16_t)v); break;
+  default: break;
+  }
+}

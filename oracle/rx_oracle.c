@@ -660,3 +660,113 @@ done:
       status[i] = st;
   }
 }
+
+/* ---- TCP MSS clamping (include/pptk_rx.h pptk_tcp_mss_clamp_device).
+ * tcp_parse_options, iphdr/iphdr.c:4-132, restated literally per kind: the
+ * kinds it decodes (8 timestamp :29-48, 3 wscale :49-67, 2 MSS :68-87, 4
+ * SACK-permitted :88-106) and the generic skip (:107-119); only the MSS
+ * outputs are kept. Returns options_valid. */
+static int parse_tcp_mss(const uint8_t *t, uint32_t *mss, uint32_t *mssoff)
+{
+  const size_t dataoff = (size_t)(t[12] >> 4) * 4;   /* tcp_data_offset :1491 */
+  size_t curoff = 20;
+  *mss = 536;
+  *mssoff = 0;
+  while (curoff < dataoff) {
+    size_t lenval, want = 0;
+    if (t[curoff] == 0)
+      return 1;
+    if (t[curoff] == 1) {
+      curoff++;
+      continue;
+    }
+    switch (t[curoff]) {
+    case 8: want = 10; break;
+    case 3: want = 3; break;
+    case 2: want = 4; break;
+    case 4: want = 2; break;
+    default: break;
+    }
+    if (want) {
+      lenval = dataoff - curoff;
+      if (curoff + 1 < dataoff && t[curoff + 1] < lenval)
+        lenval = t[curoff + 1];
+      if (lenval < 2)
+        return 0;
+      if (lenval == want && t[curoff] == 2) {
+        *mss = be16_at(t + curoff + 2);
+        *mssoff = (uint32_t)curoff;
+      }
+      curoff += lenval;
+      continue;
+    }
+    if (curoff + 1 >= dataoff)
+      return 0;
+    lenval = dataoff - curoff;
+    if (t[curoff + 1] < lenval)
+      lenval = t[curoff + 1];
+    if (lenval < 2)
+      return 0;
+    curoff += lenval;
+  }
+  return 1;
+}
+
+/* tcp_set_mss_cksum_update, iphdr/ipcksum.h:466-489 */
+static void set_mss_update(uint8_t *t, uint32_t mssoff, uint16_t mss)
+{
+  uint16_t c = be16_at(t + 16);
+  if (mssoff % 2 == 0) {
+    c = orc_update_cksum16(c, be16_at(t + mssoff + 2), mss);
+    put_be16(t + mssoff + 2, mss);
+  } else {
+    const uint16_t o1 = be16_at(t + mssoff + 1), o2 = be16_at(t + mssoff + 3);
+    put_be16(t + mssoff + 2, mss);
+    c = orc_update_cksum16(c, o1, be16_at(t + mssoff + 1));
+    c = orc_update_cksum16(c, o2, be16_at(t + mssoff + 3));
+  }
+  put_be16(t + 16, c);
+}
+
+void orc_mss_clamp_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                         uint32_t fixed_len, size_t n, uint16_t mss, uint32_t flags,
+                         uint8_t *status)
+{
+  struct orc_opts o;
+  size_t i;
+  memset(&o, 0, sizeof(o));
+  for (i = 0; i < n; i++) {
+    uint8_t *f = buf + (off ? off[i] : i * stride);
+    const uint32_t flen = len ? len[i] : fixed_len;
+    struct pptk_rx_rec r;
+    uint8_t *t, st = 0;
+    uint32_t mv, mo;
+    orc_rx_one(f, flen, &o, &r);
+    if ((r.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED | PPTK_RX_F_L4)) !=
+            (PPTK_RX_F_PARSED | PPTK_RX_F_L4) ||
+        r.proto != 6)
+      goto done;
+    t = f + r.l4_off;
+    if ((flags & PPTK_MSS_SYN_ONLY) && !(t[13] & 2))   /* tcp_syn :1357 */
+      goto done;
+    st = PPTK_MSS_ST_TCP;
+    if ((uint32_t)(t[12] >> 4) * 4 > r.l4_len) {
+      st |= PPTK_MSS_ST_BADOPT;
+      goto done;
+    }
+    if (!parse_tcp_mss(t, &mv, &mo)) {
+      st |= PPTK_MSS_ST_BADOPT;
+      goto done;
+    }
+    if (mo == 0)
+      goto done;
+    st |= PPTK_MSS_ST_FOUND;
+    if (mv > mss) {
+      set_mss_update(t, mo, mss);
+      st |= PPTK_MSS_ST_CLAMPED;
+    }
+done:
+    if (status)
+      status[i] = st;
+  }
+}

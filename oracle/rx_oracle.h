@@ -53,5 +53,8 @@ uint16_t orc_update_cksum32(uint16_t cksum, uint32_t old32, uint32_t new32);
 void orc_rewrite_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
                        uint32_t fixed_len, size_t n, const struct pptk_rewrite *rw,
                        uint64_t rw_count, uint8_t *status);
+void orc_mss_clamp_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, uint64_t stride,
+                         uint32_t fixed_len, size_t n, uint16_t mss, uint32_t flags,
+                         uint8_t *status);
 
 #endif

@@ -403,6 +403,32 @@ int pptk_tx_rewrite_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint6
   return hip_err(launch_rewrite(a, grid, (hipStream_t)stream));
 }
 
+int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,
+                              const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
+                              uint64_t n, uint16_t mss, uint32_t flags, uint8_t *d_status,
+                              void *stream) {
+  if (!c || n > 0xffffffffull) return -EINVAL;
+  if (n == 0) return 0;
+  if (!d_frames || (flags & ~PPTK_MSS_SYN_ONLY) || (!d_off && stride == 0 && n > 1) ||
+      (!d_len && fixed_len > 65535))
+    return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  RxKArgs a = c->tmpl;
+  a.frames = d_frames;
+  a.frames_w = d_frames;
+  a.off = d_off;
+  a.len = d_len;
+  a.stride = stride;
+  a.fixed_len = fixed_len;
+  a.n = n;
+  a.mss = mss;
+  a.mss_flags = flags;
+  a.rw_status = d_status;
+  const uint64_t blocks = (n + 255) / 256;
+  const int grid = (int)std::min<uint64_t>(blocks, (uint64_t)c->ncu * 8);
+  return hip_err(launch_mss_clamp(a, grid, (hipStream_t)stream));
+}
+
 int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
                                uint32_t *d_perm, void *d_scratch, void *stream) {
   int rc = check_batch(c, b);

@@ -41,6 +41,9 @@ struct RxKArgs {
   const pptk_rewrite *rw;
   uint32_t rw_one;
   uint8_t *rw_status;
+  // MSS clamping (pptk_tcp_mss_clamp_device): new MSS, PPTK_MSS_* flags;
+  // the per-frame status goes to rw_status
+  uint32_t mss, mss_flags;
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S
@@ -66,6 +69,7 @@ constexpr int kGroupVariant[kGroups] = {RX_T4S2, RX_T8S2, RX_T16S2, RX_T16S4, RX
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
 hipError_t launch_rewrite(const RxKArgs &a, int grid, hipStream_t s);
+hipError_t launch_mss_clamp(const RxKArgs &a, int grid, hipStream_t s);
 int rx_variant_blocks_per_cu(int variant);
 
 // Stable counting sort of 0..n-1 into kGroups length groups.  After it,

@@ -1143,6 +1143,102 @@ __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
   }
 }
 
+// TCP MSS clamping (pptk_tcp_mss_clamp_device): one lane per frame, the
+// frame's first eight aligned chunks in the lane's LDS slot (Ethernet, IPv4
+// or IPv6 with a VLAN tag and a 20-byte IP header leave the TCP options in
+// it; longer headers reach the rest through the FrameView rare path), the
+// receive transform's parse, tcp_parse_options (iphdr/iphdr.c:4-132) over
+// the options, and tcp_set_mss_cksum_update (iphdr/ipcksum.h:466-489) when
+// the MSS option exceeds the clamp.  Only clamped frames are written (four
+// bytes: the option value and the checksum).
+constexpr int MSS_SLOT = 128;
+
+__global__ __launch_bounds__(256) void rx_mss_kernel(RxKArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[256 * MSS_SLOT];
+  LDS_AS uint8_t *slot = (LDS_AS uint8_t *)lds + threadIdx.x * MSS_SLOT;
+  const uint64_t step = (uint64_t)gridDim.x * 256u;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += step) {
+    const uint64_t base = a.off ? a.off[i] : i * a.stride;
+    const uint32_t len = a.len ? a.len[i] : a.fixed_len;
+    const int m = (int)(base & 15);
+    const int nch = max((m + (int)len + 15) >> 4, 1);
+    const u32x4 *c0 = (const u32x4 *)(a.frames + (base - (uint64_t)m));
+#pragma unroll
+    for (int c = 0; c < MSS_SLOT / 16; ++c)
+      ((LDS_AS u32x4 *)slot)[c] = c0[min(c, nch - 1)];
+    const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + base, m, MSS_SLOT - m};
+    const Parse p = parse_frame(v, len);
+    uint32_t st = 0;
+    if ((p.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED | PPTK_RX_F_L4)) ==
+            (PPTK_RX_F_PARSED | PPTK_RX_F_L4) &&
+        p.proto == 6) {
+      const int t = (int)p.rs;   // TCP header
+      if (!(a.mss_flags & PPTK_MSS_SYN_ONLY) || (v.u8(t + 13) & 2u)) {
+        st = PPTK_MSS_ST_TCP;
+        const int end = (int)(v.u8(t + 12) >> 4) * 4;   // tcp_data_offset
+        if (t + end > (int)p.re) {
+          st |= PPTK_MSS_ST_BADOPT;   // options past the segment
+        } else {
+          // tcp_parse_options: kind 0 ends the list, kind 1 is a NOP, any
+          // other option is min(length byte, bytes left) long (the bytes
+          // left when its length byte is past the options) and the list is
+          // malformed below 2; the last 4-byte MSS option counts
+          int off = 20, mssoff = 0;
+          uint32_t mssv = 536u;
+          bool valid = true;
+          while (off < end) {
+            const uint32_t kind = v.u8(t + off);
+            if (kind == 0) break;
+            if (kind == 1) {
+              ++off;
+              continue;
+            }
+            int L = end - off;
+            if (off + 1 < end) L = min(L, (int)v.u8(t + off + 1));
+            if (L < 2) {
+              valid = false;
+              break;
+            }
+            if (kind == 2 && L == 4) {
+              mssv = v.be16(t + off + 2);
+              mssoff = off;
+            }
+            off += L;
+          }
+          if (!valid) {
+            st |= PPTK_MSS_ST_BADOPT;
+          } else if (mssoff) {
+            st |= PPTK_MSS_ST_FOUND;
+            if (mssv > a.mss) {
+              // tcp_set_mss_cksum_update: a value at an even TCP offset is
+              // one checksum word; at an odd offset it straddles two, each
+              // updated with its other byte unchanged (that byte cancels in
+              // the RFC 1624 sum, so a byte past the frame is taken as 0)
+              const int f = t + mssoff + 2;
+              uint32_t ck = v.be16(t + 16);
+              if (!(mssoff & 1)) {
+                ck = upd16(ck, mssv, a.mss);
+              } else {
+                const uint32_t x1 = v.u8(f - 1);
+                const uint32_t x2 = f + 2 < (int)len ? v.u8(f + 2) : 0u;
+                ck = upd16(ck, (x1 << 8) | (mssv >> 8), (x1 << 8) | (a.mss >> 8));
+                ck = upd16(ck, ((mssv & 0xffu) << 8) | x2, ((a.mss & 0xffu) << 8) | x2);
+              }
+              GLB_AS uint8_t *fw = (GLB_AS uint8_t *)a.frames_w + base;
+              fw[f] = (uint8_t)(a.mss >> 8);
+              fw[f + 1] = (uint8_t)a.mss;
+              fw[t + 16] = (uint8_t)(ck >> 8);
+              fw[t + 17] = (uint8_t)ck;
+              st |= PPTK_MSS_ST_CLAMPED;
+            }
+          }
+        }
+      }
+    }
+    if (a.rw_status) a.rw_status[i] = (uint8_t)st;
+  }
+}
+
 template <int T, int S, int D, int AL>
 hipError_t launch_variant(const RxKArgs &a0, int grid, hipStream_t s) {
   const dim3 gd(grid), bd(WAVE * WPB);
@@ -1213,6 +1309,11 @@ hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s) {
 
 hipError_t launch_rewrite(const RxKArgs &a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(rx_rewrite_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_mss_clamp(const RxKArgs &a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(rx_mss_kernel, dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

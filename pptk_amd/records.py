@@ -30,6 +30,8 @@ REWRITE_DTYPE = np.dtype([("ops", "<u4"), ("src", "<u4"), ("dst", "<u4"),
 assert REWRITE_DTYPE.itemsize == 16
 RW_DECR_TTL, RW_SRC, RW_DST, RW_SPORT, RW_DPORT = 0x1, 0x2, 0x4, 0x8, 0x10
 RW_ST_IP, RW_ST_L4, RW_ST_TTL_ZERO, RW_ST_EXPIRED = 0x1, 0x2, 0x4, 0x8
+MSS_SYN_ONLY = 0x1
+MSS_ST_TCP, MSS_ST_FOUND, MSS_ST_CLAMPED, MSS_ST_BADOPT = 0x1, 0x2, 0x4, 0x8
 
 REC32_DTYPE = np.dtype([
     ("flow_hash", "<u8"),

@@ -46,9 +46,11 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_rewrite_device",
+           "pptk_tcp_mss_clamp_device",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
-           "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init")
+           "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init",
+           "tcp_parse_options", "tcp_find_sack_ts_headers", "tcp_find_sack_header")
 
 # Kernel variants, in the order of enum RxVariant (pptk_amd/csrc/rx_internal.h).
 VARIANTS = ("T4S1", "T4S2", "T16S2", "T16S6", "T32S3", "T64S2", "T16S7L", "T32S4L",
@@ -89,6 +91,11 @@ def lib(path=None):
             L.pptk_tx_rewrite_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp]
             L.pptk_tx_rewrite_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_tcp_mss_clamp_device"):    # absent from older A/B builds
+            L.pptk_tcp_mss_clamp_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64,
+                                                    ctypes.c_uint32, ctypes.c_uint64,
+                                                    ctypes.c_uint16, ctypes.c_uint32, vp, vp]
+            L.pptk_tcp_mss_clamp_device.restype = ctypes.c_int
         if hasattr(L, "pptk_rx_permit_device"):        # absent from older A/B builds
             L.pptk_rx_permit_scratch_bytes.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
             L.pptk_rx_permit_scratch_bytes.restype = ctypes.c_size_t
@@ -267,6 +274,19 @@ class RxContext:
                                             ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise OSError(-rc, f"pptk_tx_rewrite_device failed ({rc})")
+
+    def mss_clamp_device(self, frames, n, mss, syn_only=False, off=None, lens=None, stride=0,
+                         fixed_len=0, status=None, stream=None):
+        """TCP MSS clamping with incremental checksum update, in place and
+        asynchronously; status: optional torch uint8 CUDA tensor of n
+        PPTK_MSS_ST_* bytes."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = self._L.pptk_tcp_mss_clamp_device(self._ctx, _dp(frames), _dp(off), _dp(lens),
+                                               stride, fixed_len, n, mss, 1 if syn_only else 0,
+                                               _dp(status), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_tcp_mss_clamp_device failed ({rc})")
 
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""

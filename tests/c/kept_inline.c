@@ -48,3 +48,71 @@ void kept_set_cksums(uint8_t *f, int l3, int l4, int v6, int proto, int l4ok, ui
     else udp_set_cksum_calc(ip, ip_hdr_len(ip), p, l4len);
   }
 }
+
+/* The kept TCP option API (include/iphdr.h walks, include/ipcksum.h option
+ * rewrites), packed exactly as oracle/refgen.c's ref_tcp_* wrappers pack the
+ * reference's results, so the two compare field for field. */
+uint32_t kept_tcp_parse_options(uint8_t *t, uint16_t *mss, uint32_t *ts, uint32_t *tsecho)
+{
+  struct tcp_information info;
+  tcp_parse_options(t, &info);
+  *mss = info.mss;
+  *ts = info.ts;
+  *tsecho = info.tsecho;
+  return (uint32_t)info.options_valid | ((uint32_t)info.wscale << 8) |
+         ((uint32_t)info.sack_permitted << 16) | ((uint32_t)info.ts_present << 17) |
+         ((uint32_t)info.mssoff << 24);
+}
+
+uint32_t kept_tcp_find_sack_ts(uint8_t *t)
+{
+  struct sack_ts_headers h;
+  tcp_find_sack_ts_headers(t, &h);
+  return (uint32_t)h.sackoff | ((uint32_t)h.sacklen << 8) | ((uint32_t)h.tsoff << 16);
+}
+
+int64_t kept_tcp_find_sack(uint8_t *t, uint32_t *sacklen, int *align)
+{
+  size_t l = 0;
+  uint8_t *p = tcp_find_sack_header(t, &l, align);
+  *sacklen = (uint32_t)l;
+  return p ? (int64_t)(p - t) : -1;
+}
+
+void kept_tcp_opt_op(uint8_t *t, int op, uint32_t v)
+{
+  struct tcp_information info;
+  struct sack_ts_headers h;
+  size_t sl = 0;
+  int al = 0;
+  void *sack;
+  switch (op) {
+  case 0:
+    tcp_parse_options(t, &info);
+    if (info.options_valid && info.mssoff)
+      tcp_set_mss_cksum_update(t, &info, (uint16_t)v);
+    break;
+  case 1:
+    sack = tcp_find_sack_header(t, &sl, &al);
+    if (sack)
+      tcp_disable_sack_cksum_update(t, sack, sl, al);
+    break;
+  case 2:
+    tcp_find_sack_ts_headers(t, &h);
+    tcp_adjust_sack_cksum_update_2(t, &h, v);
+    break;
+  case 3:
+    tcp_find_sack_ts_headers(t, &h);
+    tcp_adjust_tsval_cksum_update(t, &h, v);
+    break;
+  case 4:
+    tcp_find_sack_ts_headers(t, &h);
+    tcp_adjust_tsecho_cksum_update(t, &h, v);
+    break;
+  case 5: tcp_set_ack_off_cksum_update(t); break;
+  case 6: tcp_set_seq_number_cksum_update(t, 0, v); break;
+  case 7: tcp_set_ack_number_cksum_update(t, 0, v); break;
+  case 8: tcp_set_window_cksum_update(t, 0, (uint16_t)v); break;
+  default: break;
+  }
+}

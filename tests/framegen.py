@@ -398,3 +398,143 @@ def gen_permit(n=3000, seed=0x9E7):
         else:
             frames.append(frame_v4(rng, 17, 64)[:30])  # runt: malformed
     return pack(frames)
+
+
+# ------------------------------------------------------------ TCP options
+def tcp_options(rng, syn=True):
+    """A random TCP option list (bytes, padded to a multiple of 4, <= 40):
+    well-formed lists most of the time, plus the malformed shapes the
+    reference's walks distinguish (length bytes 0/1, lengths past the end,
+    a length byte past the options, unknown kinds, EOL before the end)."""
+    out = bytearray()
+    for _ in range(int(rng.integers(0, 7))):
+        c = int(rng.integers(0, 100))
+        if c < 20:
+            out += b"\x01"                                   # NOP (shifts parity)
+        elif c < 45:
+            out += struct.pack(">BBH", 2, 4, int(rng.choice([536, 1200, 1380, 1400, 1440,
+                                                              1460, 8960, 65535,
+                                                              int(rng.integers(0, 65536))])))
+        elif c < 55:
+            out += bytes([3, 3, int(rng.integers(0, 15))])     # window scale
+        elif c < 62:
+            out += b"\x04\x02"                               # SACK permitted
+        elif c < 72:
+            out += struct.pack(">BBII", 8, 10, *(int(x) for x in rng.integers(0, 2**32, 2)))
+        elif c < 80:
+            k = int(rng.integers(1, 4))                      # SACK blocks
+            out += bytes([5, 2 + 8 * k]) + bytes(rng.integers(0, 256, 8 * k, dtype=np.uint8))
+        elif c < 85:
+            out += bytes([int(rng.choice([2, 3, 8, 5, 30])), int(rng.integers(0, 2))])  # len 0/1
+        elif c < 90:
+            out += bytes([int(rng.choice([2, 3, 4, 8, 30])), int(rng.integers(2, 60))])  # odd len
+        elif c < 95:
+            out += bytes([int(rng.integers(9, 256)), 2 + int(rng.integers(0, 5))])  # unknown
+        else:
+            out += b"\x00"                                   # EOL
+    out = out[:40]
+    while len(out) % 4:
+        out += bytes([int(rng.choice([0, 1]))])
+    return bytes(out)
+
+
+def frame_tcp_opts(rng, v6=False, vlan=None, ihl_words=5, syn=True, opts=None, payload=None,
+                   doff_override=None):
+    """A TCP frame (valid checksums) carrying `opts` (random if None)."""
+    opts = tcp_options(rng) if opts is None else opts
+    payload = bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8)) \
+        if payload is None else payload
+    sp, dp = (int(x) for x in rng.integers(0, 65536, 2))
+    flags = 0x02 if syn else 0x10
+    seg = bytearray(tcp_hdr(sp, dp, int(rng.integers(0, 2**32)), 0, flags=flags, opts=opts)
+                    + payload)
+    if doff_override is not None:
+        seg[12] = (doff_override << 4) | (seg[12] & 0x0f)
+    l4len = len(seg)
+    if v6:
+        src = bytes([0x20, 0x01]) + bytes(rng.integers(0, 256, 14, dtype=np.uint8))
+        dst = bytes([0xfd]) + bytes(rng.integers(0, 256, 15, dtype=np.uint8))
+        seg = fill_l4(seg, 6, pseudo6(src, dst, 6, l4len))
+        return eth(ETH_IP6, vlan) + ipv6_hdr(src, dst, 6, l4len) + seg
+    src = bytes([10]) + bytes(rng.integers(0, 256, 3, dtype=np.uint8))
+    dst = bytes([192, 168]) + bytes(rng.integers(0, 256, 2, dtype=np.uint8))
+    seg = fill_l4(seg, 6, pseudo4(src, dst, 6, l4len))
+    ipo = bytes(rng.integers(0, 256, (ihl_words - 5) * 4, dtype=np.uint8))
+    return eth(ETH_IP, vlan) + ipv4_hdr(src, dst, 6, l4len, ipo) + seg
+
+
+def gen_mss(n=4000, seed=0x355):
+    """MSS-clamping fixture frames: TCP over IPv4 (IHL 5-15) / IPv6, with and
+    without a VLAN tag, SYN and non-SYN, random option lists incl. malformed
+    ones, data offsets past the segment, plus UDP / non-IP frames that must
+    stay untouched."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for i in range(n):
+        c = int(rng.integers(0, 100))
+        vlan = int(rng.integers(1, 4095)) if rng.random() < 0.25 else None
+        if c < 85:
+            v6 = rng.random() < 0.3
+            ihl = 5 if v6 or rng.random() < 0.7 else int(rng.integers(6, 16))
+            frames.append(frame_tcp_opts(rng, v6=v6, vlan=vlan, ihl_words=ihl,
+                                         syn=rng.random() < 0.7))
+        elif c < 92:
+            # data offset past the segment end (options overrun): BADOPT
+            frames.append(frame_tcp_opts(rng, vlan=vlan, opts=b"\x02\x04\x05\xb4",
+                                         payload=b"", doff_override=int(rng.integers(7, 16))))
+        elif c < 96:
+            frames.append(frame_v4(rng, 17, int(rng.integers(60, 200)), vlan=vlan))
+        else:
+            frames.append(bytes(rng.integers(0, 256, int(rng.integers(14, 120)), dtype=np.uint8)))
+    return frames
+
+
+def sack_ts_walk(t):
+    """The reference's tcp_find_sack_ts_headers (iphdr/iphdr.c:134-199) on
+    TCP header bytes t, simulated: (terminates, sackoff, sacklen, tsoff).
+    A SACK or timestamp option whose length byte is 0 makes the reference
+    loop forever (terminates False) -- test inputs for the reference must
+    avoid those."""
+    end = (t[12] >> 4) * 4
+    off, sackoff, sacklen, tsoff = 20, 0, 0, 0
+    while off < end:
+        k = t[off]
+        if k == 0:
+            break
+        if k == 1:
+            off += 1
+            continue
+        ln = end - off
+        if off + 1 < end and t[off + 1] < ln:
+            ln = t[off + 1]
+        if k == 5:
+            sackoff, sacklen = off, ln
+        elif k == 8:
+            if ln == 10:
+                tsoff = off
+        elif ln < 2:
+            break
+        if ln == 0:
+            return False, sackoff, sacklen, tsoff
+        off += ln
+    return True, sackoff, sacklen, tsoff
+
+
+def tcp_headers(n=3000, seed=0x7C9, width=80):
+    """n TCP headers (width bytes each: the header with its options, then
+    payload bytes) for the kept option API: random option lists, odd
+    offsets, data offsets 0-15."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, width), np.uint8)
+    for i in range(n):
+        opts = tcp_options(rng)
+        h = bytearray(tcp_hdr(*(int(x) for x in rng.integers(0, 65536, 2)),
+                              int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32)),
+                              flags=int(rng.integers(0, 256)), win=int(rng.integers(0, 65536)),
+                              opts=opts))
+        h[16:18] = bytes(rng.integers(0, 256, 2, dtype=np.uint8))
+        if rng.random() < 0.1:
+            h[12] = (int(rng.integers(0, 16)) << 4) | (h[12] & 0x0F)
+        h += bytes(rng.integers(0, 256, width - len(h), dtype=np.uint8))
+        out[i] = np.frombuffer(bytes(h[:width]), np.uint8)
+    return out

@@ -20,6 +20,19 @@ ports), and the frames after the reference's ip_decr_ttl_cksum_update /
 ip_set_src/dst_cksum_update / tcp/udp_set_src/dst_port_cksum_update
 (oracle/refgen.c ref_rewrite_batch) with the per-frame status.
 
+mss.npz holds TCP MSS-clamping cases (pptk_tcp_mss_clamp_device): the
+framegen.gen_mss frames and, per (mss, flags) case, the changed bytes and
+per-frame status after the reference's tcp_parse_options +
+tcp_set_mss_cksum_update (oracle/refgen.c ref_mss_clamp_batch).
+
+tcpopt.npz holds kept-API cases for the TCP option functions: TCP headers
+(framegen.tcp_headers), the reference's tcp_parse_options /
+tcp_find_sack_ts_headers / tcp_find_sack_header results on them, and each
+header after one option rewrite (tcp_set_mss / disable_sack /
+adjust_sack_2 / adjust_tsval / adjust_tsecho / set_ack_off / seq / ack /
+window *_cksum_update; oracle/refgen.c ref_tcp_opt_op).  Inputs on which
+the reference never returns are marked and not run.
+
 permit.npz additionally holds rate-limiter cases: token arrays before/after
 and per-frame verdicts of the reference's ip_permitted / ipv6_permitted
 called once per subject frame in frame order (oracle/refgen.c
@@ -183,11 +196,73 @@ def gen_rewrite(ref):
     return out
 
 
+MSS_CASES = ((1200, 0), (1460, 1), (536, 0), (0, 1))
+
+
+def gen_mss(ref):
+    frames = framegen.gen_mss()
+    buf, off, lens = framegen.pack(frames)
+    out = {"buf": buf, "off": off, "len": lens, "cases": np.array(MSS_CASES, np.uint32)}
+    for k, (mss, flags) in enumerate(MSS_CASES):
+        b, st = ref.mss_clamp_batch(buf, mss, flags, off=off, lens=lens)
+        pos = np.nonzero(b != buf)[0]
+        out[f"c{k}_pos"] = pos.astype(np.uint64)
+        out[f"c{k}_out"] = b[pos]
+        out[f"c{k}_status"] = st
+    return out
+
+
+def gen_tcpopt(ref):
+    import ctypes
+    hdrs = framegen.tcp_headers()
+    n, w = hdrs.shape
+    rng = np.random.default_rng(0x0F7)
+    parse = np.zeros((n, 4), np.uint32)         # packed flags, mss, ts, tsecho
+    sackts = np.zeros((n, 2), np.uint32)        # packed (sackoff, sacklen, tsoff), ok
+    sack = np.zeros((n, 3), np.int64)           # offset or -1, length, 16-bit aligned
+    ops = np.zeros((n, 3), np.uint32)           # op, value, ran
+    after = hdrs.copy()
+    L = ref.lib
+    for i in range(n):
+        h = np.ascontiguousarray(hdrs[i]).copy()
+        p = h.ctypes.data_as(ctypes.c_void_p)
+        mss, ts, te = ctypes.c_uint16(), ctypes.c_uint32(), ctypes.c_uint32()
+        parse[i, 0] = L.ref_tcp_parse_options(p, ctypes.byref(mss), ctypes.byref(ts),
+                                              ctypes.byref(te))
+        parse[i, 1:] = (mss.value, ts.value, te.value)
+        term, so, sl, to = framegen.sack_ts_walk(h)
+        if term:
+            sackts[i] = (L.ref_tcp_find_sack_ts(p), 1)
+        sl_, al = ctypes.c_uint32(), ctypes.c_int()
+        sack[i] = (L.ref_tcp_find_sack(p, ctypes.byref(sl_), ctypes.byref(al)), sl_.value,
+                   al.value)
+        op, val = i % 9, int(rng.integers(0, 2 ** 32))
+        if op in (0, 8):
+            val &= 0xFFFF
+        ok = True
+        if op in (2, 3, 4):
+            ok = term and not (op == 2 and so % 2 == 1 and sl >= 10)
+        ops[i] = (op, val, ok)
+        if ok:
+            L.ref_tcp_opt_op(p, op, val)
+        after[i] = h
+    return {"hdrs": hdrs, "parse": parse, "sackts": sackts, "sack": sack, "ops": ops,
+            "after": after}
+
+
 def main():
     build()
     ref = Reference()
     opts = make_opts(KEY, BITS4, BITS6, HASH_SIZE)
-    want = set(sys.argv[1:]) or set(SETS) | {"permit", "tx", "rewrite"}
+    want = set(sys.argv[1:]) or set(SETS) | {"permit", "tx", "rewrite", "mss", "tcpopt"}
+    if "mss" in want:
+        path = os.path.join(HERE, "mss.npz")
+        np.savez_compressed(path, **gen_mss(ref))
+        print(f"mss -> {os.path.getsize(path)} B")
+    if "tcpopt" in want:
+        path = os.path.join(HERE, "tcpopt.npz")
+        np.savez_compressed(path, **gen_tcpopt(ref))
+        print(f"tcpopt -> {os.path.getsize(path)} B")
     if "rewrite" in want:
         path = os.path.join(HERE, "rewrite.npz")
         np.savez_compressed(path, **gen_rewrite(ref))

@@ -260,3 +260,90 @@ def test_kept_tx_setters_match_fixture(kept_inline, name):
         kept_inline.kept_set_cksums(fr, int(r["l3_off"]), int(r["l4_off"]), int(bool(fl & F_IPV6)),
                                     int(r["proto"]), int(bool(fl & F_L4)), int(r["l4_len"]))
     assert np.array_equal(buf, want), int((buf != want).sum())
+
+
+# ---- kept TCP option API (include/iphdr.h walks, include/ipcksum.h option
+# rewrites) vs the reference's results in tests/golden/tcpopt.npz
+def _kept_tcpopt(kept_inline):
+    L = kept_inline
+    vp = ctypes.c_void_p
+    L.kept_tcp_parse_options.restype = ctypes.c_uint32
+    L.kept_tcp_parse_options.argtypes = [vp, vp, vp, vp]
+    L.kept_tcp_find_sack_ts.restype = ctypes.c_uint32
+    L.kept_tcp_find_sack_ts.argtypes = [vp]
+    L.kept_tcp_find_sack.restype = ctypes.c_int64
+    L.kept_tcp_find_sack.argtypes = [vp, vp, vp]
+    L.kept_tcp_opt_op.restype = None
+    L.kept_tcp_opt_op.argtypes = [vp, ctypes.c_int, ctypes.c_uint32]
+    return L
+
+
+def test_kept_tcp_option_walks_match_fixture(kept_inline):
+    L = _kept_tcpopt(kept_inline)
+    z = load_golden("tcpopt")
+    for i, h0 in enumerate(z["hdrs"]):
+        h = np.ascontiguousarray(h0).copy()
+        p = h.ctypes.data_as(ctypes.c_void_p)
+        mss, ts, te = ctypes.c_uint16(), ctypes.c_uint32(), ctypes.c_uint32()
+        got = L.kept_tcp_parse_options(p, ctypes.byref(mss), ctypes.byref(ts), ctypes.byref(te))
+        assert [got, mss.value, ts.value, te.value] == list(z["parse"][i]), i
+        if z["sackts"][i, 1]:                  # the reference returned on this input
+            assert L.kept_tcp_find_sack_ts(p) == z["sackts"][i, 0], i
+        sl, al = ctypes.c_uint32(), ctypes.c_int()
+        off = L.kept_tcp_find_sack(p, ctypes.byref(sl), ctypes.byref(al))
+        assert [off, sl.value, al.value] == list(z["sack"][i]), i
+        assert np.array_equal(h, h0)           # the walks never write
+
+
+def test_kept_tcp_option_rewrites_match_fixture(kept_inline):
+    L = _kept_tcpopt(kept_inline)
+    z = load_golden("tcpopt")
+    ran = 0
+    for i, h0 in enumerate(z["hdrs"]):
+        op, val, ok = (int(x) for x in z["ops"][i])
+        if not ok:                             # the reference never returns here
+            continue
+        h = np.ascontiguousarray(h0).copy()
+        L.kept_tcp_opt_op(h.ctypes.data_as(ctypes.c_void_p), op, val)
+        assert np.array_equal(h, z["after"][i]), (i, op)
+        ran += 1
+    assert ran > 2900
+
+
+def test_kept_tcp_option_api_vs_reference(kept_inline, reference_lib):
+    """Fresh headers (another seed) against live reference calls."""
+    L = _kept_tcpopt(kept_inline)
+    R = reference_lib.lib
+    hdrs = framegen.tcp_headers(2000, seed=0xBEE)
+    rng = np.random.default_rng(5)
+    for h0 in hdrs:
+        term, so, sl, _ = framegen.sack_ts_walk(h0)
+        a, b = h0.copy(), h0.copy()
+        pa, pb = a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p)
+        m1, m2 = ctypes.c_uint16(), ctypes.c_uint16()
+        t1, t2, e1, e2 = (ctypes.c_uint32() for _ in range(4))
+        assert L.kept_tcp_parse_options(pa, ctypes.byref(m1), ctypes.byref(t1),
+                                        ctypes.byref(e1)) == \
+            R.ref_tcp_parse_options(pb, ctypes.byref(m2), ctypes.byref(t2), ctypes.byref(e2))
+        assert (m1.value, t1.value, e1.value) == (m2.value, t2.value, e2.value)
+        if term:
+            assert L.kept_tcp_find_sack_ts(pa) == R.ref_tcp_find_sack_ts(pb)
+        for op in range(9):
+            if op in (2, 3, 4) and (not term or (op == 2 and so % 2 == 1 and sl >= 10)):
+                continue
+            v = int(rng.integers(0, 2 ** 32))
+            L.kept_tcp_opt_op(pa, op, v)
+            R.ref_tcp_opt_op(pb, op, v)
+            assert np.array_equal(a, b), op
+
+
+def test_kept_tcp_find_sack_ts_stops_where_reference_loops(kept_inline):
+    """A SACK option with length byte 0: the reference's walk never returns
+    (iphdr/iphdr.c:152-163 adds 0); the kept walk stops there with the SACK
+    option recorded."""
+    L = _kept_tcpopt(kept_inline)
+    h = np.zeros(80, np.uint8)
+    h[12] = 8 << 4                              # 32-byte header, 12 bytes of options
+    h[20:24] = [1, 1, 5, 0]
+    assert not framegen.sack_ts_walk(h)[0]
+    assert L.kept_tcp_find_sack_ts(h.ctypes.data_as(ctypes.c_void_p)) == 22 | (0 << 8)
