@@ -36,7 +36,17 @@ namespace {
 constexpr int WAVE = 64;
 constexpr int WPB = 4;            // waves per block (256 threads)
 constexpr int IMG_CHUNKS = 8;     // 16-byte chunks parked in LDS per frame
-constexpr int IMG_STRIDE = 144;   // LDS bytes per frame slot (9 x 16: no b128 bank conflicts)
+#ifndef PPTK_RX_IMG_STRIDE
+#define PPTK_RX_IMG_STRIDE 144
+#endif
+// LDS bytes per frame slot.  144 = 9 x 16: no b128 bank conflicts when a
+// team parks its chunks; an odd dword pitch (148) instead spreads the
+// per-frame phase's byte reads (every lane reading the same offset of its
+// own frame) over all banks, at the price of parking chunks as dwords:
+// measured equal (CMIX 2.717 vs 2.721 ms, C1500 4.161 vs 4.160 ms,
+// in-process A/B) -- the per-frame phase is hidden behind the streaming --
+// so 144 stays.
+constexpr int IMG_STRIDE = PPTK_RX_IMG_STRIDE;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -852,8 +862,17 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
         for (int s = 0; s < S; ++s) {
           if (s * T < IMGC + (int)(ALM >> 4)) {
             const int ci = s * T + j - c_img;      // image = 16-byte chunks from floor16(frame)
-            if (ci >= 0 && ci < IMGC)
-              *(LDS_AS u32x4 *)(img + 16 * ci) = cb.v[s];
+            if (ci >= 0 && ci < IMGC) {
+              if constexpr (IMG_STRIDE % 16 == 0) {
+                *(LDS_AS u32x4 *)(img + 16 * ci) = cb.v[s];
+              } else {
+                LDS_AS uint32_t *w = (LDS_AS uint32_t *)(img + 16 * ci);
+                w[0] = cb.v[s].x;
+                w[1] = cb.v[s].y;
+                w[2] = cb.v[s].z;
+                w[3] = cb.v[s].w;
+              }
+            }
           }
         }
         uint32_t acc = 0;
@@ -1049,7 +1068,8 @@ struct FieldWriter {
     for (int c = 0; c < SLOT / 16; ++c) {
       const int fo = 16 * c - m;                    // frame offset of the chunk
       if (fo >= 0 && fo + 16 <= (int)len) {
-        *(GLB_AS u32x4 *)(row + 16 * c) = ((const LDS_AS u32x4 *)img)[c];
+        const LDS_AS uint32_t *w = (const LDS_AS uint32_t *)img + 4 * c;
+        *(GLB_AS u32x4 *)(row + 16 * c) = (u32x4){w[0], w[1], w[2], w[3]};
       } else {
         uint32_t t = (uint32_t)(touched >> (16 * c)) & 0xffffu;
         while (t) {
@@ -1069,19 +1089,36 @@ struct FieldWriter {
 // come from global memory through the FrameView rare path.
 constexpr int RW_SLOT = 64;
 
+// Lane slots of the header kernels sit an odd number of dwords apart (slot
+// + 4 bytes): the per-frame parse reads the same frame offset in every
+// lane's slot, which at a 64- or 128-byte pitch falls into one or two LDS
+// banks (a 32- to 64-way conflict on every byte read: SQ_ACTIVE_INST_LDS
+// ~15x SQ_INSTS_LDS); at an odd dword pitch the lanes spread over all 32
+// banks.  The slots are then only 4-byte aligned, so chunks are parked and
+// read back as dwords.
+template <int SLOT>
+__device__ __forceinline__ void park_chunks(LDS_AS uint8_t *slot, const u32x4 *c0, int nch) {
+  LDS_AS uint32_t *w = (LDS_AS uint32_t *)slot;
+#pragma unroll
+  for (int c = 0; c < SLOT / 16; ++c) {
+    const u32x4 v = c0[min(c, nch - 1)];
+    w[4 * c] = v.x;
+    w[4 * c + 1] = v.y;
+    w[4 * c + 2] = v.z;
+    w[4 * c + 3] = v.w;
+  }
+}
+
 __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[256 * RW_SLOT];
-  LDS_AS uint8_t *slot = (LDS_AS uint8_t *)lds + threadIdx.x * RW_SLOT;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[256 * (RW_SLOT + 4)];
+  LDS_AS uint8_t *slot = (LDS_AS uint8_t *)lds + threadIdx.x * (RW_SLOT + 4);
   const uint64_t step = (uint64_t)gridDim.x * 256u;
   for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += step) {
     const uint64_t base = a.off ? a.off[i] : i * a.stride;
     const uint32_t len = a.len ? a.len[i] : a.fixed_len;
     const int m = (int)(base & 15);
     const int nch = max((m + (int)len + 15) >> 4, 1);
-    const u32x4 *c0 = (const u32x4 *)(a.frames + (base - (uint64_t)m));
-#pragma unroll
-    for (int c = 0; c < RW_SLOT / 16; ++c)
-      ((LDS_AS u32x4 *)slot)[c] = c0[min(c, nch - 1)];
+    park_chunks<RW_SLOT>(slot, (const u32x4 *)(a.frames + (base - (uint64_t)m)), nch);
     const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + base, m, RW_SLOT - m};
     const Parse p = parse_frame(v, len);
     uint32_t st = 0;
@@ -1154,18 +1191,15 @@ __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
 constexpr int MSS_SLOT = 128;
 
 __global__ __launch_bounds__(256) void rx_mss_kernel(RxKArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[256 * MSS_SLOT];
-  LDS_AS uint8_t *slot = (LDS_AS uint8_t *)lds + threadIdx.x * MSS_SLOT;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[256 * (MSS_SLOT + 4)];
+  LDS_AS uint8_t *slot = (LDS_AS uint8_t *)lds + threadIdx.x * (MSS_SLOT + 4);
   const uint64_t step = (uint64_t)gridDim.x * 256u;
   for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += step) {
     const uint64_t base = a.off ? a.off[i] : i * a.stride;
     const uint32_t len = a.len ? a.len[i] : a.fixed_len;
     const int m = (int)(base & 15);
     const int nch = max((m + (int)len + 15) >> 4, 1);
-    const u32x4 *c0 = (const u32x4 *)(a.frames + (base - (uint64_t)m));
-#pragma unroll
-    for (int c = 0; c < MSS_SLOT / 16; ++c)
-      ((LDS_AS u32x4 *)slot)[c] = c0[min(c, nch - 1)];
+    park_chunks<MSS_SLOT>(slot, (const u32x4 *)(a.frames + (base - (uint64_t)m)), nch);
     const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + base, m, MSS_SLOT - m};
     const Parse p = parse_frame(v, len);
     uint32_t st = 0;
