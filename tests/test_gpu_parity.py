@@ -403,3 +403,41 @@ def test_lane_kernel_large_batch(dev):
         assert (ctx.last_variant() == RX_L4) == lane
         d = diff_records(got.cpu().numpy().reshape(-1), want)
         assert not d, f"shift {shift}: {d}"
+
+
+@pytest.mark.parametrize("cfg", ["c64", "c1500"])
+def test_host_batch_worker_pool_large_chunks(cfg, dev):
+    """Chunks big enough that the worker pool splits both the frame gather
+    and the record copy-out (>= 2 MiB of records per chunk), over repeated
+    calls on one context and then from two contexts on two host threads at
+    once: every record equals the device-resident path's."""
+    import threading
+    from pptk_amd.rx import RxContext, ldp_packets
+    from tools.synth import make_batch
+    n = 200_000 if cfg == "c64" else 70_000
+    b = make_batch(cfg, n, dev)
+    stride = b["stride"]
+    ring = b["frames"][: n * stride + 64].cpu().numpy()
+    ref = RxContext(0, bytes(range(1, 17))).batch_device(b["frames"], n, stride=stride,
+                                                         fixed_len=b["fixed_len"])
+    want = ref.cpu().numpy().reshape(-1).view(np.uint8).reshape(n, 64)
+    pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
+                       np.full(n, b["fixed_len"], np.uint16))
+    ctxs = [RxContext(0, bytes(range(1, 17)), max_batch=65536, max_frame=1518,
+                      gather_threads=8) for _ in range(2)]
+    for _ in range(2):
+        got = ctxs[0].batch_host(pkts)
+        assert np.array_equal(got.view(np.uint8).reshape(n, 64), want)
+    out = [None, None]
+
+    def run(k):
+        out[k] = ctxs[k].batch_host(pkts)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for k in range(2):
+        assert np.array_equal(out[k].view(np.uint8).reshape(n, 64), want)
+        ctxs[k].close()
