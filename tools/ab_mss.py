@@ -26,7 +26,7 @@ def main():
         for k, p in libs.items():
             ctx = RxContext(0, bench.KEY, lib_path=p)
             r = bench.mss_bench(ctx, n, dev, 10, 2)
-            assert r["clamped_every_frame"]
+            assert r["clamped_every_frame"] or k.startswith("d")   # d*: diagnostic builds
             res[k].append(r["kernel_ms"])
             ctx.close()
     print(json.dumps({k or "current": sorted(v)[len(v) // 2] for k, v in res.items()}))
