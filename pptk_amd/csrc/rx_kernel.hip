@@ -462,8 +462,9 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
 // values txv[k], network byte order.  Each field is a 2-byte write into a
 // line this wave read long before, so every field costs the memory a whole
 // write granule; writing 16/32/64-byte granules around the fields from the
-// patched LDS image instead was measured no faster, so plain
-// byte stores it is.
+// patched LDS image instead was measured no faster, nor were
+// 16-bit stores of the aligned fields (C1500 5.329 vs 5.327 ms, CMIX 3.008
+// vs 3.004 ms, tools/ab_tx.py), so plain byte stores it is.
 __device__ __forceinline__ void tx_store(const RxKArgs &a, uint64_t base, const int txp[2],
                                          const uint32_t txv[2]) {
 #pragma unroll
