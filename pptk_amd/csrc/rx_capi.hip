@@ -47,16 +47,14 @@ struct RxSlot {
 class WorkerPool {
  public:
   explicit WorkerPool(size_t nworkers) {
-    for (size_t t = 0; t < nworkers; ++t) th_.emplace_back([this] { loop(); });
-  }
-  ~WorkerPool() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
+    try {
+      for (size_t t = 0; t < nworkers; ++t) th_.emplace_back([this] { loop(); });
+    } catch (...) {   // a thread could not be started: stop the others
+      shutdown();
+      throw;
     }
-    cv_.notify_all();
-    for (std::thread &t : th_) t.join();
   }
+  ~WorkerPool() { shutdown(); }
   size_t size() const { return th_.size() + 1; }
   void parallel_for(size_t n, const std::function<void(size_t)> &f) {
     if (n == 0) return;
@@ -96,6 +94,15 @@ class WorkerPool {
       }
       work();
     }
+  }
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread &t : th_) t.join();
+    th_.clear();
   }
   std::vector<std::thread> th_;
   std::mutex mu_;
@@ -539,10 +546,18 @@ static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {
   return 0;
 }
 
-// The context's worker pool (nullptr with gather_threads <= 1).
+// The context's worker pool (nullptr with gather_threads <= 1).  If the
+// threads cannot be started the batch runs on the calling thread alone (and
+// later batches try again): no exception leaves the C ABI.
 static WorkerPool *pool_of(pptk_rx_ctx *c) {
   const size_t nth = std::max<size_t>(1, std::min<size_t>(c->opts.gather_threads, 64));
-  if (nth > 1 && !c->pool) c->pool = new (std::nothrow) WorkerPool(nth - 1);
+  if (nth > 1 && !c->pool) {
+    try {
+      c->pool = new WorkerPool(nth - 1);
+    } catch (...) {
+      c->pool = nullptr;
+    }
+  }
   return c->pool;
 }
 
