@@ -34,6 +34,11 @@ struct RxSlot {
   uint64_t *h_off = nullptr, *d_off = nullptr;
   uint16_t *h_len = nullptr, *d_len = nullptr;
   pptk_rx_rec *h_recs = nullptr, *d_recs = nullptr;
+  // device addresses of the pinned h_* buffers (direct small chunks)
+  uint8_t *hd_frames = nullptr;
+  uint64_t *hd_off = nullptr;
+  uint16_t *hd_len = nullptr;
+  pptk_rx_rec *hd_recs = nullptr;
   pptk_rx_rec *out = nullptr;   // caller's records of the chunk in flight
   size_t count = 0;
   bool busy = false;
@@ -541,9 +546,32 @@ static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {
     free_slot(sl);
     return -ENOMEM;
   }
+  if (hipHostGetDevicePointer((void **)&sl.hd_frames, sl.h_frames, 0) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&sl.hd_off, sl.h_off, 0) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&sl.hd_len, sl.h_len, 0) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&sl.hd_recs, sl.h_recs, 0) != hipSuccess) {
+    free_slot(sl);
+    return -EIO;
+  }
   sl.cap_pkts = pkts;
   sl.cap_bytes = bytes;
   return 0;
+}
+
+// Chunks of at most this many frames run "direct": the kernel reads the
+// descriptors and frames from the pinned staging buffers and writes the
+// records into pinned memory over PCIe, so a chunk costs one kernel launch
+// instead of three host-to-device copies, the launch and a device-to-host
+// copy -- the fixed cost that dominates LDP-sized batches of 32 - 4096
+// frames.  Larger chunks are copied (PCIe reads by the kernel are slower
+// than DMA for bulk data).  PPTK_RX_DIRECT_MAX overrides (A/B knob).
+static size_t direct_max() {
+  static long v = -2;
+  if (v == -2) {
+    const char *e = getenv("PPTK_RX_DIRECT_MAX");
+    v = e ? atol(e) : 4096;
+  }
+  return v < 0 ? 0 : (size_t)v;
 }
 
 // The context's worker pool (nullptr with gather_threads <= 1).  If the
@@ -582,6 +610,8 @@ static void copy_out(WorkerPool *pool, void *dst, const void *src, size_t n) {
 static int retire(RxSlot &sl, WorkerPool *pool) {
   if (!sl.busy) return 0;
   sl.busy = false;
+  // (HIP spins before it blocks: polling hipEventQuery instead measured
+  // equal on 32-frame chunks)
   if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
   copy_out(pool, sl.out, sl.h_recs, sl.count * 64);
   return 0;
@@ -688,23 +718,26 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
       }
     }
     hipStream_t s = sl.stream;
-    if ((!ring && hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
-                                 hipMemcpyHostToDevice, s) != hipSuccess) ||
-        hipMemcpyAsync(sl.d_off, sl.h_off, cnt * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(sl.d_len, sl.h_len, cnt * 2, hipMemcpyHostToDevice, s) != hipSuccess) {
+    const bool direct = cnt <= direct_max();
+    if (!direct &&
+        ((!ring && hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
+                                  hipMemcpyHostToDevice, s) != hipSuccess) ||
+         hipMemcpyAsync(sl.d_off, sl.h_off, cnt * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+         hipMemcpyAsync(sl.d_len, sl.h_len, cnt * 2, hipMemcpyHostToDevice, s) != hipSuccess)) {
       rc = -EIO;
       break;
     }
     pptk_rx_dev_batch b;
     memset(&b, 0, sizeof(b));
-    b.d_frames = ring ? ring->dev : sl.d_frames;
-    b.d_off = sl.d_off;
-    b.d_len = sl.d_len;
+    b.d_frames = ring ? ring->dev : direct ? sl.hd_frames : sl.d_frames;
+    b.d_off = direct ? sl.hd_off : sl.d_off;
+    b.d_len = direct ? sl.hd_len : sl.d_len;
     b.max_len = maxlen;
     b.n = cnt;
-    b.d_recs = sl.d_recs;
+    b.d_recs = direct ? sl.hd_recs : sl.d_recs;
     if ((rc = pptk_rx_batch_device(c, &b, s)) != 0) break;
-    if (hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if ((!direct && hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
+                        hipSuccess) ||
         hipEventRecord(sl.done, s) != hipSuccess) {
       rc = -EIO;
       break;

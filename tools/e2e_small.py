@@ -1,0 +1,56 @@
+"""BENCH TOOLING: latency of pptk_rx_batch for small LDP-sized batches (the
+rx loop hands out 32 - 4096 frames per ldp_in_nextpkts call): median
+microseconds per call and the frame rate, staged and zero-copy ring.
+
+    python tools/e2e_small.py [cfg]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from pptk_amd.records import diff_records
+    from pptk_amd.rx import RxContext, ldp_packets
+    from tools.synth import make_batch
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c64"
+    dev = torch.device("cuda", 0)
+    nmax = 4096
+    b = make_batch(cfg, nmax, dev)
+    stride = b["stride"]
+    ring = b["frames"][: nmax * stride + 64].cpu().numpy()
+    want = RxContext(0, bytes(range(1, 17))).batch_device(
+        b["frames"], nmax, stride=stride, fixed_len=b["fixed_len"]).cpu().numpy()
+    out = {"cfg": cfg}
+    for mode in ("staged", "ring"):
+        ctx = RxContext(0, bytes(range(1, 17)), max_batch=nmax, max_frame=1518,
+                        gather_threads=int(os.environ.get("E2E_GATHER_THREADS", "1")))
+        if mode == "ring":
+            ctx.register_ring(ring)
+        for n in (32, 256, 1024, 4096):
+            pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
+                               np.full(n, b["fixed_len"], np.uint16))
+            got = ctx.batch_host(pkts)
+            assert not diff_records(got, want[:n]), (mode, n)
+            ts = []
+            for _ in range(300):
+                t0 = time.perf_counter()
+                ctx.batch_host(pkts)
+                ts.append(time.perf_counter() - t0)
+            us = float(np.median(ts)) * 1e6
+            out[f"{mode}_{n}"] = {"us_per_call": round(us, 1), "mpkts": round(n / us, 2)}
+        if mode == "ring":
+            ctx.unregister_ring(ring)
+        ctx.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
