@@ -558,18 +558,19 @@ static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {
   return 0;
 }
 
-// Chunks of at most this many frames run "direct": the kernel reads the
-// descriptors and frames from the pinned staging buffers and writes the
-// records into pinned memory over PCIe, so a chunk costs one kernel launch
-// instead of three host-to-device copies, the launch and a device-to-host
-// copy -- the fixed cost that dominates LDP-sized batches of 32 - 4096
-// frames.  Larger chunks are copied (PCIe reads by the kernel are slower
-// than DMA for bulk data).  PPTK_RX_DIRECT_MAX overrides (A/B knob).
-static size_t direct_max() {
+// Chunks run "direct" -- the kernel reads the descriptors (and staged
+// frames) from the pinned staging buffers and writes the records into
+// pinned memory over PCIe: one kernel launch per chunk instead of three
+// host-to-device copies, the launch and a device-to-host copy -- when the
+// frames come from a registered ring (the kernel reads them over PCIe
+// anyway) or the staged frame bytes are at most this many (8 MiB: above
+// it the DMA copy of bulky frames beats the kernel's PCIe reads; measured,
+// DESIGN.md "Small LDP-sized batches").  PPTK_RX_DIRECT_MAX_BYTES overrides.
+static size_t direct_max_bytes() {
   static long v = -2;
   if (v == -2) {
-    const char *e = getenv("PPTK_RX_DIRECT_MAX");
-    v = e ? atol(e) : 4096;
+    const char *e = getenv("PPTK_RX_DIRECT_MAX_BYTES");
+    v = e ? atol(e) : 8l << 20;
   }
   return v < 0 ? 0 : (size_t)v;
 }
@@ -718,7 +719,7 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
       }
     }
     hipStream_t s = sl.stream;
-    const bool direct = cnt <= direct_max();
+    const bool direct = ring ? direct_max_bytes() > 0 : pos <= direct_max_bytes();
     if (!direct &&
         ((!ring && hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
                                   hipMemcpyHostToDevice, s) != hipSuccess) ||
