@@ -11,7 +11,8 @@ CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wextra -Iinclude
 LIB := pptk_amd/libpptkrx.so
 HIP_SRCS := pptk_amd/csrc/rx_kernel.hip pptk_amd/csrc/rx_bin.hip pptk_amd/csrc/rx_permit.hip \
             pptk_amd/csrc/rx_capi.hip
-C_SRCS := pptk_amd/csrc/host/ipcksum.c pptk_amd/csrc/host/hashseed.c pptk_amd/csrc/host/tcpopt.c
+C_SRCS := pptk_amd/csrc/host/ipcksum.c pptk_amd/csrc/host/hashseed.c pptk_amd/csrc/host/tcpopt.c \
+          pptk_amd/csrc/host/iphash.c pptk_amd/csrc/host/timerlink.c
 HDRS := $(wildcard include/*.h) pptk_amd/csrc/rx_internal.h
 HIP_OBJS := $(patsubst pptk_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 C_OBJS := $(patsubst pptk_amd/csrc/host/%.c,$(OBJDIR)/host/%.o,$(C_SRCS))

@@ -1,0 +1,83 @@
+/*
+ * timerlink.h -- the timer heap that ip_hash_init() registers its refill
+ * timers in (include/iphash.h).
+ *
+ * Same types, names and behaviour as the reference's
+ * timerlinkheap/timerlink.h: struct timer_link (expiry time, callback,
+ * userdata, tree links) and struct timer_linkheap (root = the earliest
+ * timer, size), TIMER_LINKHEAP_INITER, init/free, next_expiry_time/timer,
+ * add/remove/modify.  The implementation (pptk_amd/csrc/host/timerlink.c) is
+ * a skew heap on the same three links, not the reference's complete binary
+ * tree: only the root is specified (the earliest timer), so an application
+ * loop -- "while next_expiry_time(heap) <= now: take the root, remove it,
+ * call its fn" -- behaves the same.  Timers with equal expiry times may fire
+ * in another order than in the reference.
+ */
+#ifndef _TIMERLINK_H_
+#define _TIMERLINK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct timer_linkheap;
+struct timer_link;
+
+typedef void (*timer_link_fn)(struct timer_link *timer, struct timer_linkheap *heap,
+                              void *userdata, void *threaddata);
+
+struct timer_link {
+  uint64_t time64;
+  timer_link_fn fn;
+  void *userdata;
+  struct timer_link *parent;
+  struct timer_link *left;
+  struct timer_link *right;
+};
+
+struct timer_linkheap {
+  struct timer_link *root;
+  size_t size;
+};
+
+#define TIMER_LINKHEAP_INITER { .root = NULL, .size = 0 }
+
+static inline void timer_linkheap_init(struct timer_linkheap *heap)
+{
+  heap->root = NULL;
+  heap->size = 0;
+}
+
+/* the reference aborts when timers are left in a heap being freed */
+static inline void timer_linkheap_free(struct timer_linkheap *heap)
+{
+  if (heap->root != NULL || heap->size != 0)
+    abort();
+}
+
+static inline uint64_t timer_linkheap_next_expiry_time(struct timer_linkheap *heap)
+{
+  return heap->root ? heap->root->time64 : UINT64_MAX;
+}
+
+static inline struct timer_link *timer_linkheap_next_expiry_timer(struct timer_linkheap *heap)
+{
+  return heap->root;
+}
+
+void timer_linkheap_add(struct timer_linkheap *heap, struct timer_link *timer);
+void timer_linkheap_remove(struct timer_linkheap *heap, struct timer_link *timer);
+/* after changing timer->time64 of a timer in the heap */
+void timer_linkheap_modify(struct timer_linkheap *heap, struct timer_link *timer);
+/* 1 if the links, the heap order and the size are consistent */
+int timer_linkheap_verify(struct timer_linkheap *heap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

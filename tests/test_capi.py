@@ -347,3 +347,133 @@ def test_kept_tcp_find_sack_ts_stops_where_reference_loops(kept_inline):
     h[20:24] = [1, 1, 5, 0]
     assert not framegen.sack_ts_walk(h)[0]
     assert L.kept_tcp_find_sack_ts(h.ctypes.data_as(ctypes.c_void_p)) == 22 | (0 << 8)
+
+
+# ---- kept rate limiter (include/iphash.h) and timer heap (include/timerlink.h)
+def _build_iphash_harness(out, reference=False):
+    """tests/c/iphash_scenario.c against the kept API (include/ +
+    libpptkrx.so) or, reference=True, against the reference's own headers and
+    objects in oracle/_ref (built from /root/reference)."""
+    src = os.path.join(ROOT, "tests", "c", "iphash_scenario.c")
+    if not reference:
+        libdir = os.path.join(ROOT, "pptk_amd")
+        cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-Werror", "-fPIC", "-shared", "-I", INCLUDE,
+               src, "-L", libdir, "-lpptkrx", f"-Wl,-rpath,{libdir}", "-o", out]
+    else:
+        from oracle.oracle import REF_SO
+        ref, obj = "/root/reference", os.path.join(os.path.dirname(REF_SO), "obj")
+        incs = [f"-I{ref}/{d}" for d in ("iphash", "timerlinkheap", "misc", "hashtable", "log",
+                                           "hashlist", "linkedlist")]
+        objs = [os.path.join(obj, p) for p in ("iphash/iphash.o", "timerlinkheap/timerlink.o",
+                                               "misc/hashseed.o", "log/log.o")]
+        cmd = ["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", *incs, src, *objs, "-pthread",
+               "-o", out]
+    subprocess.check_call(cmd)
+    L = ctypes.CDLL(out)
+    vp, u32, u8, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_size_t
+    L.iphash_scenario.restype = u32
+    L.iphash_scenario.argtypes = [vp, ctypes.c_int, u8, vp, vp, sz, u32, u32, u32, u32, u32, sz,
+                                  vp, vp]
+    L.iphash_permit_seq.restype = None
+    L.iphash_permit_seq.argtypes = [vp, ctypes.c_int, u8, vp, vp, vp, sz, u32, u32, vp, vp, vp]
+    L.timer_heap_exercise.restype = ctypes.c_long
+    L.timer_heap_exercise.argtypes = [ctypes.c_uint64, sz, sz, vp, sz]
+    return L
+
+
+@pytest.fixture(scope="module")
+def iphash_kept(tmp_path_factory):
+    return _build_iphash_harness(str(tmp_path_factory.mktemp("iph") / "kept.so"))
+
+
+@pytest.fixture(scope="module")
+def iphash_ref(tmp_path_factory):
+    from oracle.oracle import REF_SO
+    if not os.path.exists(REF_SO) or not os.path.isdir("/root/reference/iphash"):
+        pytest.skip("reference tree / oracle/_ref absent")
+    return _build_iphash_harness(str(tmp_path_factory.mktemp("iphr") / "ref.so"), True)
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _sources(recs):
+    from pptk_amd.records import F_IPV6, F_PARSED, as_records
+    r = as_records(recs)
+    src4 = np.ascontiguousarray(r["src"][:, :4].astype(np.uint32) @ np.array([1 << 24, 1 << 16, 1 << 8, 1],
+                                                                               np.uint32))
+    src6 = np.ascontiguousarray(r["src"])
+    parsed = (r["flags"] & F_PARSED) != 0
+    v6 = (r["flags"] & F_IPV6) != 0
+    return src4.astype(np.uint32), src6, parsed, v6
+
+
+def test_kept_iphash_matches_permit_fixture(iphash_kept):
+    """ip_permitted / ipv6_permitted of the kept API, once per frame in frame
+    order, give the reference's verdicts and token arrays
+    (tests/golden/permit.npz, made with the reference's own functions)."""
+    z = load_golden("permit")
+    bits4, bits6, hs = (int(x) for x in z["iphash"])
+    src4, src6, parsed, v6 = _sources(z["recs"])
+    key = np.ascontiguousarray(z["key"])
+    for k, (fam, init, has_subj) in enumerate(z["case_meta"]):
+        use = (parsed & (v6 == (fam == 6))).astype(np.uint8)
+        if has_subj:
+            use &= z["case_subject"][k].astype(np.uint8)
+        verdict = np.zeros(len(use), np.uint8)
+        tok_in = np.ascontiguousarray(z["case_tok_in"][k].astype(np.uint32))
+        tok = np.zeros(hs, np.uint32)
+        iphash_kept.iphash_permit_seq(_p(key), int(fam), bits4 if fam == 4 else bits6, _p(src4),
+                                      _p(src6), _p(use), len(use), hs, int(init), _p(tok_in),
+                                      _p(verdict), _p(tok))
+        assert np.array_equal(verdict, z["case_verdict"][k]), (fam, init)
+        assert np.array_equal(tok, z["case_tok_out"][k]), (fam, init)
+
+
+@pytest.mark.parametrize("family,bits", [(4, 24), (4, 32), (6, 48), (6, 128)])
+@pytest.mark.parametrize("initial", [3, 200, 1000, 70000])
+def test_kept_iphash_timer_scenario_vs_reference(iphash_kept, iphash_ref, family, bits, initial):
+    """The same timer-driven scenario (permits, give-backs, refill timers
+    fired from the heap by a virtual clock) against the reference build:
+    verdicts, final tokens and the number of timer firings agree."""
+    rng = np.random.default_rng(family * 1000 + bits + initial)
+    n = 20000
+    prefixes = rng.integers(0, 2 ** 32, 5, dtype=np.uint64).astype(np.uint32)
+    src4 = np.ascontiguousarray(prefixes[rng.integers(0, 5, n)] ^
+                                rng.integers(0, 256, n).astype(np.uint32))
+    src6 = np.ascontiguousarray(rng.integers(0, 256, (n, 16), dtype=np.uint8))
+    src6[:, :6] = rng.integers(0, 256, (5, 6), dtype=np.uint8)[rng.integers(0, 5, n)]
+    key = np.arange(1, 17, dtype=np.uint8)
+    out = []
+    for L in (iphash_kept, iphash_ref):
+        verdict = np.zeros(n, np.uint8)
+        tok = np.zeros(256, np.uint32)
+        fired = L.iphash_scenario(_p(key), family, bits, _p(src4), _p(src6), n, 256, 32, initial,
+                                  max(1, initial // 4), 9000, 500, _p(verdict), _p(tok))
+        out.append((verdict, tok, fired))
+    assert out[0][2] == out[1][2] and out[0][2] > 8
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert (out[0][0] == 1).any()
+    if initial <= 200 and bits not in (32, 128):    # prefixes share buckets: demand outruns refills
+        assert (out[0][0] == 0).any()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_kept_timer_heap(iphash_kept, seed):
+    """Random add / modify / remove sequences: pops come out in time order
+    and every timer left in the heap comes out."""
+    outs = np.zeros(5000, np.uint64)
+    n = iphash_kept.timer_heap_exercise(seed, 4000, 200000, _p(outs), len(outs))
+    assert n > 1000
+    assert np.all(np.diff(outs[:min(n, len(outs))].astype(np.int64)) >= 0)
+
+
+def test_kept_timer_heap_same_pops_as_reference(iphash_kept, iphash_ref):
+    """The same operation sequence on the reference's heap pops the same
+    multiset of times in the same (non-decreasing) order."""
+    a, b = np.zeros(5000, np.uint64), np.zeros(5000, np.uint64)
+    na = iphash_kept.timer_heap_exercise(7, 3000, 100000, _p(a), len(a))
+    nb = iphash_ref.timer_heap_exercise(7, 3000, 100000, _p(b), len(b))
+    assert na == nb and np.array_equal(a, b)
