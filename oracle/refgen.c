@@ -19,6 +19,12 @@
  *   ip_permitted, ipv6_permitted                   (iphash/iphash.c)
  *   ip_update_cksum16/32, ip_decr_ttl_cksum_update, ip_set_src/dst_cksum_update,
  *   tcp/udp_set_src/dst_port_cksum_update, ip_ttl   (iphdr/ipcksum.h, iphdr.h)
+ *   tcp_parse_options, tcp_find_sack_ts_headers, tcp_find_sack_header,
+ *   tcp_syn, tcp_data_offset                       (iphdr/iphdr.c, iphdr.h)
+ *   tcp_set_mss_cksum_update, tcp_disable_sack_cksum_update,
+ *   tcp_adjust_sack_cksum_update_2, tcp_adjust_tsval/tsecho_cksum_update,
+ *   tcp_set_ack_off_cksum_update, tcp_set_seq/ack_number_cksum_update,
+ *   tcp_set_window_cksum_update                    (iphdr/ipcksum.h)
  */
 #include <pthread.h>
 #include <stdint.h>
