@@ -4,9 +4,10 @@
  *
  * Same types, names and behaviour as the reference's
  * timerlinkheap/timerlink.h: struct timer_link (expiry time, callback,
- * userdata, tree links) and struct timer_linkheap (root = the earliest
- * timer, size), TIMER_LINKHEAP_INITER, init/free, next_expiry_time/timer,
- * add/remove/modify.  The implementation (pptk_amd/csrc/host/timerlink.c) is
+ * userdata, tree links; :14-24) and struct timer_linkheap (root = the
+ * earliest timer, size; :26-29), TIMER_LINKHEAP_INITER (:39-42),
+ * init/free (:62-78), next_expiry_time/timer (:44-60), add/remove/modify
+ * (:80-84), verify (:35).  The implementation (pptk_amd/csrc/host/timerlink.c) is
  * a skew heap on the same three links, not the reference's complete binary
  * tree: only the root is specified (the earliest timer), so an application
  * loop -- "while next_expiry_time(heap) <= now: take the root, remove it,
