@@ -464,7 +464,8 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
 // write granule; writing 16/32/64-byte granules around the fields from the
 // patched LDS image instead was measured no faster, nor were
 // 16-bit stores of the aligned fields (C1500 5.329 vs 5.327 ms, CMIX 3.008
-// vs 3.004 ms, tools/ab_tx.py), so plain byte stores it is.
+// vs 3.004 ms, tools/ab_tx.py), and non-temporal 16-bit stores were much
+// slower (5.90 vs 5.36 ms, 3.63 vs 3.13 ms), so plain byte stores it is.
 __device__ __forceinline__ void tx_store(const RxKArgs &a, uint64_t base, const int txp[2],
                                          const uint32_t txv[2]) {
 #pragma unroll
