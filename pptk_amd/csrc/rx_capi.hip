@@ -288,7 +288,19 @@ static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n) {
     const char *e = getenv("PPTK_RX_GRID_MULT");
     grid_mult = e ? std::max(1, atoi(e)) : 1;
   }
-  const uint64_t cap = (uint64_t)c->ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
+  // PPTK_RX_RESERVE_CUS: leave that many CUs' worth of resident blocks
+  // free, so a concurrent kernel (an RCCL collective overlapping the batch)
+  // finds room on the chip instead of waiting for the persistent grid.
+  static int reserve = -1;
+  if (reserve < 0) {
+    const char *e = getenv("PPTK_RX_RESERVE_CUS");
+#ifndef PPTK_RX_RESERVE_DEFAULT
+#define PPTK_RX_RESERVE_DEFAULT 0
+#endif
+    reserve = e ? std::max(0, atoi(e)) : PPTK_RX_RESERVE_DEFAULT;
+  }
+  const uint64_t ncu = (uint64_t)std::max(1, c->ncu - std::min(reserve, c->ncu - 1));
+  const uint64_t cap = ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, cap));
 }
 
