@@ -1069,6 +1069,9 @@ struct FieldWriter {
 #pragma unroll
     for (int c = 0; c < SLOT / 16; ++c) {
       const int fo = 16 * c - m;                    // frame offset of the chunk
+      // only chunks holding a changed byte (writing back the untouched ones
+      // as well cost C64 0.526 vs 0.463 ms, C1500 1.300 vs 1.220 ms)
+      if (!((touched >> (16 * c)) & 0xffffu)) continue;
       if (fo >= 0 && fo + 16 <= (int)len) {
         const LDS_AS uint32_t *w = (const LDS_AS uint32_t *)img + 4 * c;
         *(GLB_AS u32x4 *)(row + 16 * c) = (u32x4){w[0], w[1], w[2], w[3]};
