@@ -441,3 +441,32 @@ def test_host_batch_worker_pool_large_chunks(cfg, dev):
     for k in range(2):
         assert np.array_equal(out[k].view(np.uint8).reshape(n, 64), want)
         ctxs[k].close()
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_large_fresh_batches_vs_oracle(seed, oracle_lib, dev):
+    """Fresh seeds, not in any fixture: 60 K fuzzed frames (malformed,
+    truncated, odd lengths, extension chains, jumbo) and 60 K CMIX frames,
+    interleaved in one batch and packed at an odd alignment, through the
+    default variant and the compact records: bit-exact against the CPU
+    restatement (itself pinned to the reference by the golden fixtures)."""
+    import framegen
+    from oracle.oracle import make_opts
+    fb, fo, fl = framegen.gen_fuzz(60000, seed=0x7100 + seed)
+    cb, co, cl = framegen.gen_cmix(60000, seed=0x7200 + seed)
+    frames = []
+    for k in range(60000):
+        frames.append(fb[int(fo[k]):int(fo[k]) + int(fl[k])].tobytes())
+        frames.append(cb[int(co[k]):int(co[k]) + int(cl[k])].tobytes())
+    buf, off, lens = framegen.pack(frames, align=1 + 2 * seed)
+    key = bytes(range(3, 19))
+    z = {"buf": buf, "off": off, "len": lens, "key": np.frombuffer(key, np.uint8),
+         "iphash": np.array([22, 56, 1 << 14])}
+    want = oracle_lib.rx_batch(buf, off, lens, opts=make_opts(key, 22, 56, 1 << 14), nthreads=8)
+    ctx = _ctx(z)
+    got = _run(ctx, z, dev, shift=3)
+    d = diff_records(got, want)
+    assert not d, d
+    got32 = _run(ctx, z, dev, shift=3, compact=True)
+    d = diff_records(got32, to_rec32(want), dtype=REC32_DTYPE)
+    assert not d, d
