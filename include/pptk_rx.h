@@ -218,12 +218,16 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint6
  *   PPTK_RW_DST       ip_set_dst_cksum_update(dst)      (:349-372)
  *   PPTK_RW_SPORT     tcp/udp_set_src_port_cksum_update (:263-271, :323-334)
  *   PPTK_RW_DPORT     tcp/udp_set_dst_port_cksum_update (:273-281, :336-347)
+ *   PPTK_RW_ICMP_ID   icmp_set_echo_identifier_cksum_update (:283-291), with
+ *                     the new identifier in `sport`
  * each computing the new checksum from the old one with ip_update_cksum16/32
  * (:213-236), results identical to calling those functions in that order.
  * Applies to every frame the receive transform parses as IPv4; the TCP/UDP
  * parts (the L4 checksum follow-up of an address change, the port writes)
  * only when its record has PPTK_RX_F_L4 (an L4 header, not a fragment), and
- * a UDP checksum of 0 stays 0 as in the reference.  A frame whose TTL is 0
+ * a UDP checksum of 0 stays 0 as in the reference; the ICMP identifier
+ * only on an echo request or reply (type 8 / 0) that is not a fragment and
+ * has its 8-byte header inside the packet.  A frame whose TTL is 0
  * under PPTK_RW_DECR_TTL (the reference abort()s) is left untouched.
  * Addresses and ports are host order, as the reference's setters take them.
  * d_rw holds rw_count = 1 (one rewrite for every frame) or n entries.
@@ -241,10 +245,12 @@ struct pptk_rewrite {
 #define PPTK_RW_DST 0x4u
 #define PPTK_RW_SPORT 0x8u
 #define PPTK_RW_DPORT 0x10u
+#define PPTK_RW_ICMP_ID 0x20u
 #define PPTK_RW_ST_IP 0x1u         /* parsed IPv4: the IP-level ops applied */
 #define PPTK_RW_ST_L4 0x2u         /* L4 header present: the L4 ops applied */
 #define PPTK_RW_ST_TTL_ZERO 0x4u   /* TTL was 0: frame left untouched      */
 #define PPTK_RW_ST_EXPIRED 0x8u    /* TTL reached 0 (reference returns 0)  */
+#define PPTK_RW_ST_ICMP 0x10u      /* ICMP echo: the identifier op applied  */
 int pptk_tx_rewrite_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint64_t *d_off,
                            const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
                            uint64_t n, const struct pptk_rewrite *d_rw, uint64_t rw_count,

@@ -550,6 +550,11 @@ void ref_rewrite_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, u
       else
         udp_set_dst_port_cksum_update(l4, r.l4_len, w->dport);
     }
+    if ((w->ops & PPTK_RW_ICMP_ID) && r.proto == 1 && !(r.flags & PPTK_RX_F_FRAGMENT) &&
+        r.l4_len >= 8 && (icmp_type(l4) == 8 || icmp_type(l4) == 0)) {
+      icmp_set_echo_identifier_cksum_update(l4, r.l4_len, w->sport);
+      st |= PPTK_RW_ST_ICMP;
+    }
 done:
     if (status)
       status[i] = st;

@@ -655,6 +655,14 @@ void orc_rewrite_batch(uint8_t *buf, const uint64_t *off, const uint16_t *len, u
       l4_port_update(l4, r.proto, 0, w->sport);
     if (l4ok && (w->ops & PPTK_RW_DPORT))
       l4_port_update(l4, r.proto, 2, w->dport);
+    /* icmp_set_echo_identifier_cksum_update (:283-291) on an echo request /
+     * reply with its 8-byte header inside the packet, not a fragment */
+    if ((w->ops & PPTK_RW_ICMP_ID) && r.proto == 1 && !(r.flags & PPTK_RX_F_FRAGMENT) &&
+        r.l4_len >= 8 && (l4[0] == 8 || l4[0] == 0)) {
+      put_be16(l4 + 2, orc_update_cksum16(be16_at(l4 + 2), be16_at(l4 + 4), w->sport));
+      put_be16(l4 + 4, w->sport);
+      st |= PPTK_RW_ST_ICMP;
+    }
 done:
     if (status)
       status[i] = st;

@@ -1174,6 +1174,18 @@ __global__ __launch_bounds__(256) void rx_rewrite_kernel(RxKArgs a) {
             fw.put(l4 + 2 * k, nw, 2);
           }
         }
+        if ((w.ops & PPTK_RW_ICMP_ID) && proto == 1 && !(p.flags & PPTK_RX_F_FRAGMENT) &&
+            p.re - p.rs >= 8u) {
+          // icmp_set_echo_identifier_cksum_update (:283-291) on an echo
+          // request / reply; the ICMP checksum has no pseudo-header, so the
+          // address changes above leave it alone
+          const uint32_t type = v.u8(l4);
+          if (type == 8 || type == 0) {
+            fw.put(l4 + 2, upd16(v.be16(l4 + 2), v.be16(l4 + 4), w.sport), 2);
+            fw.put(l4 + 4, w.sport, 2);
+            st |= PPTK_RW_ST_ICMP;
+          }
+        }
         if (w.ops & (PPTK_RW_DECR_TTL | PPTK_RW_SRC | PPTK_RW_DST))
           fw.put(l3 + 10, ipc, 2);
         if (l4c_w)

@@ -29,7 +29,8 @@ REWRITE_DTYPE = np.dtype([("ops", "<u4"), ("src", "<u4"), ("dst", "<u4"),
                           ("sport", "<u2"), ("dport", "<u2")])
 assert REWRITE_DTYPE.itemsize == 16
 RW_DECR_TTL, RW_SRC, RW_DST, RW_SPORT, RW_DPORT = 0x1, 0x2, 0x4, 0x8, 0x10
-RW_ST_IP, RW_ST_L4, RW_ST_TTL_ZERO, RW_ST_EXPIRED = 0x1, 0x2, 0x4, 0x8
+RW_ST_IP, RW_ST_L4, RW_ST_TTL_ZERO, RW_ST_EXPIRED, RW_ST_ICMP = 0x1, 0x2, 0x4, 0x8, 0x10
+RW_ICMP_ID = 0x20
 MSS_SYN_ONLY = 0x1
 MSS_ST_TCP, MSS_ST_FOUND, MSS_ST_CLAMPED, MSS_ST_BADOPT = 0x1, 0x2, 0x4, 0x8
 

@@ -11,7 +11,7 @@ uint16_t kept_update32(uint16_t c, uint32_t o, uint32_t n) { return (uint16_t)ip
 /* one frame: ops as pptk_rewrite (bit 0 ttl, 1 src, 2 dst, 3 sport, 4 dport)
  * applied with the kept inline functions; ip/l4 offsets and proto given */
 int kept_rewrite(uint8_t *f, int l3, int l4, int proto, int l4ok, uint32_t ops, uint32_t src,
-                 uint32_t dst, uint16_t sport, uint16_t dport)
+                 uint32_t dst, uint16_t sport, uint16_t dport, int l4len, int frag)
 {
   uint8_t *ip = f + l3, *p = f + l4;
   int alive = 1;
@@ -29,6 +29,9 @@ int kept_rewrite(uint8_t *f, int l3, int l4, int proto, int l4ok, uint32_t ops, 
     if (proto == 6) tcp_set_dst_port_cksum_update(p, 0, dport);
     else udp_set_dst_port_cksum_update(p, 0, dport);
   }
+  /* bit 5: ICMP echo identifier (the new id in sport) */
+  if ((ops & 32) && proto == 1 && !frag && l4len >= 8 && (icmp_type(p) == 8 || icmp_type(p) == 0))
+    icmp_set_echo_identifier_cksum_update(p, (uint16_t)l4len, sport);
   return alive;
 }
 

@@ -538,3 +538,53 @@ def tcp_headers(n=3000, seed=0x7C9, width=80):
         h += bytes(rng.integers(0, 256, width - len(h), dtype=np.uint8))
         out[i] = np.frombuffer(bytes(h[:width]), np.uint8)
     return out
+
+
+# ------------------------------------------------------------ ICMP
+def frame_icmp4(rng, icmp_type=8, payload_len=None, vlan=None, ihl_words=5, mf=False,
+                frag_off=0, l4_len=None):
+    """IPv4/ICMP frame (valid checksums): echo request/reply by default,
+    identifier and sequence random; l4_len truncates the ICMP message
+    (< 8 bytes: a short header)."""
+    pl = int(rng.integers(0, 64)) if payload_len is None else payload_len
+    ident, seq = (int(x) for x in rng.integers(0, 65536, 2))
+    msg = bytearray(struct.pack(">BBHHH", icmp_type, 0, 0, ident, seq) +
+                    bytes(rng.integers(0, 256, pl, dtype=np.uint8)))
+    if l4_len is not None:
+        msg = msg[:l4_len]
+    if len(msg) >= 4:
+        msg[2:4] = b"\0\0"
+        struct.pack_into(">H", msg, 2, csum(bytes(msg)))
+    src = bytes([10]) + bytes(rng.integers(0, 256, 3, dtype=np.uint8))
+    dst = bytes([192, 168]) + bytes(rng.integers(0, 256, 2, dtype=np.uint8))
+    opts = bytes(rng.integers(0, 256, (ihl_words - 5) * 4, dtype=np.uint8))
+    ip = ipv4_hdr(src, dst, 1, len(msg), opts, mf=mf, frag_off=frag_off,
+                  ident=int(rng.integers(0, 65536)))
+    return eth(ETH_IP, vlan) + ip + bytes(msg)
+
+
+def gen_icmp(n=1500, seed=0x1C3):
+    """ICMP fixture frames: echo request / reply (most), other types (3, 11,
+    13), short messages (< 8 bytes), fragments, IP options, VLAN tags, some
+    Ethernet padding, and TCP/UDP frames in between."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for _ in range(n):
+        c = int(rng.integers(0, 100))
+        vlan = int(rng.integers(1, 4095)) if rng.random() < 0.2 else None
+        ihl = 5 if rng.random() < 0.8 else int(rng.integers(6, 16))
+        if c < 60:
+            f = frame_icmp4(rng, int(rng.choice([0, 8])), vlan=vlan, ihl_words=ihl)
+        elif c < 70:
+            f = frame_icmp4(rng, int(rng.choice([3, 11, 13, 5])), vlan=vlan, ihl_words=ihl)
+        elif c < 76:
+            f = frame_icmp4(rng, 8, vlan=vlan, l4_len=int(rng.integers(0, 8)))
+        elif c < 82:
+            f = frame_icmp4(rng, 8, vlan=vlan, mf=rng.random() < 0.5,
+                            frag_off=int(rng.integers(0, 4)))
+        else:
+            f = frame_v4(rng, int(rng.choice([6, 17])), int(rng.integers(64, 200)), vlan=vlan)
+        if rng.random() < 0.1:
+            f = f + bytes(int(rng.integers(1, 20)))          # Ethernet padding
+        frames.append(f)
+    return pack(frames)

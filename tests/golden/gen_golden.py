@@ -61,6 +61,7 @@ SETS = {
     "c64": lambda: framegen.gen_c64(4096),
     "c1500": lambda: framegen.gen_c1500(1024),
     "cmix": lambda: framegen.gen_cmix(2048),
+    "icmp": lambda: framegen.gen_icmp(1500),
 }
 
 
@@ -161,10 +162,10 @@ def rewrite_inputs(z, rng):
     return buf
 
 
-def random_rewrites(n, rng):
+def random_rewrites(n, rng, nops=32):
     from pptk_amd.records import REWRITE_DTYPE
     rw = np.zeros(n, REWRITE_DTYPE)
-    rw["ops"] = rng.integers(0, 32, n)
+    rw["ops"] = rng.integers(0, nops, n)
     rw["src"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
     rw["dst"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
     rw["sport"] = rng.integers(0, 65536, n)
@@ -178,12 +179,14 @@ def gen_rewrite(ref):
     for c64 also one shared rewrite entry for every frame ("c64_one")."""
     rng = np.random.default_rng(0x5E7)
     out = {}
+    # (the ICMP case comes last, with the identifier op among the random
+    # ops, so the earlier cases' random streams are unchanged)
     cases = [("edge", "edge", None), ("fuzz", "fuzz", None), ("cmix", "cmix", None),
-             ("c64", "c64", None), ("c64_one", "c64", 1)]
+             ("c64", "c64", None), ("c64_one", "c64", 1), ("icmp", "icmp", None)]
     for tag, name, count in cases:
         z = dict(np.load(os.path.join(HERE, f"{name}.npz")))
         buf_in = rewrite_inputs(z, rng)
-        rw = random_rewrites(count or len(z["off"]), rng)
+        rw = random_rewrites(count or len(z["off"]), rng, 64 if tag == "icmp" else 32)
         if count == 1:
             rw["ops"] = 0x1F
         buf_out, status = ref.rewrite_batch(buf_in, rw, z["off"], z["len"])

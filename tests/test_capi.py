@@ -190,7 +190,8 @@ def kept_inline(tmp_path_factory):
     u16, u32, vp = ctypes.c_uint16, ctypes.c_uint32, ctypes.c_void_p
     L.kept_update16.argtypes, L.kept_update16.restype = [u16, u16, u16], u16
     L.kept_update32.argtypes, L.kept_update32.restype = [u16, u32, u32], u16
-    L.kept_rewrite.argtypes = [vp] + [ctypes.c_int] * 4 + [u32, u32, u32, u16, u16]
+    L.kept_rewrite.argtypes = [vp] + [ctypes.c_int] * 4 + [u32, u32, u32, u16, u16,
+                                                         ctypes.c_int, ctypes.c_int]
     L.kept_set_cksums.argtypes = [vp] + [ctypes.c_int] * 5 + [u16]
     L.kept_set_cksums.restype = None
     return L
@@ -212,12 +213,13 @@ def test_kept_update_helpers_vs_reference(kept_inline, reference_lib):
         assert kept_inline.kept_update16(c, a, b) == reference_lib.update_cksum16(c, a, b)
 
 
-@pytest.mark.parametrize("tag,name", [("edge", "edge"), ("fuzz", "fuzz"), ("cmix", "cmix")])
+@pytest.mark.parametrize("tag,name", [("edge", "edge"), ("fuzz", "fuzz"), ("cmix", "cmix"),
+                                      ("icmp", "icmp")])
 def test_kept_rewrite_functions_match_fixture(kept_inline, tag, name):
     """The kept per-frame *_cksum_update functions, applied frame by frame
     as pptk_tx_rewrite_device composes them, give the reference's bytes."""
     import ctypes
-    from pptk_amd.records import (F_L4, F_PARSED, RW_ST_TTL_ZERO, as_records)
+    from pptk_amd.records import (F_FRAGMENT, F_L4, F_PARSED, RW_ST_TTL_ZERO, as_records)
     from test_oracle import rewrite_case
     z, buf_in, buf_out, rw, status = rewrite_case(tag, name)
     recs = as_records(z["recs"])
@@ -231,7 +233,8 @@ def test_kept_rewrite_functions_match_fixture(kept_inline, tag, name):
         fr = (ctypes.c_uint8 * L).from_buffer(buf, int(o))
         kept_inline.kept_rewrite(fr, int(r["l3_off"]), int(r["l4_off"]), int(r["proto"]),
                                  int(bool(r["flags"] & F_L4)), int(w["ops"]), int(w["src"]),
-                                 int(w["dst"]), int(w["sport"]), int(w["dport"]))
+                                 int(w["dst"]), int(w["sport"]), int(w["dport"]),
+                                 int(r["l4_len"]), int(bool(r["flags"] & F_FRAGMENT)))
         assert r["flags"] & F_PARSED
         n_done += 1
     assert n_done > 50
