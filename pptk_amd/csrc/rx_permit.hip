@@ -19,7 +19,9 @@
 //      log2(hash_size) + 1 key bits;
 //   3. bucket bounds from the sorted keys: first[b] / end[b] = the sorted
 //      positions where bucket b's run starts / ends (0 / 0 when absent);
-//   4. verdict of the frame at sorted position p: p - first[b] < T_b;
+//   4. verdict of frame i in bucket b: permitted iff it is among the first
+//      T_b frames of b's run, i.e. i < lim[b] = (index of the T_b-th frame of
+//      the run) + 1 -- everything when the run is no longer than T_b;
 //   5. T_b -= min(T_b, end[b] - first[b]).
 // (Counting with atomics instead -- device-scope atomics on a 2^16-entry
 // array shared by all eight XCDs -- made step 1 take 0.72 of the batch's
@@ -77,13 +79,26 @@ __global__ __launch_bounds__(PT) void permit_bounds(PermitArgs a, const uint32_t
   if (p + 1 == a.n || skeys[p + 1] != b) end[b] = (uint32_t)(p + 1);
 }
 
-__global__ __launch_bounds__(PT) void permit_rank(PermitArgs a, const uint32_t *skeys,
-                                                  const uint32_t *svals, const uint32_t *first) {
-  const uint64_t p = (uint64_t)blockIdx.x * PT + threadIdx.x;
-  if (p >= a.n) return;
-  const uint32_t b = skeys[p];
-  if (b >= a.hash_size) return;       // non-subject (sorted last)
-  a.verdict[svals[p]] = (p - first[b]) < a.tokens[b] ? 1 : 0;
+// lim[b] per bucket: frames of b with index < lim[b] are permitted (the run
+// is in frame order: the sort is stable).
+__global__ __launch_bounds__(PT) void permit_limits(PermitArgs a, const uint32_t *svals,
+                                                    const uint32_t *first, const uint32_t *end,
+                                                    uint32_t *lim) {
+  const uint64_t b = (uint64_t)blockIdx.x * PT + threadIdx.x;
+  if (b >= a.hash_size) return;
+  const uint32_t t = a.tokens[b], c = end[b] - first[b];
+  lim[b] = c <= t ? 0xffffffffu : t == 0 ? 0u : svals[first[b] + t - 1] + 1u;
+}
+
+// Verdicts in frame order (coalesced stores; the sorted-order pass this
+// replaces scattered one byte per frame: 0.22 ms per 16 M frames).
+__global__ __launch_bounds__(PT) void permit_verdicts(PermitArgs a, const uint32_t *keys,
+                                                      const uint32_t *lim) {
+  const uint64_t i = (uint64_t)blockIdx.x * PT + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t b = keys[i];
+  if (b >= a.hash_size) return;       // non-subject: verdict 2 already
+  a.verdict[i] = (uint32_t)i < lim[b] ? 1 : 0;
 }
 
 __global__ __launch_bounds__(PT) void permit_consume(PermitArgs a, const uint32_t *first,
@@ -115,7 +130,7 @@ int key_bits(uint32_t hash_size) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct PermitScratch {
-  uint32_t *keys, *vals, *skeys, *svals, *first, *end;
+  uint32_t *keys, *vals, *skeys, *svals, *first, *end, *lim;
   void *tmp;
   size_t tmp_bytes, total;
 };
@@ -140,6 +155,7 @@ hipError_t layout(uint64_t n, uint32_t hash_size, void *base, PermitScratch &s) 
   s.svals = (uint32_t *)take(n * 4);
   s.first = (uint32_t *)take((size_t)hash_size * 8);   // first[hash_size], then end[]
   s.end = s.first ? s.first + hash_size : nullptr;
+  s.lim = (uint32_t *)take((size_t)hash_size * 4);
   s.tmp_bytes = sort_tmp;
   s.tmp = take(s.tmp_bytes);
   s.total = off;
@@ -169,8 +185,9 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(permit_bounds, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.skeys, s.first,
                      s.end);
-  hipLaunchKernelGGL(permit_rank, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.skeys, s.svals,
-                     s.first);
+  hipLaunchKernelGGL(permit_limits, dim3(blocks(a.hash_size)), dim3(PT), 0, st, a, s.svals,
+                     s.first, s.end, s.lim);
+  hipLaunchKernelGGL(permit_verdicts, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.keys, s.lim);
   hipLaunchKernelGGL(permit_consume, dim3(blocks(a.hash_size)), dim3(PT), 0, st, a, s.first,
                      s.end);
   return hipGetLastError();
