@@ -480,3 +480,35 @@ def test_kept_timer_heap_same_pops_as_reference(iphash_kept, iphash_ref):
     na = iphash_kept.timer_heap_exercise(7, 3000, 100000, _p(a), len(a))
     nb = iphash_ref.timer_heap_exercise(7, 3000, 100000, _p(b), len(b))
     assert na == nb and np.array_equal(a, b)
+
+
+def test_entry_points_reject_bad_arguments(lib):
+    """Every C-ABI entry point answers a null context or contract-violating
+    arguments with -EINVAL before touching the GPU (include/pptk_rx.h error
+    conventions: 0 or -errno, never an abort)."""
+    from pptk_amd.rx import RxDevBatch, RxOpts
+    EINVAL = -22
+    vp = ctypes.c_void_p
+    assert lib.pptk_rx_ctx_create(None, None) == EINVAL
+    out = vp()
+    bad = RxOpts()
+    lib.pptk_rx_opts_default(ctypes.byref(bad))
+    bad.iphash_bits4 = 33
+    assert lib.pptk_rx_ctx_create(ctypes.byref(out), ctypes.byref(bad)) == EINVAL
+    bad.iphash_bits4, bad.iphash_size = 24, 1000          # not a power of two
+    assert lib.pptk_rx_ctx_create(ctypes.byref(out), ctypes.byref(bad)) == EINVAL
+    assert lib.pptk_rx_batch(None, None, 1, None) == EINVAL
+    b = RxDevBatch()
+    assert lib.pptk_rx_batch_device(None, ctypes.byref(b), None) == EINVAL
+    assert lib.pptk_rx_batch_device_mixed(None, ctypes.byref(b), None, None, None) == EINVAL
+    assert lib.pptk_tx_cksum_device(None, None, None, None, 0, 0, 1, 0, None) == EINVAL
+    assert lib.pptk_tx_rewrite_device(None, None, None, None, 0, 0, 1, None, 1, None, None) == EINVAL
+    assert lib.pptk_tcp_mss_clamp_device(None, None, None, None, 0, 0, 1, 1460, 0, None, None) == EINVAL
+    assert lib.pptk_rx_permit_device(None, None, None, 1, 4, None, None, None, None, None) == EINVAL
+    assert lib.pptk_rx_tokens_refill_device(None, None, 0, 1, 1, 1, None) == EINVAL
+    assert lib.pptk_rx_bin_device(None, None, 1, None, None, None) == EINVAL
+    assert lib.pptk_rx_set_tuning(None, 0, 0) == EINVAL
+    assert lib.pptk_rx_register_ring(None, None, 0) == EINVAL
+    assert lib.pptk_rx_unregister_ring(None, None) == EINVAL
+    assert lib.pptk_rx_last_variant(None) == -1
+    lib.pptk_rx_ctx_destroy(None)                           # a no-op
