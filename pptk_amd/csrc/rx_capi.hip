@@ -143,6 +143,14 @@ struct pptk_rx_ctx {
 
 static int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
 
+// An integer environment knob, read once (the callers keep it in a function-
+// local static: initialised once, thread-safe, as rx threads may race on
+// their first batches).
+static long env_long(const char *name, long dflt) {
+  const char *e = getenv(name);
+  return e ? atol(e) : dflt;
+}
+
 static uint64_t le64(const uint8_t *p) {
   uint64_t v = 0;
   for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
@@ -257,11 +265,7 @@ static int pick_variant(uint32_t span) {
 // batches with the streaming variants (C1500 4.47 -> 4.25 ms; they cost 14 %
 // on C64 and 10 % on offset-described CMIX).  PPTK_RX_TUNE overrides.
 static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
-  static int tune = -2;
-  if (tune == -2) {
-    const char *e = getenv("PPTK_RX_TUNE");
-    tune = e ? atoi(e) : -1;
-  }
+  static const long tune = env_long("PPTK_RX_TUNE", -1);
   if (c->forced_flags >= 0) return (uint32_t)c->forced_flags;
   if (tune >= 0) return (uint32_t)tune;
   const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2 ||
@@ -271,34 +275,20 @@ static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
 }
 
 static int forced_variant(const pptk_rx_ctx *c) {
-  static int force = -2;   // PPTK_RX_VARIANT: A/B override (results never change)
-  if (force == -2) {
-    const char *e = getenv("PPTK_RX_VARIANT");
-    force = e ? atoi(e) : -1;
-  }
+  // PPTK_RX_VARIANT: A/B override (results never change)
+  static const long force = env_long("PPTK_RX_VARIANT", -1);
   if (c->forced_variant >= 0) return c->forced_variant;
-  return force >= 0 && force < RX_NVARIANTS ? force : -1;
+  return force >= 0 && force < RX_NVARIANTS ? (int)force : -1;
 }
 
 static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n) {
   const uint64_t ntiles = (n + 63) / 64;
   const uint64_t want_blocks = (ntiles + 3) / 4;
-  static int grid_mult = -1;
-  if (grid_mult < 0) {
-    const char *e = getenv("PPTK_RX_GRID_MULT");
-    grid_mult = e ? std::max(1, atoi(e)) : 1;
-  }
+  static const long grid_mult = std::max(1l, env_long("PPTK_RX_GRID_MULT", 1));
   // PPTK_RX_RESERVE_CUS: leave that many CUs' worth of resident blocks
   // free, so a concurrent kernel (an RCCL collective overlapping the batch)
   // finds room on the chip instead of waiting for the persistent grid.
-  static int reserve = -1;
-  if (reserve < 0) {
-    const char *e = getenv("PPTK_RX_RESERVE_CUS");
-#ifndef PPTK_RX_RESERVE_DEFAULT
-#define PPTK_RX_RESERVE_DEFAULT 0
-#endif
-    reserve = e ? std::max(0, atoi(e)) : PPTK_RX_RESERVE_DEFAULT;
-  }
+  static const int reserve = (int)std::max(0l, env_long("PPTK_RX_RESERVE_CUS", 0));
   const uint64_t ncu = (uint64_t)std::max(1, c->ncu - std::min(reserve, c->ncu - 1));
   const uint64_t cap = ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, cap));
@@ -579,11 +569,7 @@ static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {
 // it the DMA copy of bulky frames beats the kernel's PCIe reads; measured,
 // DESIGN.md "Small LDP-sized batches").  PPTK_RX_DIRECT_MAX_BYTES overrides.
 static size_t direct_max_bytes() {
-  static long v = -2;
-  if (v == -2) {
-    const char *e = getenv("PPTK_RX_DIRECT_MAX_BYTES");
-    v = e ? atol(e) : 8l << 20;
-  }
+  static const long v = env_long("PPTK_RX_DIRECT_MAX_BYTES", 8l << 20);
   return v < 0 ? 0 : (size_t)v;
 }
 
