@@ -90,7 +90,7 @@ def sum_over_ranks(x, ws, dev):
 
 
 def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=SETTLE_S,
-               compact=False, batch=None):
+               compact=False, batch=None, autotune=True):
     """Generate shard `rank` of config `cfg` (or reuse `batch`), time `steps`
     launches.  compact: 32-byte records (struct pptk_rx_rec32)."""
     import torch
@@ -110,6 +110,10 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     gout = None
     if gather and dist_on(ws):
         gout = torch.empty(n * ws, dtype=torch.int64, device=dev)
+    if autotune:
+        # pick this GPU's fastest interchangeable kernel shape for the batch
+        # (pptk_rx_autotune: results identical, untimed, before the settle)
+        ctx.autotune(b["frames"], n, recs=recs, compact=compact, **kw)
 
     work = [None]
 
@@ -163,10 +167,12 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     # the launch plus the (async) collective enqueue
     kms = [a.elapsed_time(z) for a, z in ev]
     kernel_ms = float(np.median(kms))
+    from pptk_amd.rx import VARIANTS
+    variant = VARIANTS[ctx._L.pptk_rx_last_variant(ctx._ctx)]
     res = {
         "n": n, "bytes": b["bytes"], "rec_bytes": n * (32 if compact else 64), "wall_s": wall,
         "ms_per_step": wall / steps * 1e3, "kernel_ms": kernel_ms,
-        "mpkts": n * ws * steps / wall / 1e6,
+        "mpkts": n * ws * steps / wall / 1e6, "variant": variant,
     }
     # size-independent parity on the full batch: every frame parsed, and the
     # checksum verdicts equal what the generator planted
@@ -197,8 +203,8 @@ def summary(r, n):
     ach = r["bytes"] / ks / 1e9
     rw = (r["bytes"] + r["rec_bytes"]) / ks / 1e9
     return {"value": round(r["mpkts"], 1), "unit": "Mpkts/s",
-            "kernel_ms": round(r["kernel_ms"], 4), "frames_per_gpu": n,
-            "frame_bytes": r["bytes"], "record_bytes": r["rec_bytes"],
+            "kernel_ms": round(r["kernel_ms"], 4), "kernel_variant": r.get("variant"),
+            "frames_per_gpu": n, "frame_bytes": r["bytes"], "record_bytes": r["rec_bytes"],
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                          "rw_achieved": round(rw, 1), "rw_frac": round(rw / HBM_PEAK_GBS, 4)},
@@ -564,7 +570,7 @@ def main():
                 "rw_achieved": round(rw, 1), "rw_frac": round(rw / HBM_PEAK_GBS, 4),
                 "traffic_source": tsrc,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
-                "kernel_ms": round(kernel_ms, 4)}
+                "kernel_ms": round(kernel_ms, 4), "kernel_variant": prim["variant"]}
     if box and "mix_ms" in box:
         # fraction of this GPU's speed of light for the same read/write mix
         # (a trivial kernel moving the same bytes, tools/rwmix.hip)

@@ -302,6 +302,17 @@ int pptk_rx_variant_count(void);
  * batch).  Diagnostics for tests and benchmarks. */
 int pptk_rx_last_variant(const struct pptk_rx_ctx *ctx);
 
+/* Autotuning: run the batch (records are written, as by
+ * pptk_rx_batch_device) with the automatic kernel variant and the shapes
+ * interchangeable with it -- reps timed launches each after two warm-ups --
+ * and let later device batches of the same automatic variant and layout
+ * (fixed-stride or offset-described) use the fastest.  The best shape
+ * depends on the GPU (how expensive its record writes are);
+ * results never change.  Synchronous; reps 1..100.
+ * pptk_rx_set_tuning's forced variant still takes precedence. */
+int pptk_rx_autotune(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *batch, int reps,
+                     void *stream);
+
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);
 

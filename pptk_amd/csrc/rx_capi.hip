@@ -136,6 +136,9 @@ struct pptk_rx_ctx {
   int forced_variant = -1;
   int forced_flags = -1;
   int last_variant = -1;
+  // pptk_rx_autotune's choice per automatic variant, for fixed-stride [0]
+  // and offset-described [1] batches (-1: the automatic variant itself)
+  int tuned[2][RX_NVARIANTS];
   RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch)
   std::vector<RxRing> rings;
   WorkerPool *pool = nullptr;   // started by the first host batch
@@ -192,7 +195,10 @@ int pptk_rx_ctx_create(struct pptk_rx_ctx **out, const struct pptk_rx_opts *opts
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->ncu = prop.multiProcessorCount;
-  for (int v = 0; v < RX_NVARIANTS; ++v) c->bpc[v] = rx_variant_blocks_per_cu(v);
+  for (int v = 0; v < RX_NVARIANTS; ++v) {
+    c->bpc[v] = rx_variant_blocks_per_cu(v);
+    c->tuned[0][v] = c->tuned[1][v] = -1;
+  }
   if (hipMalloc(&c->d_zero, 64) != hipSuccess || hipMemset(c->d_zero, 0, 64) != hipSuccess) {
     (void)hipFree(c->d_zero);
     delete c;
@@ -328,12 +334,10 @@ static RxKArgs batch_args(const pptk_rx_ctx *c, const pptk_rx_dev_batch *b) {
   return a;
 }
 
-int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
-                         void *stream) {
-  int rc = check_batch(c, b);
-  if (rc || b->n == 0) return rc;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
-
+// The automatic kernel variant for a device batch: the lane kernel for
+// fixed-stride 16-byte-aligned frames of at most 64 bytes, else the team
+// shape sized for the longest frame plus its worst misalignment.
+static int auto_variant(const pptk_rx_dev_batch *b, bool *lane_ok_out) {
   // worst misalignment of a frame start inside a 16-byte chunk
   uint32_t mmax = 15;
   if (!b->d_off) {
@@ -345,14 +349,91 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   // the lane kernel takes fixed-stride batches of small frames that all
   // start on a 16-byte boundary (mmax == 0: aligned buffer and stride)
   const bool lane_ok = !b->d_off && !b->d_len && !b->d_perm && mmax == 0 && b->fixed_len <= 64;
-  int variant = lane_ok ? RX_L4 : pick_variant(maxlen + mmax);
-  const int fv = forced_variant(c);
-  if (fv >= 0) variant = fv;
-  if (variant == RX_L4 && !lane_ok) variant = pick_variant(maxlen + mmax);
+  if (lane_ok_out) *lane_ok_out = lane_ok;
+  return lane_ok ? RX_L4 : pick_variant(maxlen + mmax);
+}
+
+static int launch_batch(pptk_rx_ctx *c, const pptk_rx_dev_batch *b, int variant, void *stream) {
   RxKArgs a = batch_args(c, b);
   a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm);
   c->last_variant = variant;
   return hip_err(launch_rx(variant, a, grid_for(c, variant, b->n), (hipStream_t)stream));
+}
+
+int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
+                         void *stream) {
+  int rc = check_batch(c, b);
+  if (rc || b->n == 0) return rc;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  bool lane_ok = false;
+  int variant = auto_variant(b, &lane_ok);
+  const int tv = c->tuned[b->d_off || b->d_len || b->d_perm ? 1 : 0][variant];
+  if (tv >= 0) variant = tv;                  // pptk_rx_autotune's choice
+  const int fv = forced_variant(c);
+  if (fv >= 0) variant = fv;
+  if (variant == RX_L4 && !lane_ok) variant = auto_variant(b, nullptr);   // (a team shape)
+  return launch_batch(c, b, variant, stream);
+}
+
+// Interchangeable shapes per automatic variant (same frame capacity, same
+// results: every variant is parity-tested on every fixture).  Which is
+// fastest depends on the GPU: on boxes whose record writes are expensive
+// (the read/write-mix speed of light ~4.8 ms for C1500) T32S3D7 ran C1500
+// 6 % faster than T16S6; T16S6 was chosen on boxes where the mix costs
+// ~4.0 ms.  The 1536-byte class is the one measured.
+static int autotune_candidates(int variant, int cand[8]) {
+  int n = 0;
+  cand[n++] = variant;
+  if (variant == RX_T16S6) {
+    cand[n++] = RX_T32S3;
+    cand[n++] = RX_T32S3D7;
+    cand[n++] = RX_T16S7L;
+  }
+  return n;
+}
+
+int pptk_rx_autotune(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b, int reps,
+                     void *stream) {
+  int rc = check_batch(c, b);
+  if (rc || b->n == 0) return rc;
+  if (reps < 1 || reps > 100) return -EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  const int base = auto_variant(b, nullptr);
+  const int g = b->d_off || b->d_len || b->d_perm ? 1 : 0;
+  int cand[8];
+  const int nc = autotune_candidates(base, cand);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return -EIO;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  int best = base;
+  float best_ms = 1e30f;
+  for (int k = 0; k < nc && rc == 0; ++k) {
+    std::vector<float> ms;
+    for (int r = 0; r < reps + 2 && rc == 0; ++r) {   // 2 untimed warm-ups
+      if (hipEventRecord(e0, s) != hipSuccess) rc = -EIO;
+      if (rc == 0) rc = launch_batch(c, b, cand[k], stream);
+      if (rc == 0 && (hipEventRecord(e1, s) != hipSuccess ||
+                      hipEventSynchronize(e1) != hipSuccess))
+        rc = -EIO;
+      float t = 0.f;
+      if (rc == 0 && r >= 2 && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms.push_back(t);
+    }
+    if (rc == 0 && !ms.empty()) {
+      std::sort(ms.begin(), ms.end());
+      const float med = ms[ms.size() / 2];
+      if (med < best_ms) {
+        best_ms = med;
+        best = cand[k];
+      }
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc == 0) c->tuned[g][base] = best == base ? -1 : best;
+  return rc;
 }
 
 int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,

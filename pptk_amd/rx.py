@@ -46,7 +46,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_rewrite_device",
-           "pptk_tcp_mss_clamp_device",
+           "pptk_tcp_mss_clamp_device", "pptk_rx_autotune",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init",
@@ -91,6 +91,9 @@ def lib(path=None):
             L.pptk_tx_rewrite_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp]
             L.pptk_tx_rewrite_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_autotune"):             # absent from older A/B builds
+            L.pptk_rx_autotune.argtypes = [vp, ctypes.POINTER(RxDevBatch), ctypes.c_int, vp]
+            L.pptk_rx_autotune.restype = ctypes.c_int
         if hasattr(L, "pptk_tcp_mss_clamp_device"):    # absent from older A/B builds
             L.pptk_tcp_mss_clamp_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64,
                                                     ctypes.c_uint32, ctypes.c_uint64,
@@ -197,6 +200,36 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch_device failed ({rc})")
         return recs
+
+    def autotune(self, frames, n, off=None, lens=None, stride=0, fixed_len=0, max_len=0,
+                 recs=None, compact=False, reps=5, stream=None):
+        """pptk_rx_autotune on this batch layout (synchronous): later device
+        batches of the same shape use the fastest interchangeable kernel
+        variant; returns its name (VARIANTS)."""
+        import torch
+        rb = 32 if compact else 64
+        if recs is None:
+            recs = torch.empty((n, rb), dtype=torch.uint8, device=frames.device)
+        b = RxDevBatch(frames.data_ptr(), None if off is None else off.data_ptr(),
+                       None if lens is None else lens.data_ptr(), None, stride, fixed_len,
+                       max_len, n, None if compact else recs.data_ptr(), None,
+                       recs.data_ptr() if compact else None)
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = self._L.pptk_rx_autotune(self._ctx, ctypes.byref(b), reps,
+                                      ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_autotune failed ({rc})")
+        return self.tuned_variant(frames, n, off, lens, stride, fixed_len, max_len, compact)
+
+    def tuned_variant(self, frames, n, off=None, lens=None, stride=0, fixed_len=0, max_len=0,
+                      compact=False):
+        """Name of the variant a device batch of this shape launches now
+        (runs one batch of it: the variant is reported by the library)."""
+        import torch
+        self.batch_device(frames, n, off=off, lens=lens, stride=stride, fixed_len=fixed_len,
+                          max_len=max_len, compact=compact)
+        torch.cuda.synchronize(frames.device)
+        return VARIANTS[self._L.pptk_rx_last_variant(self._ctx)]
 
     def batch_device_mixed(self, frames, n, off, lens, recs=None, hash_out=None, max_len=0,
                            perm=None, scratch=None, stream=None):

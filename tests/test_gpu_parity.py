@@ -470,3 +470,29 @@ def test_large_fresh_batches_vs_oracle(seed, oracle_lib, dev):
     got32 = _run(ctx, z, dev, shift=3, compact=True)
     d = diff_records(got32, to_rec32(want), dtype=REC32_DTYPE)
     assert not d, d
+
+
+@pytest.mark.parametrize("layout", ["fixed", "offsets"])
+def test_autotune_keeps_records(layout, dev):
+    """pptk_rx_autotune picks one of the interchangeable shapes for a
+    C1500-class batch; later batches launch it and their records are the
+    automatic variant's, bit for bit."""
+    from pptk_amd.rx import RxContext, VARIANTS
+    from tools.synth import make_batch
+    n = 1 << 17
+    b = make_batch("c1500" if layout == "fixed" else "cmix", n, dev)
+    kw = (dict(stride=b["stride"], fixed_len=b["fixed_len"]) if "off" not in b else
+          dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]))
+    ref = RxContext(0, bytes(range(1, 17)))
+    want = ref.batch_device(b["frames"], n, **kw).cpu()
+    ctx = RxContext(0, bytes(range(1, 17)))
+    name = ctx.autotune(b["frames"], n, reps=2, **kw)
+    assert name in ("T16S6", "T32S3", "T32S3D7", "T16S7L")
+    got = ctx.batch_device(b["frames"], n, **kw)
+    torch.cuda.synchronize()
+    assert VARIANTS[ctx._L.pptk_rx_last_variant(ctx._ctx)] == name
+    assert torch.equal(got.cpu(), want)
+    ctx.set_tuning(VARIANTS.index("T16S2"), -1)        # a forced variant still wins
+    ctx.batch_device(b["frames"], n, **kw)
+    torch.cuda.synchronize()
+    assert VARIANTS[ctx._L.pptk_rx_last_variant(ctx._ctx)] == "T16S2"
