@@ -113,7 +113,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     if autotune:
         # pick this GPU's fastest interchangeable kernel shape for the batch
         # (pptk_rx_autotune: results identical, untimed, before the settle)
-        ctx.autotune(b["frames"], n, recs=recs, compact=compact, **kw)
+        ctx.autotune(b["frames"], n, recs=recs, compact=compact, reps=9, **kw)
 
     work = [None]
 

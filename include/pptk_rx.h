@@ -306,7 +306,8 @@ int pptk_rx_last_variant(const struct pptk_rx_ctx *ctx);
  * pptk_rx_batch_device) with the automatic kernel variant and the shapes
  * interchangeable with it -- reps timed launches each after two warm-ups --
  * and let later device batches of the same automatic variant and layout
- * (fixed-stride or offset-described) use the fastest.  The best shape
+ * (fixed-stride or offset-described) use the fastest (another shape must
+ * beat the automatic one by 1 % to replace it).  The best shape
  * depends on the GPU (how expensive its record writes are);
  * results never change.  Synchronous; reps 1..100.
  * pptk_rx_set_tuning's forced variant still takes precedence. */

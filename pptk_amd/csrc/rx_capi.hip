@@ -423,8 +423,11 @@ int pptk_rx_autotune(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b, i
     }
     if (rc == 0 && !ms.empty()) {
       std::sort(ms.begin(), ms.end());
+      // another shape must beat the best so far by 1 %: a noise-level
+      // difference never moves the choice away from the automatic variant
+      // (candidate 0)
       const float med = ms[ms.size() / 2];
-      if (med < best_ms) {
+      if (k == 0 || med < 0.99f * best_ms) {
         best_ms = med;
         best = cand[k];
       }
