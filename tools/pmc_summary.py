@@ -22,12 +22,17 @@ def rows(d, name):
 
 
 def counter(d, cname):
-    vals, durs = [], []
+    """Per-launch values of the dominant rx kernel variant (the one the run's
+    autotune chose: its settle + timed launches outnumber the 9 trial
+    launches of every other shape)."""
+    by = {}
     for r in rows(d, "*counter_collection.csv"):
         if "rx_kernel" in r["Kernel_Name"] and r["Counter_Name"] == cname:
-            vals.append(float(r["Counter_Value"]))
-            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-    return vals, durs
+            v, t = by.setdefault(r["Kernel_Name"], ([], []))
+            v.append(float(r["Counter_Value"]))
+            t.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    name = max(by, key=lambda k: len(by[k][0]))
+    return by[name][0], by[name][1], name
 
 
 def main():
@@ -35,9 +40,9 @@ def main():
     for arg in sys.argv[2:]:
         cfg, dirs = arg.split("=")
         dirs = dirs.split(",")
-        fetch, fd = counter(dirs[0], "FETCH_SIZE")
-        write, wd = counter(dirs[1], "WRITE_SIZE")
-        e = {"launches": len(fetch),
+        fetch, fd, fname = counter(dirs[0], "FETCH_SIZE")
+        write, wd, wname = counter(dirs[1], "WRITE_SIZE")
+        e = {"launches": len(fetch), "pmc_kernel": fname, "pmc_kernel_write": wname,
              "fetch_size_kib": sum(fetch) / len(fetch), "write_size_kib": sum(write) / len(write)}
         e["hbm_read_bytes"] = e["fetch_size_kib"] * 1024 * 2
         e["hbm_write_bytes"] = e["write_size_kib"] * 1024
@@ -45,6 +50,7 @@ def main():
         e["pmc_pass_kernel_ms"] = sum(fd + wd) / len(fd + wd)
         if len(dirs) > 2:
             ks = [r for r in rows(dirs[2], "*kernel_stats.csv") if "rx_kernel" in r["Name"]]
+            ks.sort(key=lambda r: -int(r["Calls"]))
             if ks:
                 e["kernel_trace_avg_ms"] = float(ks[0]["AverageNs"]) / 1e6
                 e["kernel_trace_calls"] = int(ks[0]["Calls"])
