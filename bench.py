@@ -477,14 +477,17 @@ def gather_bench(n, ws, dev, steps):
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
 
 
-def pmc_traffic(cfg):
+def pmc_traffic(cfg, frames):
     """HBM bytes per launch of this config from the committed rocprofv3 PMC
     passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected; see
-    tools/pmc_summary.py); (None, None) when no summary exists."""
+    tools/pmc_summary.py), taken at N_PER_GPU frames per launch and scaled
+    linearly to `frames` (every tile moves the same bytes); (None, None)
+    when no summary exists."""
     try:
         with open(PMC_SUMMARY) as f:
             e = json.load(f)[cfg]
-        return int(e["traffic_bytes"]), os.path.relpath(PMC_SUMMARY, ROOT)
+        return (int(e["traffic_bytes"] * frames / N_PER_GPU),
+                os.path.relpath(PMC_SUMMARY, ROOT))
     except (OSError, KeyError, ValueError):
         return None, None
 
@@ -563,7 +566,7 @@ def main():
     # without the collective
     kernel_ms = (nog or prim)["kernel_ms"]
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(primary_cfg)
+    traffic, tsrc = pmc_traffic(primary_cfg, n)
     rw = (bytes_per_launch + prim["rec_bytes"]) / (kernel_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
