@@ -5,12 +5,12 @@ HIPCC ?= /opt/rocm/bin/hipcc
 CC ?= gcc
 ARCH ?= gfx950
 OBJDIR := build/obj
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude -I/opt/rocm/include
 CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wextra -Iinclude
 
 LIB := pptk_amd/libpptkrx.so
 HIP_SRCS := pptk_amd/csrc/rx_kernel.hip pptk_amd/csrc/rx_bin.hip pptk_amd/csrc/rx_permit.hip \
-            pptk_amd/csrc/rx_capi.hip
+            pptk_amd/csrc/rx_capi.hip pptk_amd/csrc/rx_comm.hip
 C_SRCS := pptk_amd/csrc/host/ipcksum.c pptk_amd/csrc/host/hashseed.c pptk_amd/csrc/host/tcpopt.c \
           pptk_amd/csrc/host/iphash.c pptk_amd/csrc/host/timerlink.c
 HDRS := $(wildcard include/*.h) pptk_amd/csrc/rx_internal.h
@@ -28,7 +28,7 @@ $(OBJDIR)/host/%.o: pptk_amd/csrc/host/%.c $(HDRS)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(LIB): $(HIP_OBJS) $(C_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle

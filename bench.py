@@ -39,15 +39,39 @@ def log(*a):
 
 def dist_on(ws):
     """A process group exists: N > 1, or PPTK_BENCH_FORCE_DIST=1 (a one-rank
-    RCCL group, to exercise the all-gather path on a one-GPU box)."""
+    RCCL communicator, to exercise the all-gather path on a one-GPU box)."""
     return ws > 1 or os.environ.get("PPTK_BENCH_FORCE_DIST") == "1"
 
 
+def launch_ranks(argv, ngpus):
+    """`python bench.py --gpus N` (N > 1) outside a launcher: start N rank
+    processes through torch.distributed.run (127.0.0.1 rendezvous) before
+    anything here touches a GPU, and exit with their status.  Under a
+    launcher (LOCAL_RANK set) this is a no-op."""
+    if ngpus <= 1 or "LOCAL_RANK" in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ngpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + argv
+    log(f"launching {ngpus} ranks: {' '.join(cmd[1:])}")
+    raise SystemExit(subprocess.call(cmd))
+
+
 def dist_setup(ngpus):
+    """One process per GPU.  The host control plane (barriers, max over
+    ranks, the communicator uid) is a gloo group; the data-path collective
+    is RCCL inside libpptkrx.so (pptk_rx_allgather_hash)."""
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != ngpus and "LOCAL_RANK" in os.environ:
+        log(f"[rank {rank}] --gpus {ngpus} but WORLD_SIZE {ws}: using {ws}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if dist_on(ws):
@@ -56,7 +80,7 @@ def dist_setup(ngpus):
         os.environ.setdefault("MASTER_PORT", "29517")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(ws))
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")
     return ws, rank, dev
 
 
@@ -69,63 +93,79 @@ def barrier(ws, dev):
         dist.barrier()
 
 
-def max_over_ranks(x, ws, dev):
+def _reduce(x, ws, op):
     if not dist_on(ws):
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([x], dtype=torch.float64)      # gloo: host tensors
+    dist.all_reduce(t, op=op)
     return float(t.item())
 
 
-def sum_over_ranks(x, ws, dev):
-    if not dist_on(ws):
-        return x
-    import torch
+def max_over_ranks(x, ws, dev=None):
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce(x, ws, dist.ReduceOp.MAX)
 
 
-def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=SETTLE_S,
-               compact=False, batch=None, autotune=True):
-    """Generate shard `rank` of config `cfg` (or reuse `batch`), time `steps`
-    launches.  compact: 32-byte records (struct pptk_rx_rec32)."""
+def sum_over_ranks(x, ws, dev=None):
+    import torch.distributed as dist
+    return _reduce(x, ws, dist.ReduceOp.SUM)
+
+
+def gather_bw(per, ws, seconds):
+    """All-gather bandwidths (RCCL convention): algorithmic = bytes received
+    per rank / time, bus = algorithmic * (ws - 1) / ws."""
+    alg = per * ws * 8 / seconds / 1e9
+    return round(alg, 1), round(alg * (ws - 1) / ws, 1)
+
+
+def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SETTLE_S,
+               compact=False, batch=None, autotune=True, first=None):
+    """Generate this rank's shard of config `cfg` (n frames from global frame
+    `first`, default rank * n) or reuse `batch`, time `steps` launches.
+    gbs: two shard.GatherBuffer (double-buffered all-gather of the flow
+    hashes after every launch, on a second stream) or None.  compact:
+    32-byte records (struct pptk_rx_rec32)."""
     import torch
-    from pptk_amd.shard import allgather_flow_hash
     from tools.synth import make_batch
-    b = batch if batch is not None else make_batch(cfg, n, dev, first=rank * n)
+    first = rank * n if first is None else first
+    b = batch if batch is not None else make_batch(cfg, n, dev, first=first)
     torch.cuda.synchronize(dev)
     recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
-    hbuf = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)] if (gather and dist_on(ws)) else None
     if "off" in b:
         # mixed sizes: per-frame offset/length arrays, frames in batch order
-        # (measured faster than length-binned order, whose per-frame record
-        # scatter costs more than the uniform team shape wastes; DESIGN.md)
+        # (the binned order is measured separately: DESIGN.md)
         kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
     else:
         kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
-    gout = None
-    if gather and dist_on(ws):
-        gout = torch.empty(n * ws, dtype=torch.int64, device=dev)
     if autotune:
         # pick this GPU's fastest interchangeable kernel shape for the batch
         # (pptk_rx_autotune: results identical, untimed, before the settle)
         ctx.autotune(b["frames"], n, recs=recs, compact=compact, reps=9, **kw)
 
-    work = [None]
+    main = torch.cuda.current_stream(dev)
+    gs = torch.cuda.Stream(dev) if gbs else None
+    kdone = [torch.cuda.Event() for _ in range(2)]
+    gdone = [torch.cuda.Event() for _ in range(2)]
 
     def step(k, collective=True):
         # the dense flow-hash array only feeds the all-gather (N > 1); at
-        # N = 1 the records (which carry flow_hash) are the whole output
-        h = hbuf[k & 1] if gout is not None else None
-        ctx.batch_device(b["frames"], n, recs=recs, hash_out=h, compact=compact, **kw)
-        if gout is not None and collective:
-            if work[0] is not None:
-                work[0].wait()                  # previous gather done before reuse
-            _, work[0] = allgather_flow_hash(h, gout, async_op=True)
+        # N = 1 the records (which carry flow_hash) are the whole output.
+        # The kernel writes this rank's hashes into its slice of gather
+        # buffer k % 2 (after the gather of step k - 2 has read it), then
+        # the in-place all-gather runs on the second stream, overlapping
+        # the next launch.
+        gb = gbs[k & 1] if gbs else None
+        if gb is not None:
+            main.wait_event(gdone[k & 1])
+        ctx.batch_device(b["frames"], n, recs=recs, compact=compact,
+                         hash_out=None if gb is None else gb.local[:n], **kw)
+        if gb is not None and collective:
+            kdone[k & 1].record(main)
+            gs.wait_event(kdone[k & 1])
+            gb.gather(ctx, stream=gs)
+            gdone[k & 1].record(gs)
 
     # settle: clocks ramp up over the first few hundred ms of sustained
     # load (the kernel trace shows the first launches 4-5 % slower, and a
@@ -140,39 +180,35 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
         k += 1
         if k % 16 == 0:
             torch.cuda.synchronize(dev)
-    if gout is not None:
+    if gbs:
         # one untimed collective whatever the warmup count, so that RCCL's
-        # lazy communicator / channel setup never lands in the timed steps
-        allgather_flow_hash(hbuf[0], gout)
+        # lazy channel setup never lands in the timed steps
+        gbs[0].gather(ctx, stream=main)
     for k in range(warmup):
         step(k)
-    if work[0] is not None:
-        work[0].wait()
-        work[0] = None
     barrier(ws, dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     t0 = time.perf_counter()
     for k in range(steps):
-        ev[k][0].record()
+        ev[k][0].record(main)
         step(k)
-        ev[k][1].record()
-    if work[0] is not None:
-        work[0].wait()
+        ev[k][1].record(main)
     barrier(ws, dev)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(wall, ws, dev)
     # kernel-only duration: the rx launch is the only work between the
-    # events when there is no gather; with a gather the event pair brackets
-    # the launch plus the (async) collective enqueue
+    # events when there is no gather; with a gather the event pair also
+    # spans the wait for the gather of step k - 2
     kms = [a.elapsed_time(z) for a, z in ev]
     kernel_ms = float(np.median(kms))
     from pptk_amd.rx import VARIANTS
     variant = VARIANTS[ctx._L.pptk_rx_last_variant(ctx._ctx)]
+    n_all = gbs[0].n_total if gbs else n * ws
     res = {
         "n": n, "bytes": b["bytes"], "rec_bytes": n * (32 if compact else 64), "wall_s": wall,
         "ms_per_step": wall / steps * 1e3, "kernel_ms": kernel_ms,
-        "mpkts": n * ws * steps / wall / 1e6, "variant": variant,
+        "mpkts": n_all * steps / wall / 1e6, "variant": variant,
     }
     # size-independent parity on the full batch: every frame parsed, and the
     # checksum verdicts equal what the generator planted
@@ -193,6 +229,82 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gather, check, settle=
     res["_batch"] = b
     res["_recs"] = recs
     return res
+
+
+def gathered_check(prim, gbs, n, dev, k=64):
+    """The all-gathered flow hashes: this rank's slice equals the flow_hash
+    column of its own records (every frame), and the first k frames of
+    every rank's shard, regenerated here from the same synthetic recipe and
+    run through the CPU oracle, equal their gathered slots."""
+    import torch
+    from oracle.oracle import Oracle, make_opts
+    from tools.synth import make_batch
+    gb = gbs[0]
+    got = gb.out.cpu().numpy().view(np.uint64)
+    own = prim["_recs"].view(torch.int64)[:, 0] if prim["_recs"].shape[1] == 64 else None
+    ok_own = own is not None and bool(torch.equal(own, gb.local[:n]))
+    bad = 0
+    cfg = prim["_batch"]["cfg"]
+    for r in range(gb.world):
+        lo = r * gb.per
+        cnt = min(k, max(0, gb.n_total - lo))
+        if cnt == 0:
+            continue
+        b = make_batch(cfg, cnt, dev, first=lo)
+        host = b["frames"][: cnt * b["stride"]].cpu().numpy()
+        want = Oracle().rx_batch(host, None, None, stride=b["stride"], fixed_len=b["fixed_len"],
+                                 n=cnt, opts=make_opts(KEY))
+        bad += int((want["flow_hash"] != got[lo:lo + cnt]).sum())
+    return {"own_slice_equals_records": ok_own, "sampled_frames": k * gb.world,
+            "sampled_mismatches": bad}
+
+
+def mix_sol(b, recs, n):
+    """(ms, description) of the speed of light of an rx launch's traffic mix
+    on this GPU: a trivial kernel (tools/rwmix.hip) reading the same frame
+    bytes in the same 64-frame tiles and writing the same 4 KB of records
+    per tile, nothing computed; the faster of its plain and non-temporal
+    forms.  Offset-described batches (CMIX): the frame buffer read as
+    equal tiles of its whole length (the 10-byte descriptors, ~1 % of the
+    bytes, left out); None if the shapes do not fit."""
+    from tools.rwmix import mix_ms
+    ntiles = n // 64
+    if ntiles == 0:
+        return None
+    rb = 64 * b["stride"] if "off" not in b else (b["frames"].numel() - 64) // ntiles // 16 * 16
+    wb = 64 * (recs.shape[1] if recs.dim() == 2 else 64)
+    if rb % 16 or rb == 0:
+        return None
+    ms = min(mix_ms(b["frames"], rb, ntiles, recs, wb, nt=nt) for nt in (0, 1))
+    return round(ms, 4), f"{ntiles} tiles x {rb} B read + {wb} B written, grid-strided, no compute"
+
+
+def binned_bench(ctx, b, n, dev, steps, warmup):
+    """The binned CMIX path BASELINE.json names (configs[3], "lanes binned
+    by length"): pptk_rx_batch_device_mixed -- the device length binning
+    plus one launch per length group -- timed per batch, whole call."""
+    import torch
+    recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    scratch = torch.empty(ctx._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8, device=dev)
+    kw = dict(max_len=b["max_len"], recs=recs, perm=perm, scratch=scratch)
+    for _ in range(max(warmup, 3)):
+        ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], **kw)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for a, z in ev:
+        a.record()
+        ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], **kw)
+        z.record()
+    torch.cuda.synchronize(dev)
+    ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
+    ach = b["bytes"] / (ms * 1e-3) / 1e9
+    return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "ms_per_batch": round(ms, 4),
+            "workload": "CMIX, pptk_rx_batch_device_mixed: device length binning + one launch "
+                        "per length group, records at the frames' own indices",
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
 
 
 def summary(r, n):
@@ -260,8 +372,41 @@ def _cpu_lib():
     return kind, lib, kw
 
 
-def _cpu_threads():
-    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+def _cpu_topology():
+    """(threads to use, description): the physical cores this process may
+    run on (its CPU affinity, one hardware thread per core, from the sysfs
+    core ids), capped by its cgroup CPU quota (cpu.max) -- on the GPU box
+    the job's share of the host, not the whole machine."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            cores.add((pkg, core))
+        except OSError:
+            cores.add(("?", c))
+    phys = max(1, len(cores))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    n = min(phys, quota) if quota else phys
+    env = int(os.environ.get("PPTK_CPU_THREADS", "0") or 0)
+    if env > 0:
+        n = env
+    desc = (f"{len(cpus)} CPUs in affinity = {phys} physical cores"
+            + (f", cgroup quota {quota} CPUs" if quota else "") + f" -> {n} threads")
+    return n, desc
 
 
 def _cpu_rate(b, n, nth, seconds):
@@ -280,15 +425,18 @@ def _cpu_rate(b, n, nth, seconds):
             return done / el / 1e6, el
 
 
-def cpu_baseline(b, seconds=10.0, sample=262144):
-    """PPTK's CPU path on this host's cores over a sample of the
-    same C1500 batch: the reference's own functions when oracle/_ref was
-    built, else the C restatement.  Full path on all threads (the value) and
-    on one thread, plus ipcksumperf semantics (iphdr/ipcksumperf.c:21-29:
-    ip_cksum_feed over one 1500 B buffer, one thread, Gbit/s)."""
+def cpu_baseline(b, seconds=10.0, sample=1 << 20):
+    """PPTK's CPU path on this host's cores (BASELINE.json
+    configs[0]) over 1,048,576 distinct C1500 frames (1500 B IPv4/TCP) of
+    the same batch: the reference's own functions (oracle/_ref, built from
+    /root/reference by oracle/Makefile and shipped to the box as a binary;
+    kind "reference"), else the C restatement ("port").  Full path on every
+    physical core the job may use (the value) and on one thread, plus
+    ipcksumperf semantics (iphdr/ipcksumperf.c:21-29: ip_cksum_feed over
+    one 1500 B buffer, one thread, Gbit/s)."""
     kind, lib, _ = _cpu_lib()
     n = min(sample, b["n"])
-    threads = _cpu_threads()
+    threads, topo = _cpu_topology()
     mt, el_mt = _cpu_rate(b, n, threads, seconds)
     st, _ = _cpu_rate(b, n, 1, seconds / 2) if seconds >= 1 else (None, 0)
     one = b["frames"][: b["stride"]].cpu().numpy()
@@ -301,6 +449,7 @@ def cpu_baseline(b, seconds=10.0, sample=262144):
             "sample": f"{n} distinct C1500 frames (1500 B IPv4/TCP) from the same batch, "
                       f"full path (IPv4 hdr cksum + TCP cksum + parse + 40 B SipHash), "
                       f"repeated for {el_mt:.1f} s on {threads} threads",
+            "topology": topo,
             "single_thread_mpkts": None if st is None else round(st, 3),
             "ipcksumperf_gbps_1thread": round(gbps, 2),
             "cpu_model": _cpu_model()}
@@ -310,7 +459,7 @@ def cpu_baseline_small(b, seconds=4.0, sample=1 << 20):
     """The same CPU full path over a sample of the C64 batch."""
     kind, _, _ = _cpu_lib()
     n = min(sample, b["n"])
-    threads = _cpu_threads()
+    threads, _ = _cpu_topology()
     mt, el = _cpu_rate(b, n, threads, seconds)
     st, _ = _cpu_rate(b, n, 1, seconds / 2)
     return {"value": round(mt, 3), "unit": "Mpkts/s", "cores": threads, "kind": kind,
@@ -454,27 +603,28 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
             "workload": "C64 records, IPv4 /24 buckets, all frames subject"}
 
 
-def gather_bench(n, ws, dev, steps):
-    """All-gather of n u64 flow hashes per rank alone: time,
-    algorithmic and bus bandwidth (RCCL convention: bus = alg * (ws-1)/ws)."""
+def gather_bench(ctx, gb, ws, dev, steps):
+    """The all-gather of `per` u64 flow hashes per rank alone
+    (pptk_rx_allgather_hash): time and bandwidths."""
     import torch
-    from pptk_amd.shard import allgather_flow_hash
-    h = torch.zeros(n, dtype=torch.int64, device=dev)
-    out = torch.empty(n * ws, dtype=torch.int64, device=dev)
+    main = torch.cuda.current_stream(dev)
     for _ in range(3):
-        allgather_flow_hash(h, out)
+        gb.gather(ctx, stream=main)
     barrier(ws, dev)
     t0 = time.perf_counter()
     for _ in range(steps):
-        allgather_flow_hash(h, out)
+        gb.gather(ctx, stream=main)
     barrier(ws, dev)
     t = max_over_ranks((time.perf_counter() - t0) / steps, ws, dev)
-    alg = n * ws * 8 / t / 1e9
-    return {"bytes_per_rank": n * 8, "ms": round(t * 1e3, 4), "algbw_gbs": round(alg, 1),
-            "busbw_gbs": round(alg * (ws - 1) / ws, 1)}
+    alg, bus = gather_bw(gb.per, ws, t)
+    return {"bytes_per_rank": gb.per * 8, "ms": round(t * 1e3, 4), "algbw_gbs": alg,
+            "busbw_gbs": bus, "rccl_ranks": ctx.comm_info()[0]}
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+# the newest round's committed PMC summary (tools/pmc_summary.py)
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json")
+                                for r in ("r02", "r01")) if os.path.exists(p)),
+                   os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"))
 
 
 def pmc_traffic(cfg, frames):
@@ -513,51 +663,50 @@ def main():
     ap.add_argument("--settle", type=float, default=SETTLE_S,
                     help="seconds of untimed launches before the warmup steps")
     args = ap.parse_args()
+    launch_ranks(sys.argv[1:], args.gpus)
 
     import torch
     from pptk_amd.rx import RxContext
+    from pptk_amd.shard import GatherBuffer, join
     ws, rank, dev = dist_setup(args.gpus)
     ctx = RxContext(dev.index, KEY)
-    if args.scaling == "strong":
-        if args.frames % ws:
-            raise SystemExit(f"--frames {args.frames} not divisible by {ws} GPUs")
-        n = args.frames // ws          # equal shards: the all-gather needs them
+    # weak: --frames per GPU; strong: --frames in total, equal shards
+    # (pptk_rx_shard_range: the last shards padded for the all-gather)
+    n_total = args.frames * ws if args.scaling == "weak" else args.frames
+    gbs = None
+    if dist_on(ws):
+        join(ctx, ws, rank)                       # RCCL communicator in libpptkrx.so
+        gbs = [GatherBuffer(n_total, ws, rank, dev) for _ in range(2)]
+        first, n = gbs[0].first, gbs[0].count
     else:
-        n = args.frames
+        first, n = 0, n_total
     check = not args.no_check
 
     primary_cfg = args.only or "c1500"
-    prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, True, check,
-                      args.settle)
+    prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, gbs, check,
+                      args.settle, first=first)
     log(f"[rank {rank}] {primary_cfg}: {prim['mpkts']:.1f} Mpkts/s, kernel {prim['kernel_ms']:.3f} ms")
     nog = gat = None
-    if dist_on(ws):
+    if gbs:
         # same launches without the collective: the kernel-only duration the
         # roofline uses, and the rate "without the gather" 
-        nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, False,
-                         args.settle, batch=prim["_batch"])
+        nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None, False,
+                         args.settle, batch=prim["_batch"], first=first)
         del nog["_batch"], nog["_recs"]
-        gat = gather_bench(n, ws, dev, args.steps)
+        nog["mpkts"] = n_total * args.steps / nog["wall_s"] / 1e6
+        gat = gather_bench(ctx, gbs[0], ws, dev, args.steps)
+        gat["overlap_loss"] = round(1.0 - prim["mpkts"] / nog["mpkts"], 4)
+        if check:
+            gat["gathered_check"] = gathered_check(prim, gbs, n, dev)
         log(f"[rank {rank}] no gather: {nog['mpkts']:.1f} Mpkts/s; all-gather {gat}")
 
     box = None
     if not args.no_membench:
         from tools.membench import measure
         box = measure(prim["_batch"]["frames"])
-        b = prim["_batch"]
-        if "stride" in b and "off" not in b:
-            # the speed of light of this launch's traffic mix: the same frame
-            # bytes read in the same 64-frame tiles, 4 KB of records written
-            # per tile, nothing computed (tools/rwmix.hip)
-            from tools.rwmix import mix_ms
-            rb = 64 * b["stride"]
-            ntiles = n // 64
-            if rb % 16 == 0:
-                ms = mix_ms(b["frames"], rb, ntiles, prim["_recs"], 4096,
-                            nt=1 if primary_cfg == "c1500" else 0)
-                box["mix_ms"] = round(ms, 4)
-                box["mix_desc"] = (f"{ntiles} tiles x {rb} B read + 4096 B written, "
-                                   "grid-strided, no compute")
+        sol = mix_sol(prim["_batch"], prim["_recs"], n)
+        if sol:
+            box["mix_ms"], box["mix_desc"] = sol
         log(f"[rank {rank}] box HBM: {box}")
 
     bytes_per_launch = prim["bytes"]
@@ -583,8 +732,8 @@ def main():
     # the same batch with compact 32-byte records (struct pptk_rx_rec32)
     rec32 = None
     if not args.no_rec32:
-        r32 = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False,
-                         check, args.settle, compact=True, batch=prim["_batch"])
+        r32 = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None,
+                         check, args.settle, compact=True, batch=prim["_batch"], first=first)
         rec32 = summary(r32, n)
         del r32["_batch"], r32["_recs"]
         log(f"[rank {rank}] {primary_cfg} rec32: {rec32['value']} Mpkts/s")
@@ -607,12 +756,20 @@ def main():
     secondary = {}
     if not args.no_secondary and args.only is None:
         for cfg in ("c64", "cmix"):
-            r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False, check,
-                           args.settle)
+            r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None, check,
+                           args.settle, first=first)
             secondary[cfg] = summary(r, n)
+            if not args.no_membench:
+                sol = mix_sol(r["_batch"], r["_recs"], n)
+                if sol:
+                    secondary[cfg]["roofline"]["mix_sol_ms"] = sol[0]
+                    secondary[cfg]["roofline"]["mix_sol_frac"] = round(sol[0] / r["kernel_ms"], 4)
+            if cfg == "cmix":
+                secondary[cfg]["binned"] = binned_bench(ctx, r["_batch"], n, dev, args.steps,
+                                                        args.warmup)
             if cfg == "c64" and not args.no_rec32:
-                r32 = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, False,
-                                 check, args.settle, compact=True, batch=r["_batch"])
+                r32 = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None,
+                                 check, args.settle, compact=True, batch=r["_batch"], first=first)
                 secondary[cfg]["rec32"] = summary(r32, n)
                 del r32["_batch"], r32["_recs"]
             if cfg == "c64" and rank == 0 and ws == 1 and not args.no_cpu:
@@ -648,8 +805,9 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{primary_cfg.upper()}: {n} frames per GPU"
                                    + (" x 1500 B IPv4/TCP" if primary_cfg == "c1500" else ""),
-                       "frames_per_gpu": n, "global_frames": n * ws,
-                       "parallelism": f"shard{ws}" + ("+allgather(flow_hash)" if dist_on(ws) else ""),
+                       "frames_per_gpu": n, "global_frames": n_total,
+                       "parallelism": f"shard{ws}" + ("+rccl_allgather(flow_hash)" if gbs else ""),
+                       "rccl_ranks": ctx.comm_info()[0] if gbs else None,
                        "key": "01..10"},
             "roofline": roofline,
             "cpu_baseline": cpu,

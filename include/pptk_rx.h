@@ -77,6 +77,38 @@ struct pptk_rx_rec32 {
   uint32_t src_bucket; /* 28                                                */
 };
 
+/* ---- fragment side record (16 bytes, one per frame, written at the
+ * frame's index when pptk_rx_dev_batch.d_frag is set): what an IP
+ * reassembler needs -- reference ipfrag/ipreass.c:118-124 and
+ * ipfrag/rfc815.c:145-151 key on ip_frag_off, ip_more_frags, ip_total_len
+ * and ip_hdr_len -- so fragments can be handed on without parsing the frame
+ * a second time.  All zero for frames that are not PARSED, are MALFORMED,
+ * or are IPv6 without a fragment header.  Fields are host order. */
+struct pptk_rx_frag {
+  uint32_t ident;        /*  0 IPv4 ip_id (iphdr/iphdr.h:1093-1097); IPv6 the
+                                fragment header's 32-bit Identification     */
+  uint16_t frag_off;     /*  4 data offset in bytes: ip_frag_off (:1124-1128)
+                                / ipv6_frag_off (:727-731)                  */
+  uint16_t data_len;     /*  6 fragment data bytes: IPv4 ip_total_len - ihl;
+                                IPv6 40 + payload_len - (frag_hdr_off + 8)  */
+  uint16_t frag_hdr_off; /*  8 IPv6: *frag_hdr_off_ptr of
+                                ipv6_const_proto_hdr_2 (:804-860), counted
+                                from the IPv6 header (the last fragment
+                                header of the chain); IPv4: 0               */
+  uint16_t proto_hdr_off_from_frag; /* 10 IPv6: its *proto_hdr_off_from_frag
+                                (0 for a non-first fragment); IPv4: 0       */
+  uint8_t next_hdr;      /* 12 IPv4 ip_proto; IPv6 the fragment header's
+                                Next Header byte                            */
+  uint8_t flags;         /* 13 PPTK_RX_FRAG_*                               */
+  uint16_t reserved;     /* 14 always 0                                     */
+};
+
+#define PPTK_RX_FRAG_IS 0x01u   /* a fragment: PPTK_RX_F_FRAGMENT            */
+#define PPTK_RX_FRAG_MF 0x02u   /* ip_more_frags (:1023-1027) /
+                                   ipv6_more_frags (:733-737)               */
+#define PPTK_RX_FRAG_DF 0x04u   /* ip_dont_frag (:1040-1044), IPv4 only      */
+#define PPTK_RX_FRAG_V6 0x08u   /* fields taken from an IPv6 fragment header */
+
 #define PPTK_RX_F_PARSED 0x0001u      /* IPv4/IPv6 header parsed            */
 #define PPTK_RX_F_IP_OK 0x0002u       /* ip_cksum == 0 (always for IPv6)    */
 #define PPTK_RX_F_L4_OK 0x0004u       /* L4 present and l4_cksum == 0       */
@@ -132,9 +164,11 @@ int pptk_rx_unregister_ring(struct pptk_rx_ctx *ctx, void *base);
  * pptk_rx_bin_device); records always land at d_recs[i] (or d_recs32[i]
  * when that is set: compact records, d_recs unused) for frame i.
  * d_hash (nullable) additionally receives flow_hash[i] as a dense u64 array,
- * the send buffer of the multi-GPU all-gather.
+ * the send buffer of the multi-GPU all-gather; d_frag (nullable) receives
+ * the fragment side record of every frame (struct pptk_rx_frag).
  * The frame buffer must stay readable up to the next 16-byte boundary past
- * the last frame (any hipMalloc allocation is). */
+ * the last frame (any hipMalloc allocation is); the 16-byte chunk holding
+ * the start of an empty (0-byte) frame is read too. */
 struct pptk_rx_dev_batch {
   const uint8_t *d_frames;
   const uint64_t *d_off;  /* nullable: fixed stride                       */
@@ -147,6 +181,7 @@ struct pptk_rx_dev_batch {
   struct pptk_rx_rec *d_recs;     /* nullable when d_recs32 is set     */
   uint64_t *d_hash;       /* nullable                                     */
   struct pptk_rx_rec32 *d_recs32; /* nullable: compact records instead */
+  struct pptk_rx_frag *d_frag;    /* nullable: fragment side records    */
 };
 
 int pptk_rx_batch_device(struct pptk_rx_ctx *ctx,
@@ -288,8 +323,8 @@ int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const 
  * PPTK_RX_TUNE_BLOCKED (each wavefront takes a contiguous block of tiles
  * instead of every nwaves-th tile).
  * Variants and flags change speed only: results are identical for every
- * setting on every input.  (Flag bits 0x8 and 0x10 are diagnostics that skip
- * record stores / the per-frame phase: never set them outside profiling.) */
+ * setting on every input.  Any other flag bit is rejected with -EINVAL
+ * (PPTK_RX_TUNE in the environment is masked to these bits). */
 #define PPTK_RX_TUNE_NT_LOADS 0x1
 #define PPTK_RX_TUNE_NO_STAGING 0x2
 #define PPTK_RX_TUNE_NT_STORES 0x20
@@ -313,6 +348,56 @@ int pptk_rx_last_variant(const struct pptk_rx_ctx *ctx);
  * pptk_rx_set_tuning's forced variant still takes precedence. */
 int pptk_rx_autotune(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *batch, int reps,
                      void *stream);
+
+/* ---- Multi-GPU (RCCL over xGMI) ------------------------------------------
+ * Batches shard embarrassingly: GPU r of R runs pptk_rx_batch_device on its
+ * own contiguous range of the batch (pptk_rx_shard_range) with d_hash set,
+ * and pptk_rx_allgather_hash then gives every GPU the flow hash of every
+ * frame (ncclAllGather of u64 over one communicator).  The reference scales
+ * with one rx thread per queue (ldp/ldprecvmt.c:174-182); here one context
+ * per GPU, driven by one process per GPU (pptk_rx_comm_uid +
+ * pptk_rx_comm_create) or by one thread per GPU of a single process
+ * (pptk_rx_comm_create_all).  The communicator belongs to its context and is
+ * destroyed with it (or by pptk_rx_comm_destroy). */
+#define PPTK_RX_COMM_UID_BYTES 128
+
+/* Number of visible GPUs (>= 0), or -EIO. */
+int pptk_rx_device_count(void);
+
+/* A new communicator id: made once by one rank and handed to every rank
+ * through the application's own channel (a file, a socket, MPI). */
+int pptk_rx_comm_uid(uint8_t uid[PPTK_RX_COMM_UID_BYTES]);
+
+/* Join `ctx` (one context per GPU) to communicator `uid` as rank `rank` of
+ * `nranks`.  Collective: blocks until every rank has called it.  -EINVAL if
+ * the context already has a communicator. */
+int pptk_rx_comm_create(struct pptk_rx_ctx *ctx, int nranks, int rank,
+                        const uint8_t uid[PPTK_RX_COMM_UID_BYTES]);
+
+/* Single process, one thread per GPU: one communicator over ctxs[0..n)
+ * (each on a different device), rank i = ctxs[i].  Call from one thread;
+ * afterwards each rx thread uses its own context concurrently. */
+int pptk_rx_comm_create_all(struct pptk_rx_ctx *const *ctxs, int n);
+
+int pptk_rx_comm_destroy(struct pptk_rx_ctx *ctx);
+
+/* The context's communicator size and rank; -EINVAL without one. */
+int pptk_rx_comm_info(const struct pptk_rx_ctx *ctx, int *nranks, int *rank);
+
+/* Equal-shard policy for a batch of n frames over nranks GPUs: per_rank =
+ * ceil(n / nranks); rank r owns frames [first, first + count) with first =
+ * min(r * per_rank, n).  Every rank all-gathers per_rank hashes (the last
+ * ranks' shards are padded), so the gathered array holds the flow hash of
+ * global frame i at index i for every i < n. */
+void pptk_rx_shard_range(uint64_t n, int nranks, int rank, uint64_t *first, uint64_t *count,
+                         uint64_t *per_rank);
+
+/* d_out[r * n + i] = d_hash[i] of rank r, for every rank r (n u64 per rank,
+ * the same n on every rank; d_hash may be d_out + rank * n).  Asynchronous
+ * on `stream`; collective: every rank calls it, in the same order relative
+ * to its other collectives. */
+int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint64_t n,
+                           uint64_t *d_out, void *stream);
 
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);

@@ -90,6 +90,22 @@ def _mss(fn, buf, mss, flags, off, lens, stride, fixed_len, n):
     return out, status
 
 
+def _frag(fn, buf, off, lens, stride, fixed_len, n):
+    from pptk_amd.records import FRAG_DTYPE
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    lens = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    if n is None:
+        n = len(off) if off is not None else len(buf) // stride
+    out = np.zeros(n, dtype=FRAG_DTYPE)
+    fn(_ptr(buf), _ptr(off), _ptr(lens), ctypes.c_uint64(stride), ctypes.c_uint32(fixed_len),
+       ctypes.c_size_t(n), _ptr(out))
+    return out
+
+
+_FRAG_ARGS = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t, _vp]
+
+
 class _Lib:
     prefix = ""
 
@@ -155,6 +171,8 @@ class Oracle(_Lib):
         L.orc_update_cksum32.argtypes = [ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32]
         L.orc_tx_batch.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_size_t]
+        L.orc_frag_batch.restype = None
+        L.orc_frag_batch.argtypes = _FRAG_ARGS
         L.orc_permit_batch.restype = None
         L.orc_permit_batch.argtypes = [_vp, ctypes.c_size_t, ctypes.c_int, _vp, _vp, _vp]
         L.orc_tokens_refill.restype = None
@@ -175,6 +193,10 @@ class Oracle(_Lib):
         tok = np.array(tokens, dtype=np.uint32)
         self.lib.orc_tokens_refill(_ptr(tok), start, end, add, initial)
         return tok
+
+    def frag_batch(self, buf, off=None, lens=None, stride=0, fixed_len=0, n=None):
+        """struct pptk_rx_frag side records (records.FRAG_DTYPE) of a batch."""
+        return _frag(self.lib.orc_frag_batch, buf, off, lens, stride, fixed_len, n)
 
     def tx_batch(self, buf, off=None, lens=None, stride=0, fixed_len=0, n=None):
         """Tx-side checksum setting; returns an updated copy of buf."""
@@ -277,6 +299,8 @@ class Reference(_Lib):
         L.ref_update_cksum32.argtypes = [ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32]
         L.ref_tx_batch.argtypes = [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_size_t]
+        L.ref_frag_batch.restype = None
+        L.ref_frag_batch.argtypes = _FRAG_ARGS
         L.ref_permit_batch.restype = None
         L.ref_permit_batch.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint8,
                                        _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]
@@ -294,6 +318,10 @@ class Reference(_Lib):
         self.lib.ref_permit_batch(bytes(key), _ptr(recs), len(recs), family, bits, _ptr(subj),
                                   hash_size, initial, _ptr(tok), _ptr(v))
         return v, tok
+
+    def frag_batch(self, buf, off=None, lens=None, stride=0, fixed_len=0, n=None):
+        """Fragment side records from the reference's own getters and walk."""
+        return _frag(self.lib.ref_frag_batch, buf, off, lens, stride, fixed_len, n)
 
     def tx_batch(self, buf, off=None, lens=None, stride=0, fixed_len=0, n=None):
         """The reference's *_set_cksum_calc on every parsed frame; returns an

@@ -9,9 +9,9 @@
  * Nothing from the reference is copied here: this file only #includes the
  * reference headers in place (-I/root/reference/...) and calls:
  *   ether_type, ip_version, ip_hdr_len, ip_total_len, ip_proto,
- *   ip_frag_off, ip_more_frags, ip_src, ip_dst, ip_const_payload,
+ *   ip_frag_off, ip_more_frags, ip_dont_frag, ip_id, ip_src, ip_dst, ip_const_payload,
  *   ipv6_payload_len, ipv6_nexthdr, is_ipv6_nexthdr, ipv6_const_src/dst,
- *   ipv6_const_proto_hdr_2, tcp/udp_src_port, tcp/udp_dst_port, udp_cksum
+ *   ipv6_const_proto_hdr_2, ipv6_frag_off, ipv6_more_frags, tcp/udp_src_port, tcp/udp_dst_port, udp_cksum
  *                                                  (iphdr/iphdr.h)
  *   ip_hdr_cksum_calc, tcp_cksum_calc, udp_cksum_calc, tcp6_cksum_calc,
  *   udp6_cksum_calc, ip_cksum_feed, ip_cksum_postprocess  (iphdr/ipcksum.*)
@@ -277,6 +277,58 @@ void ref_rx_one(const uint8_t *f, uint32_t len, const struct ref_opts *o,
       r->src_bucket = ref_ip_bucket(o->key, hdr_get32n(r->src), o->bits4, o->hash_size);
     else if (v6 && o->bits6)
       r->src_bucket = ref_ipv6_bucket(o->key, r->src, o->bits6, o->hash_size);
+  }
+}
+
+/* ---- fragment side record (struct pptk_rx_frag) with the reference's
+ * getters: ip_id, ip_frag_off, ip_more_frags, ip_dont_frag, ip_total_len,
+ * ip_hdr_len, ip_proto (iphdr/iphdr.h), and for IPv6 the outputs of
+ * ipv6_const_proto_hdr_2 (frag flag, frag_hdr_off, proto_hdr_off_from_frag)
+ * with ipv6_frag_off / ipv6_more_frags on the fragment header it found.
+ * The 32-bit IPv6 Identification has no reference getter: hdr_get32n of
+ * the fragment header's bytes 4..7 (misc/hdr.h). */
+void ref_frag_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
+                    uint64_t stride, uint32_t fixed_len, size_t n, struct pptk_rx_frag *out)
+{
+  struct ref_opts o;
+  memset(&o, 0, sizeof(o));
+  o.hash_size = 1;
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t *f = buf + (off ? off[i] : (uint64_t)i * stride);
+    uint32_t l = len ? len[i] : fixed_len;
+    struct pptk_rx_rec r;
+    struct pptk_rx_frag *fr = &out[i];
+    const char *ip;
+    memset(fr, 0, sizeof(*fr));
+    ref_rx_one(f, l, &o, &r, 0);
+    if ((r.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED)) != PPTK_RX_F_PARSED)
+      continue;
+    ip = (const char *)f + r.l3_off;
+    if (!(r.flags & PPTK_RX_F_IPV6)) {
+      fr->ident = ip_id(ip);
+      fr->frag_off = ip_frag_off(ip);
+      fr->data_len = (uint16_t)(ip_total_len(ip) - ip_hdr_len(ip));
+      fr->next_hdr = ip_proto(ip);
+      fr->flags = (uint8_t)(((ip_frag_off(ip) != 0 || ip_more_frags(ip)) ? PPTK_RX_FRAG_IS : 0) |
+                            (ip_more_frags(ip) ? PPTK_RX_FRAG_MF : 0) |
+                            (ip_dont_frag(ip) ? PPTK_RX_FRAG_DF : 0));
+    } else {
+      uint8_t proto;
+      int frag = 0;
+      uint16_t fo = 0, pfo = 0;
+      const char *fh;
+      if (ipv6_const_proto_hdr_2(ip, &proto, &frag, &fo, &pfo) == NULL || !frag)
+        continue;
+      fh = ip + fo;
+      fr->ident = hdr_get32n(fh + 4);
+      fr->frag_off = ipv6_frag_off(fh);
+      fr->data_len = (uint16_t)(ipv6_payload_len(ip) + 40u - fo - 8u);
+      fr->frag_hdr_off = fo;
+      fr->proto_hdr_off_from_frag = pfo;
+      fr->next_hdr = (uint8_t)fh[0];
+      fr->flags = (uint8_t)(PPTK_RX_FRAG_IS | PPTK_RX_FRAG_V6 |
+                            (ipv6_more_frags(fh) ? PPTK_RX_FRAG_MF : 0));
+    }
   }
 }
 

@@ -138,11 +138,13 @@ static uint32_t v6_extlen(uint8_t nh, uint8_t lenfield)
   return (uint32_t)lenfield * 8 + 8;
 }
 
-int orc_v6_walk(const uint8_t *ip6, uint8_t *proto, int *fragmented,
-                uint16_t *l4off, int *walked)
+/* The walk, also returning the offset of the last fragment header met
+ * (*frag_hdr_off_ptr of ipv6_const_proto_hdr_2, :815/:826; 0 = none). */
+static int v6_walk_full(const uint8_t *ip6, uint8_t *proto, int *fragmented,
+                        uint16_t *l4off, int *walked, uint16_t *frag_hdr_off)
 {
   uint32_t tlen = (uint32_t)be16_at(ip6 + 4) + 40u;
-  uint16_t off = 40;
+  uint16_t off = 40, fho = 0;
   uint8_t nh = ip6[6];
   int frag = 0, any = 0;
   while (is_v6_ext(nh)) {
@@ -152,6 +154,7 @@ int orc_v6_walk(const uint8_t *ip6, uint8_t *proto, int *fragmented,
       return -1;
     if (nh == 44) {
       frag = 1;
+      fho = off;
       if ((be16_at(ip6 + off + 2) & 0xfff8) > 0)
         break;
     }
@@ -165,7 +168,15 @@ int orc_v6_walk(const uint8_t *ip6, uint8_t *proto, int *fragmented,
   *fragmented = frag;
   *l4off = off;
   *walked = any;
+  *frag_hdr_off = fho;
   return 0;
+}
+
+int orc_v6_walk(const uint8_t *ip6, uint8_t *proto, int *fragmented,
+                uint16_t *l4off, int *walked)
+{
+  uint16_t fho;
+  return v6_walk_full(ip6, proto, fragmented, l4off, walked, &fho);
 }
 
 /* ---- SipHash-2-4: misc/siphash.h:11-121 (init/feed_u64/get), :132-172
@@ -447,6 +458,62 @@ int orc_rx_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
   for (t = 0; t < nthreads; t++)
     pthread_join(th[t], NULL);
   return 0;
+}
+
+/* ---- fragment side record (struct pptk_rx_frag, DESIGN.md "Fragment
+ * side record") of one frame, from the same parse as orc_rx_one: IPv4
+ * ip_id (iphdr/iphdr.h:1093-1097), ip_frag_off (:1124-1128, in bytes),
+ * ip_more_frags (:1023-1027), ip_dont_frag (:1040-1044); IPv6: the last
+ * fragment header of the ipv6_const_proto_hdr_2 walk (:804-860) with
+ * ipv6_frag_off / ipv6_more_frags (:727-737) and its 32-bit Identification.
+ * Zero unless the frame is PARSED and not MALFORMED (IPv6: and carries a
+ * fragment header). */
+void orc_frag_one(const uint8_t *f, uint32_t len, struct pptk_rx_frag *fr)
+{
+  struct pptk_rx_rec r;
+  struct orc_opts o;
+  const uint8_t *ip;
+  memset(fr, 0, sizeof(*fr));
+  memset(&o, 0, sizeof(o));
+  o.hash_size = 1;
+  orc_rx_one(f, len, &o, &r);
+  if ((r.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED)) != PPTK_RX_F_PARSED)
+    return;
+  ip = f + r.l3_off;
+  if (!(r.flags & PPTK_RX_F_IPV6)) {
+    uint16_t fw = be16_at(ip + 6);
+    fr->ident = be16_at(ip + 4);
+    fr->frag_off = (uint16_t)((fw & 0x1fff) * 8);
+    fr->data_len = r.l4_len;                  /* ip_total_len - ihl */
+    fr->next_hdr = r.proto;
+    fr->flags = (uint8_t)(((r.flags & PPTK_RX_F_FRAGMENT) ? PPTK_RX_FRAG_IS : 0) |
+                          ((fw & 0x2000) ? PPTK_RX_FRAG_MF : 0) |
+                          ((fw & 0x4000) ? PPTK_RX_FRAG_DF : 0));
+  } else {
+    uint8_t proto;
+    int frag, walked;
+    uint16_t l4off, fho;
+    const uint8_t *fh;
+    if (v6_walk_full(ip, &proto, &frag, &l4off, &walked, &fho) != 0 || !frag)
+      return;
+    fh = ip + fho;
+    fr->ident = ((uint32_t)be16_at(fh + 4) << 16) | be16_at(fh + 6);
+    fr->frag_off = (uint16_t)(be16_at(fh + 2) & 0xfff8);
+    fr->data_len = (uint16_t)((uint32_t)be16_at(ip + 4) + 40u - (uint32_t)fho - 8u);
+    fr->frag_hdr_off = fho;
+    fr->proto_hdr_off_from_frag = (uint16_t)(l4off - fho);
+    fr->next_hdr = fh[0];
+    fr->flags = (uint8_t)(PPTK_RX_FRAG_IS | PPTK_RX_FRAG_V6 |
+                          ((be16_at(fh + 2) & 1) ? PPTK_RX_FRAG_MF : 0));
+  }
+}
+
+void orc_frag_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
+                    uint64_t stride, uint32_t fixed_len, size_t n, struct pptk_rx_frag *out)
+{
+  for (size_t i = 0; i < n; i++)
+    orc_frag_one(buf + (off ? off[i] : (uint64_t)i * stride), len ? len[i] : fixed_len,
+                 &out[i]);
 }
 
 /* ipcksumperf semantics (iphdr/ipcksumperf.c:21-29): `iters` checksums of

@@ -41,6 +41,9 @@ int orc_rx_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
                  uint64_t stride, uint32_t fixed_len, size_t n,
                  const struct orc_opts *o, struct pptk_rx_rec *recs,
                  int nthreads);
+void orc_frag_one(const uint8_t *frame, uint32_t len, struct pptk_rx_frag *fr);
+void orc_frag_batch(const uint8_t *buf, const uint64_t *off, const uint16_t *len,
+                    uint64_t stride, uint32_t fixed_len, size_t n, struct pptk_rx_frag *out);
 uint32_t orc_cksum_loop(const uint8_t *buf, size_t sz, uint64_t iters);
 void orc_permit_batch(const struct pptk_rx_rec *recs, size_t n, int family,
                       const uint8_t *subject, uint32_t *tokens, uint8_t *verdict);

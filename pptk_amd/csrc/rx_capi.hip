@@ -63,28 +63,37 @@ class WorkerPool {
   size_t size() const { return th_.size() + 1; }
   void parallel_for(size_t n, const std::function<void(size_t)> &f) {
     if (n == 0) return;
+    uint64_t gen;
     {
       std::lock_guard<std::mutex> g(mu_);
       job_ = &f;
       n_ = n;
-      next_.store(0);
+      next_ = 0;
       left_ = n;
-      ++gen_;
+      gen = ++gen_;
     }
     cv_.notify_all();
-    work();
+    work(gen);
     std::unique_lock<std::mutex> g(mu_);
     done_cv_.wait(g, [this] { return left_ == 0; });
     job_ = nullptr;
   }
 
  private:
-  void work() {
+  // Items are claimed under the mutex together with the job they belong to:
+  // a worker still finishing generation k can never claim an index of
+  // generation k + 1 (which starts only after every item of k completed) or
+  // run one with a stale job pointer.  Items are ~256 frames or 1 MiB of
+  // copying, so a lock per claim costs nothing measurable.
+  void work(uint64_t gen) {
+    std::unique_lock<std::mutex> g(mu_);
     for (;;) {
-      const size_t i = next_.fetch_add(1);
-      if (i >= n_) return;
-      (*job_)(i);
-      std::lock_guard<std::mutex> g(mu_);
+      if (gen_ != gen || next_ >= n_) return;
+      const size_t i = next_++;
+      const std::function<void(size_t)> *job = job_;
+      g.unlock();
+      (*job)(i);
+      g.lock();
       if (--left_ == 0) done_cv_.notify_all();
     }
   }
@@ -97,7 +106,7 @@ class WorkerPool {
         if (stop_) return;
         seen = gen_;
       }
-      work();
+      work(seen);
     }
   }
   void shutdown() {
@@ -113,8 +122,7 @@ class WorkerPool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(size_t)> *job_ = nullptr;
-  size_t n_ = 0, left_ = 0;
-  std::atomic<size_t> next_{0};
+  size_t n_ = 0, left_ = 0, next_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
@@ -142,9 +150,16 @@ struct pptk_rx_ctx {
   RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch)
   std::vector<RxRing> rings;
   WorkerPool *pool = nullptr;   // started by the first host batch
+  void *comm = nullptr;         // RCCL communicator (rx_comm.hip), or null
 };
 
+namespace pptk {
+int ctx_device(const pptk_rx_ctx *c) { return c->device; }
+void **ctx_comm_slot(pptk_rx_ctx *c) { return &c->comm; }
+}  // namespace pptk
+
 static int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
+
 
 // An integer environment knob, read once (the callers keep it in a function-
 // local static: initialised once, thread-safe, as rx threads may race on
@@ -189,7 +204,8 @@ int pptk_rx_ctx_create(struct pptk_rx_ctx **out, const struct pptk_rx_opts *opts
   if (!c) return -ENOMEM;
   c->device = opts->device;
   c->opts = *opts;
-  if (hipSetDevice(c->device) != hipSuccess) {
+  DeviceScope dg(c->device);
+  if (!dg.ok) {
     delete c;
     return -EIO;
   }
@@ -247,7 +263,8 @@ static void free_staging(pptk_rx_ctx *c) {
 
 void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DeviceScope dg(c->device);
+  comm_release(c);
   free_staging(c);
   delete c->pool;
   (void)hipFree(c->d_zero);
@@ -270,10 +287,23 @@ static int pick_variant(uint32_t span) {
 // ms, CMIX 3.05 -> 2.97 ms); non-temporal frame loads only for fixed-stride
 // batches with the streaming variants (C1500 4.47 -> 4.25 ms; they cost 14 %
 // on C64 and 10 % on offset-described CMIX).  PPTK_RX_TUNE overrides.
+// The result-preserving memory-policy bits (pptk_rx.h).  The kernels also
+// know diagnostic bits that skip work (record stores, the per-frame phase,
+// half the record bytes, tx writes) for profiling; they are accepted only by
+// a -DPPTK_RX_DIAG build, so a product library can never produce wrong
+// records through pptk_rx_set_tuning or PPTK_RX_TUNE.
+#ifdef PPTK_RX_DIAG
+static constexpr uint32_t kTuneMask = 0xffffu;
+#else
+static constexpr uint32_t kTuneMask = PPTK_RX_TUNE_NT_LOADS | PPTK_RX_TUNE_NO_STAGING |
+                                      PPTK_RX_TUNE_NT_STORES | PPTK_RX_TUNE_SC1_STORES |
+                                      PPTK_RX_TUNE_BLOCKED;
+#endif
+
 static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
   static const long tune = env_long("PPTK_RX_TUNE", -1);
-  if (c->forced_flags >= 0) return (uint32_t)c->forced_flags;
-  if (tune >= 0) return (uint32_t)tune;
+  if (c->forced_flags >= 0) return (uint32_t)c->forced_flags & kTuneMask;
+  if (tune >= 0) return (uint32_t)tune & kTuneMask;
   const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2 ||
                      variant == RX_L4;
   return (small || gather) ? PPTK_RX_TUNE_NT_STORES
@@ -331,6 +361,7 @@ static RxKArgs batch_args(const pptk_rx_ctx *c, const pptk_rx_dev_batch *b) {
   a.recs = b->d_recs;
   a.recs32 = b->d_recs32;
   a.hash = b->d_hash;
+  a.frag = b->d_frag;
   return a;
 }
 
@@ -348,7 +379,11 @@ static int auto_variant(const pptk_rx_dev_batch *b, bool *lane_ok_out) {
   const uint32_t maxlen = b->d_len ? (b->max_len ? b->max_len : 65535u) : b->fixed_len;
   // the lane kernel takes fixed-stride batches of small frames that all
   // start on a 16-byte boundary (mmax == 0: aligned buffer and stride)
-  const bool lane_ok = !b->d_off && !b->d_len && !b->d_perm && mmax == 0 && b->fixed_len <= 64;
+  // (and write no fragment side records: those come from lane_generic)
+  // (an empty frame reads only the chunk holding its start, as the header
+  // allows)
+  const bool lane_ok = !b->d_off && !b->d_len && !b->d_perm && !b->d_frag && mmax == 0 &&
+                       b->fixed_len <= 64;
   if (lane_ok_out) *lane_ok_out = lane_ok;
   return lane_ok ? RX_L4 : pick_variant(maxlen + mmax);
 }
@@ -364,7 +399,8 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
                          void *stream) {
   int rc = check_batch(c, b);
   if (rc || b->n == 0) return rc;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   bool lane_ok = false;
   int variant = auto_variant(b, &lane_ok);
   const int tv = c->tuned[b->d_off || b->d_len || b->d_perm ? 1 : 0][variant];
@@ -397,7 +433,8 @@ int pptk_rx_autotune(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b, i
   int rc = check_batch(c, b);
   if (rc || b->n == 0) return rc;
   if (reps < 1 || reps > 100) return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   const int base = auto_variant(b, nullptr);
   const int g = b->d_off || b->d_len || b->d_perm ? 1 : 0;
   int cand[8];
@@ -446,7 +483,8 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
   if (n == 0) return 0;
   if (!d_frames || (!d_off && stride == 0 && n > 1) || (!d_len && fixed_len > 65535))
     return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   pptk_rx_dev_batch b;
   memset(&b, 0, sizeof(b));
   b.d_frames = d_frames;
@@ -469,7 +507,7 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
   RxKArgs a = batch_args(c, &b);
   a.frames_w = d_frames;
   c->last_variant = variant;
-  a.tune = c->forced_flags >= 0 ? (uint32_t)c->forced_flags
+  a.tune = c->forced_flags >= 0 ? (uint32_t)c->forced_flags & kTuneMask
                                 : pick_tune(c, variant, d_off || d_len) &
                                       ~(uint32_t)PPTK_RX_TUNE_NT_LOADS;
   return hip_err(launch_rx(variant, a, grid_for(c, variant, n), (hipStream_t)stream));
@@ -484,7 +522,8 @@ int pptk_tx_rewrite_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint6
   if (!d_frames || !d_rw || (rw_count != 1 && rw_count != n) ||
       (!d_off && stride == 0 && n > 1) || (!d_len && fixed_len > 65535))
     return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   RxKArgs a = c->tmpl;
   a.frames = d_frames;
   a.frames_w = d_frames;
@@ -510,7 +549,8 @@ int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const ui
   if (!d_frames || (flags & ~PPTK_MSS_SYN_ONLY) || (!d_off && stride == 0 && n > 1) ||
       (!d_len && fixed_len > 65535))
     return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   RxKArgs a = c->tmpl;
   a.frames = d_frames;
   a.frames_w = d_frames;
@@ -532,7 +572,8 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
   int rc = check_batch(c, b);
   if (rc || b->n == 0) return rc;
   if (!b->d_len || !d_perm || !d_scratch) return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   const hipStream_t s = (hipStream_t)stream;
   hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid);
   if (e != hipSuccess) return -EIO;
@@ -557,7 +598,8 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
 }
 
 int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
-  if (!c || variant < -1 || variant >= RX_NVARIANTS || flags < -1 || flags > 0xffff) return -EINVAL;
+  if (!c || variant < -1 || variant >= RX_NVARIANTS || flags < -1) return -EINVAL;
+  if (flags >= 0 && ((uint32_t)flags & ~kTuneMask)) return -EINVAL;
   c->forced_variant = variant;
   c->forced_flags = flags;
   return 0;
@@ -583,7 +625,8 @@ int pptk_rx_permit_device(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_rec
   if (hs == 0 || (hs & (hs - 1))) return -EINVAL;
   if (n == 0) return 0;
   if ((!d_recs && !d_recs32) || !d_tokens || !d_verdict || !d_scratch) return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   PermitArgs a{};
   a.recs = d_recs32 ? nullptr : d_recs;
   a.recs32 = d_recs32;
@@ -600,7 +643,8 @@ int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *c, uint32_t *d_tokens, uint
                                  uint32_t end, uint32_t add, uint32_t initial_tokens,
                                  void *stream) {
   if (!c || !d_tokens || start > end || end > c->opts.iphash_size) return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   return hip_err(launch_refill(d_tokens, start, end, add, initial_tokens, (hipStream_t)stream));
 }
 
@@ -610,7 +654,8 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *c, const uint16_t *d_len, uint64_t n,
                        uint32_t *d_perm, void *d_scratch, void *stream) {
   if (!c || (n && (!d_len || !d_perm || !d_scratch))) return -EINVAL;
   if (n > 0xffffffffull) return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, kBinGrid));
 }
 
@@ -721,7 +766,8 @@ static const RxRing *ring_of(const pptk_rx_ctx *c, const struct ldp_packet *pkts
 
 int pptk_rx_register_ring(struct pptk_rx_ctx *c, void *base, size_t bytes) {
   if (!c || !base || bytes == 0) return -EINVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   if (hipHostRegister(base, bytes, hipHostRegisterMapped) != hipSuccess) return -EIO;
   void *dev = nullptr;
   if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
@@ -736,7 +782,8 @@ int pptk_rx_unregister_ring(struct pptk_rx_ctx *c, void *base) {
   if (!c || !base) return -EINVAL;
   for (size_t i = 0; i < c->rings.size(); ++i) {
     if (c->rings[i].host == (uint8_t *)base) {
-      if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+      DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
       for (RxSlot &sl : c->slot)   // no chunk may still read the ring
         if (sl.stream) (void)hipStreamSynchronize(sl.stream);
       (void)hipHostUnregister(base);
@@ -751,7 +798,8 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
                   struct pptk_rx_rec *recs) {
   if (!c || num < 0 || (num > 0 && (!pkts || !recs))) return -EINVAL;
   if (num == 0) return 0;
-  if (hipSetDevice(c->device) != hipSuccess) return -EIO;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
   const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
   const RxRing *ring = ring_of(c, pkts, num);
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);

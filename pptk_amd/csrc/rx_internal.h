@@ -7,6 +7,30 @@
 
 namespace pptk {
 
+// Every C-ABI entry point works on its context's device and gives the
+// calling thread its current device back on return: a drop-in C library
+// must not move a multi-GPU rx thread's later hipMalloc or launches to
+// another GPU.
+struct DeviceScope {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope &) = delete;
+  DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
+// Context internals shared with the multi-GPU module (rx_comm.hip).
+int ctx_device(const pptk_rx_ctx *c);
+void **ctx_comm_slot(pptk_rx_ctx *c);
+void comm_release(pptk_rx_ctx *c);   // destroys the context's communicator, if any
+
 // Kernel arguments (by value; a handful of SGPRs).
 struct RxKArgs {
   const uint8_t *frames;
@@ -18,6 +42,7 @@ struct RxKArgs {
   pptk_rx_rec *recs;
   pptk_rx_rec32 *recs32; // nullable: compact records instead of recs
   uint64_t *hash;        // nullable
+  pptk_rx_frag *frag;    // nullable: fragment side records
   uint64_t k0, k1;       // SipHash key words (LE loads of key[0..7], key[8..15])
   uint64_t mask6_0, mask6_1;  // ipv6_permitted prefix mask over the 16 address bytes
   uint32_t mask4;        // ip_permitted prefix mask (host order)

@@ -164,6 +164,7 @@ struct FrameView {
 // applies.  IP_OK / L4_OK / UDP_ZERO are decided later by the owning lane.
 struct Parse {
   uint32_t flags, l3, ver, et, proto, rs, re;
+  uint32_t fho;   // IPv6: offset of the last fragment header from L3 (0: none)
 };
 
 __device__ __forceinline__ bool is_v6_ext(uint32_t nh) {
@@ -172,7 +173,7 @@ __device__ __forceinline__ bool is_v6_ext(uint32_t nh) {
 }
 
 __device__ __forceinline__ Parse parse_frame(const FrameView &v, uint32_t len) {
-  Parse p = {0, 0, 0, 0, 0, 0, 0};
+  Parse p = {0, 0, 0, 0, 0, 0, 0, 0};
   if (len < 14 || len > 65535) {
     p.flags = PPTK_RX_F_MALFORMED;
     return p;
@@ -229,10 +230,12 @@ __device__ __forceinline__ Parse parse_frame(const FrameView &v, uint32_t len) {
       walked = true;
       if (off + 8u > tlen) {
         p.flags |= PPTK_RX_F_MALFORMED;
+        p.fho = 0;
         return p;
       }
       if (nh == 44) {
         frag = 1;
+        p.fho = off;
         if ((v.be16(l3 + off + 2) & 0xfff8u) > 0)
           break;
       }
@@ -241,6 +244,7 @@ __device__ __forceinline__ Parse parse_frame(const FrameView &v, uint32_t len) {
       const uint32_t extlen = nh == 44 ? 8u : (nh == 51 ? lf * 4u + 8u : lf * 8u + 8u);
       if (off + extlen > tlen) {
         p.flags |= PPTK_RX_F_MALFORMED;
+        p.fho = 0;
         return p;
       }
       off = (off + extlen) & 0xffffu;
@@ -483,7 +487,46 @@ struct LaneRec {
   uint32_t w[16];
   uint64_t fh;
   uint32_t flags;
+  u32x4 frag;   // struct pptk_rx_frag (only when RxKArgs::frag is set)
 };
+
+// struct pptk_rx_frag (include/pptk_rx.h) of a parsed frame: the IPv4
+// fragment fields (ip_id :1093, ip_frag_off :1124, ip_more_frags :1023,
+// ip_dont_frag :1040 of iphdr/iphdr.h) or those of the last IPv6 fragment
+// header the walk met (ipv6_const_proto_hdr_2's frag_hdr_off and
+// proto_hdr_off_from_frag, :804-860; ipv6_frag_off / ipv6_more_frags
+// :727-737).
+__device__ __forceinline__ u32x4 frag_words(const FrameView &v, const Parse &p) {
+  u32x4 r = (u32x4){0u, 0u, 0u, 0u};
+  if ((p.flags & (PPTK_RX_F_PARSED | PPTK_RX_F_MALFORMED)) != PPTK_RX_F_PARSED) return r;
+  const int l3 = (int)p.l3;
+  uint32_t ident, foff, fl, dlen, nh, fho = 0, pofs = 0;
+  if (!(p.flags & PPTK_RX_F_IPV6)) {
+    const uint32_t fw = v.be16(l3 + 6);
+    ident = v.be16(l3 + 4);
+    foff = ((fw & 0x1fffu) * 8u) & 0xffffu;
+    fl = ((p.flags & PPTK_RX_F_FRAGMENT) ? PPTK_RX_FRAG_IS : 0u) |
+         ((fw & 0x2000u) ? PPTK_RX_FRAG_MF : 0u) | ((fw & 0x4000u) ? PPTK_RX_FRAG_DF : 0u);
+    dlen = p.re - p.rs;
+    nh = p.proto;
+  } else {
+    if (p.fho == 0) return r;
+    fho = p.fho;
+    const int fh = l3 + (int)fho;
+    const uint32_t fw = v.be16(fh + 2);
+    ident = (v.be16(fh + 4) << 16) | v.be16(fh + 6);
+    foff = fw & 0xfff8u;
+    fl = PPTK_RX_FRAG_IS | PPTK_RX_FRAG_V6 | ((fw & 1u) ? PPTK_RX_FRAG_MF : 0u);
+    dlen = (p.re - p.l3) - (fho + 8u);
+    nh = v.u8(fh);
+    pofs = ((p.rs - p.l3) - fho) & 0xffffu;
+  }
+  r.x = ident;
+  r.y = foff | (dlen << 16);
+  r.z = fho | (pofs << 16);
+  r.w = nh | (fl << 8);
+  return r;
+}
 
 // The per-frame part of the transform for a frame in any layout: structural
 // parse, IPv4 header checksum, L4 checksum from the team sum `my_sum` of the
@@ -494,6 +537,8 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
                                              LaneRec &o) {
   const int m = v.m;
   const Parse p = parse_frame(v, len);
+  if (a.frag)
+    o.frag = frag_words(v, p);
   uint32_t flags = p.flags;
   const uint32_t l3 = p.l3, rs = p.rs, re = p.re, proto = p.proto;
   uint32_t *w = o.w;
@@ -698,6 +743,8 @@ __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, 
   const uint32_t *w = o.w;
   if (a.hash)
     a.hash[idx] = o.fh;
+  if (a.frag)
+    ((GLB_AS u32x4 *)a.frag)[idx] = o.frag;
   if (!a.recs && !a.recs32)
     return;   // tx batch: no records
   const bool c32 = a.recs32 != nullptr;   // compact 32-byte records
@@ -725,20 +772,26 @@ __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, 
   }
 }
 
-// Batch order: the tile's 64 records, parked in the wave's LDS at an 80-byte
-// pitch, are one contiguous 4 KB run (2 KB compact) in memory; each store
-// instruction writes 1 KB contiguously instead of 64 scattered 16-byte
-// pieces.
+// The tile's 64 records, parked in the wave's LDS at an 80-byte pitch, are
+// stored with whole-record runs per instruction.  Batch order: they are one
+// contiguous 4 KB run (2 KB compact) in memory, so each store instruction
+// writes 1 KB contiguously instead of 64 scattered 16-byte pieces.
+// Permuted order (SCATTER: the binned processing order of
+// pptk_rx_batch_device_mixed, records land at the frames' own indices):
+// 4 (compact: 2) consecutive lanes write one record's 64 (32) bytes, so an
+// instruction touches 16 (32) records of whole 64-byte (32-byte) runs
+// instead of one 16-byte piece of each of 64 records.  `my_idx` is the
+// lane's frame index (~0: no record).
 __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uint8_t *wimg, uint64_t tile,
-                                              int lane) {
+                                              int lane, uint32_t my_idx, bool scatter) {
 #ifdef PPTK_RX_EXP_NO_FLUSH
   return;
 #endif
   const bool c32 = a.recs32 != nullptr;
   __builtin_amdgcn_wave_barrier();
   const LDS_AS u32x4 *st = (const LDS_AS u32x4 *)wimg;
-  GLB_AS u32x4 *dst = (GLB_AS u32x4 *)(c32 ? (GLB_AS uint8_t *)a.recs32 + tile * (uint64_t)WAVE * 32u
-                                           : (GLB_AS uint8_t *)a.recs + tile * (uint64_t)WAVE * 64u);
+  GLB_AS uint8_t *rbase = c32 ? (GLB_AS uint8_t *)a.recs32 : (GLB_AS uint8_t *)a.recs;
+  GLB_AS u32x4 *dst = (GLB_AS u32x4 *)(rbase + tile * (uint64_t)WAVE * (c32 ? 32u : 64u));
   const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
   const int lg = c32 ? 1 : 2;                 // log2 16-byte pieces per record
   int kmax = c32 ? 2 : 4;
@@ -747,19 +800,27 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
   for (int k = 0; k < 4; ++k) {
     const int e = k * WAVE + lane;   // 16-byte piece e of the tile's records
     const int r = e >> lg;
-    if ((uint64_t)r < nrec && k < kmax) {
-      const u32x4 val = st[r * 5 + (e & ((1 << lg) - 1))];
+    const int piece = e & ((1 << lg) - 1);
+    GLB_AS u32x4 *d = dst + e;
+    bool live = (uint64_t)r < nrec;
+    if (scatter) {
+      const uint32_t ridx = __shfl(my_idx, r & (WAVE - 1));
+      live = ridx != 0xffffffffu;
+      d = (GLB_AS u32x4 *)(rbase + (uint64_t)ridx * (c32 ? 32u : 64u)) + piece;
+    }
+    if (live && k < kmax) {
+      const u32x4 val = st[r * 5 + piece];
       if (a.tune & 64u) {            // bit 6: write-through, drop from L2 (sc1)
-        GLB_AS uint64_t *d8 = (GLB_AS uint64_t *)(dst + e);
+        GLB_AS uint64_t *d8 = (GLB_AS uint64_t *)d;
         __hip_atomic_store(d8, (uint64_t)val.x | ((uint64_t)val.y << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(d8 + 1, (uint64_t)val.z | ((uint64_t)val.w << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       } else if (a.tune & 32u) {     // bit 5: non-temporal stores
         asm volatile("" ::: "memory");
-        __builtin_nontemporal_store(val, dst + e);
+        __builtin_nontemporal_store(val, d);
       } else {
-        dst[e] = val;
+        *d = val;
       }
     }
   }
@@ -790,6 +851,9 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
       const uint32_t lo = *a.range_lo, hi = *a.range_hi;
       a.perm_ld += lo;
       a.n = hi > lo ? hi - lo : 0;
+      // an empty group: perm_ld points one past the permutation, and even
+      // the clamped descriptor loads below would read it
+      if (a.n == 0) return;
     }
   }
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * IMG_STRIDE];
@@ -909,7 +973,8 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     group(T - (D + 1));
 
     // ---- lane phase: frame `lane` -> record (parsed once per frame)
-    const bool stage = !(GATHER && a.perm) && !(a.tune & 2u);
+    const bool stage = !(a.tune & 2u);
+    const bool scatter = GATHER && a.perm;
     // tune bit 4 (diagnostics only, output invalid): skip the lane phase
     if (dc.idx != 0xffffffffu && !(a.tune & 16u)) {
       const int m = (int)(dc.base & 15);
@@ -932,7 +997,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
     }
     if (stage && !(a.tune & 8u) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
-      flush_records(a, wimg, tile, lane);
+      flush_records(a, wimg, tile, lane, dc.idx, scatter);
     tile += step;
     dc = dn;
     dn = d2;
@@ -959,7 +1024,7 @@ __device__ __forceinline__ void lane_load(const RxKArgs &a, uint64_t tile, int l
   const u32x4 *p = (const u32x4 *)(a.frames + i * a.stride);
 #pragma unroll
   for (int s = 0; s < 4; ++s)
-    c[s] = ldc<NT>(p + min((uint32_t)s, nch - 1));   // chunks past the frame: masked at use
+    c[s] = ldc<NT>(p + min((uint32_t)s, nch ? nch - 1 : 0u));   // past the frame: masked at use
 }
 
 template <bool NT>
@@ -995,7 +1060,7 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
     emit_record(a, o, (uint32_t)i, (LDS_AS u32x4 *)slot, true);
   }
   if (!(a.tune & 8u) && (a.recs || a.recs32))
-    flush_records(a, wimg, tile, lane);
+    flush_records(a, wimg, tile, lane, 0u, false);
 }
 
 template <bool NT>

@@ -49,6 +49,20 @@ REC32_DTYPE = np.dtype([
 ])
 assert REC32_DTYPE.itemsize == 32
 
+# struct pptk_rx_frag: the fragment side record (pptk_rx_dev_batch.d_frag)
+FRAG_DTYPE = np.dtype([
+    ("ident", "<u4"),
+    ("frag_off", "<u2"),
+    ("data_len", "<u2"),
+    ("frag_hdr_off", "<u2"),
+    ("proto_hdr_off_from_frag", "<u2"),
+    ("next_hdr", "u1"),
+    ("flags", "u1"),
+    ("reserved", "<u2"),
+])
+assert FRAG_DTYPE.itemsize == 16
+FRAG_IS, FRAG_MF, FRAG_DF, FRAG_V6 = 0x01, 0x02, 0x04, 0x08
+
 F_PARSED = 0x0001
 F_IP_OK = 0x0002
 F_L4_OK = 0x0004

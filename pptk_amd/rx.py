@@ -28,7 +28,7 @@ class RxDevBatch(ctypes.Structure):
                 ("stride", ctypes.c_uint64), ("fixed_len", ctypes.c_uint32),
                 ("max_len", ctypes.c_uint32), ("n", ctypes.c_uint64),
                 ("d_recs", ctypes.c_void_p), ("d_hash", ctypes.c_void_p),
-                ("d_recs32", ctypes.c_void_p)]
+                ("d_recs32", ctypes.c_void_p), ("d_frag", ctypes.c_void_p)]
 
 
 class LdpPacket(ctypes.Structure):
@@ -47,6 +47,10 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_rewrite_device",
            "pptk_tcp_mss_clamp_device", "pptk_rx_autotune",
+           # multi-GPU (RCCL)
+           "pptk_rx_device_count", "pptk_rx_comm_uid", "pptk_rx_comm_create",
+           "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
+           "pptk_rx_shard_range", "pptk_rx_allgather_hash",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init",
@@ -111,6 +115,26 @@ def lib(path=None):
         if hasattr(L, "pptk_rx_batch_device_mixed"):   # absent from older A/B builds
             L.pptk_rx_batch_device_mixed.argtypes = [vp, ctypes.POINTER(RxDevBatch), vp, vp, vp]
             L.pptk_rx_batch_device_mixed.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_allgather_hash"):       # absent from older A/B builds
+            L.pptk_rx_device_count.argtypes = []
+            L.pptk_rx_device_count.restype = ctypes.c_int
+            L.pptk_rx_comm_uid.argtypes = [vp]
+            L.pptk_rx_comm_uid.restype = ctypes.c_int
+            L.pptk_rx_comm_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+            L.pptk_rx_comm_create.restype = ctypes.c_int
+            L.pptk_rx_comm_create_all.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+            L.pptk_rx_comm_create_all.restype = ctypes.c_int
+            L.pptk_rx_comm_destroy.argtypes = [vp]
+            L.pptk_rx_comm_destroy.restype = ctypes.c_int
+            L.pptk_rx_comm_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int)]
+            L.pptk_rx_comm_info.restype = ctypes.c_int
+            u64p = ctypes.POINTER(ctypes.c_uint64)
+            L.pptk_rx_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                              u64p, u64p, u64p]
+            L.pptk_rx_shard_range.restype = None
+            L.pptk_rx_allgather_hash.argtypes = [vp, vp, ctypes.c_uint64, vp, vp]
+            L.pptk_rx_allgather_hash.restype = ctypes.c_int
         L.pptk_rx_version.restype = ctypes.c_char_p
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
@@ -181,10 +205,11 @@ class RxContext:
 
     def batch_device(self, frames, n, off=None, lens=None, stride=0, fixed_len=0,
                      perm=None, recs=None, hash_out=None, max_len=0, stream=None,
-                     compact=False):
+                     compact=False, frag_out=None):
         """Asynchronous device batch on `stream` (torch stream or None = current).
         frames/off/lens/perm/recs/hash_out are torch CUDA tensors; compact:
-        32-byte struct pptk_rx_rec32 records (recs is (n, 32) bytes)."""
+        32-byte struct pptk_rx_rec32 records (recs is (n, 32) bytes);
+        frag_out: (n, 16) uint8 tensor of struct pptk_rx_frag side records."""
         import torch
         rb = 32 if compact else 64
         if recs is None:
@@ -194,7 +219,8 @@ class RxContext:
                        None if perm is None else perm.data_ptr(), stride, fixed_len,
                        max_len, n, None if compact else recs.data_ptr(),
                        None if hash_out is None else hash_out.data_ptr(),
-                       recs.data_ptr() if compact else None)
+                       recs.data_ptr() if compact else None,
+                       None if frag_out is None else frag_out.data_ptr())
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
         rc = self._L.pptk_rx_batch_device(self._ctx, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
@@ -232,7 +258,7 @@ class RxContext:
         return VARIANTS[self._L.pptk_rx_last_variant(self._ctx)]
 
     def batch_device_mixed(self, frames, n, off, lens, recs=None, hash_out=None, max_len=0,
-                           perm=None, scratch=None, stream=None):
+                           perm=None, scratch=None, stream=None, frag_out=None):
         """Mixed-size batch: device binning + one launch per length group
         (asynchronous).  perm/scratch: optional preallocated device buffers."""
         import torch
@@ -245,7 +271,8 @@ class RxContext:
                                   device=frames.device)
         b = RxDevBatch(frames.data_ptr(), off.data_ptr(), lens.data_ptr(), None, 0, 0,
                        max_len, n, recs.data_ptr(),
-                       None if hash_out is None else hash_out.data_ptr())
+                       None if hash_out is None else hash_out.data_ptr(), None,
+                       None if frag_out is None else frag_out.data_ptr())
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
         rc = self._L.pptk_rx_batch_device_mixed(self._ctx, ctypes.byref(b), _dp(perm),
                                                 _dp(scratch), ctypes.c_void_p(s.cuda_stream))
@@ -321,6 +348,34 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_tcp_mss_clamp_device failed ({rc})")
 
+    # ---- multi-GPU (RCCL) -------------------------------------------------
+    def comm_create(self, nranks, rank, uid):
+        """Join communicator `uid` (bytes from comm_uid()) as rank/nranks."""
+        rc = self._L.pptk_rx_comm_create(self._ctx, nranks, rank, bytes(uid))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_comm_create({nranks}, {rank}) failed ({rc})")
+
+    def comm_destroy(self):
+        rc = self._L.pptk_rx_comm_destroy(self._ctx)
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_comm_destroy failed ({rc})")
+
+    def comm_info(self):
+        """(nranks, rank) of the context's communicator, or None."""
+        nr, r = ctypes.c_int(), ctypes.c_int()
+        rc = self._L.pptk_rx_comm_info(self._ctx, ctypes.byref(nr), ctypes.byref(r))
+        return None if rc != 0 else (nr.value, r.value)
+
+    def allgather_hash(self, d_hash, n, d_out, stream=None):
+        """pptk_rx_allgather_hash: n u64 per rank from d_hash into d_out
+        (torch int64 CUDA tensors), asynchronous on `stream`."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(d_out.device)
+        rc = self._L.pptk_rx_allgather_hash(self._ctx, _dp(d_hash), n, _dp(d_out),
+                                            ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_allgather_hash failed ({rc})")
+
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""
         import torch
@@ -354,6 +409,31 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch failed ({rc})")
         return recs
+
+
+def comm_uid(lib_path=None):
+    """A new RCCL communicator id (128 bytes), made on one rank."""
+    buf = ctypes.create_string_buffer(128)
+    rc = lib(lib_path).pptk_rx_comm_uid(buf)
+    if rc != 0:
+        raise OSError(-rc, f"pptk_rx_comm_uid failed ({rc})")
+    return buf.raw
+
+
+def comm_create_all(ctxs):
+    """One communicator over the contexts (one per GPU) of this process."""
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._ctx.value for c in ctxs])
+    rc = ctxs[0]._L.pptk_rx_comm_create_all(arr, len(ctxs))
+    if rc != 0:
+        raise OSError(-rc, f"pptk_rx_comm_create_all failed ({rc})")
+
+
+def shard_range(n, nranks, rank, lib_path=None):
+    """(first, count, per_rank) of the equal-shard policy (pptk_rx_shard_range)."""
+    f, c, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    lib(lib_path).pptk_rx_shard_range(n, nranks, rank, ctypes.byref(f), ctypes.byref(c),
+                                      ctypes.byref(p))
+    return f.value, c.value, p.value
 
 
 LDP_PACKET_DTYPE = np.dtype([("data", "<u8"), ("sz", "<u4"), ("pad", "<u4"),

@@ -1,28 +1,50 @@
-"""Multi-GPU sharding of an rx batch.
+"""Multi-GPU sharding of an rx batch -- the host-side
+mirror of the C-ABI's multi-GPU part (include/pptk_rx.h, "Multi-GPU";
+pptk_amd/csrc/rx_comm.hip).
 
-Frames are independent, so a batch is split into contiguous index ranges,
-one per rank (one process per GPU), with no data-path collective.  The one
-exchange step the north star asks for is an all-gather of the per-frame
-flow hashes (u64) so every rank sees the whole batch's hashes; over RCCL
-(backend "nccl") it runs on xGMI and bench.py overlaps it with the next
-batch's kernel.  The same code runs on gloo for the CPU tests.
+Frames are independent, so a batch of n frames is split into contiguous
+ranges, one per GPU (one process per GPU here; one thread per GPU in
+examples/rx_multigpu.c), with no data-path collective.  The one exchange
+step is the all-gather of the per-frame flow hashes (u64): RCCL's
+ncclAllGather over xGMI on the communicator each rank's pptk_rx_ctx owns.
+Shards are equal (pptk_rx_shard_range: ceil(n / world) frames, the last
+ones padded), so the gathered array holds global frame i's hash at index i.
+
+The kernel writes each rank's hashes straight into its own slice of the
+gather buffer (pptk_rx_dev_batch.d_hash = out + rank * per) and the
+all-gather runs in place: no staging copy, no extra HBM pass.
+
+The uid of the communicator is made on rank 0 and handed to the others over
+the job's host control plane (a torch.distributed gloo group here; a file,
+socket or MPI in a C application).
 """
+from .rx import comm_uid, shard_range  # noqa: F401  (re-exported)
 
 
-def shard_range(n_total, world, rank):
-    """Contiguous [first, first + count) of frames owned by `rank`."""
-    base, extra = divmod(n_total, world)
-    first = rank * base + min(rank, extra)
-    return first, base + (1 if rank < extra else 0)
-
-
-def allgather_flow_hash(local, out=None, group=None, async_op=False):
-    """All-gather equal-sized per-rank u64 flow-hash shards (torch int64
-    tensors) into `out` (world * len(local)), rank-major = global order."""
-    import torch
+def join(ctx, world, rank, group=None):
+    """Join RxContext `ctx` to a new `world`-rank RCCL communicator as
+    `rank`; rank 0 makes the uid and broadcasts it over the (gloo)
+    torch.distributed `group` (default: the world group)."""
     import torch.distributed as dist
-    world = dist.get_world_size(group)
-    if out is None:
-        out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
-    work = dist.all_gather_into_tensor(out, local, group=group, async_op=async_op)
-    return (out, work) if async_op else out
+    obj = [comm_uid() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(obj, src=0, group=group)
+    ctx.comm_create(world, rank, obj[0])
+
+
+class GatherBuffer:
+    """The all-gather destination of one rank: world * per u64 hashes on
+    `device`, and `local`, this rank's slice, which the rx kernel fills
+    (d_hash) before the in-place all-gather."""
+
+    def __init__(self, n_total, world, rank, device):
+        import torch
+        self.first, self.count, self.per = shard_range(n_total, world, rank)
+        self.n_total, self.world, self.rank = n_total, world, rank
+        self.out = torch.zeros(world * self.per, dtype=torch.int64, device=device)
+        self.local = self.out[rank * self.per: rank * self.per + self.per]
+
+    def gather(self, ctx, stream=None):
+        """pptk_rx_allgather_hash of `per` hashes per rank, in place."""
+        ctx.allgather_hash(self.local, self.per, self.out, stream=stream)
+        return self.out[:self.n_total]

@@ -9,7 +9,7 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-GOLDEN_SETS = ("edge", "fuzz", "c64", "c1500", "cmix", "icmp")
+GOLDEN_SETS = ("edge", "fuzz", "c64", "c1500", "cmix", "icmp", "frag")
 
 
 def pytest_configure(config):

@@ -371,6 +371,60 @@ def gen_fuzz(n, seed=0xF022):
     return pack(frames)
 
 
+def frag6(off_bytes=0, m=0, ident=0, reserved=0):
+    """IPv6 fragment header body (next header filled in by frame_v6):
+    reserved byte, offset (bytes, multiple of 8) | M, 32-bit Identification."""
+    return bytes([0, reserved & 0xFF]) + struct.pack(">HI", (off_bytes & 0xFFF8) | (m & 1),
+                                                      ident & 0xFFFFFFFF)
+
+
+def gen_frag(n=1500, seed=0xF7A6):
+    """Fragment workload for the fragment side record (pptk_rx_frag): IPv4
+    fragments (MF / offset / DF / ident, IHL > 5, VLAN) and non-fragments,
+    IPv6 fragment headers first / subsequent / atomic, behind hop-by-hop,
+    destination and routing headers (some long enough to put the fragment
+    header past the first 128 bytes), two fragment headers in one chain, a
+    non-zero reserved byte (the reference's extlen-from-next-header quirk),
+    and random header mutations."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for i in range(n):
+        vlan = int(rng.integers(1, 4095)) if rng.random() < 0.25 else None
+        proto = int(rng.choice([6, 17]))
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            ihl = int(rng.integers(6, 16)) if rng.random() < 0.1 else 5
+            mf = bool(rng.random() < 0.5)
+            fo = int(rng.integers(0, 0x2000)) if rng.random() < 0.6 else 0
+            minsz = 14 + (4 if vlan else 0) + 4 * ihl + (20 if proto == 6 else 8)
+            f = bytearray(frame_v4(rng, proto, max(int(rng.integers(64, 1500)), minsz), vlan,
+                                   ihl, mf=mf, frag_off=fo))
+            if rng.random() < 0.3:                      # DF cleared on some
+                f[14 + (4 if vlan else 0) + 6] &= 0xBF
+        else:
+            ext = []
+            for _ in range(int(rng.integers(0, 3))):
+                t = int(rng.choice([0, 60, 43]))
+                ext.append((t, hbh(int(rng.integers(1, 18)))))
+            m = int(rng.integers(0, 2))
+            off = int(rng.integers(1, 8000)) * 8 if rng.random() < 0.5 else 0
+            res = int(rng.integers(1, 3)) if rng.random() < 0.05 else 0
+            ext.append((44, frag6(off, m, int(rng.integers(0, 2 ** 32)), res)))
+            if rng.random() < 0.1:                      # a second fragment header
+                ext.append((44, frag6(0, int(rng.integers(0, 2)), int(rng.integers(0, 2 ** 32)))))
+            if rng.random() < 0.1:
+                ext.append((60, hbh(1)))
+            hdrs = sum(len(b) for _, b in ext)
+            minsz = 14 + (4 if vlan else 0) + 40 + hdrs + (20 if proto == 6 else 8)
+            f = bytearray(frame_v6(rng, proto, max(int(rng.integers(80, 1500)), minsz), vlan, ext))
+        if rng.random() < 0.1:
+            for _ in range(int(rng.integers(1, 3))):
+                pos = int(rng.integers(0, min(len(f), 200)))
+                f[pos] = int(rng.integers(0, 256))
+        frames.append(bytes(f))
+    return pack(frames)
+
+
 def gen_permit(n=3000, seed=0x9E7):
     """Rate-limiter workload: frames from few source prefixes (20 IPv4 /24s,
     8 IPv6 /48s) so that token buckets see long runs, in random order, with a

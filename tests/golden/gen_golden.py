@@ -33,6 +33,12 @@ adjust_sack_2 / adjust_tsval / adjust_tsecho / set_ack_off / seq / ack /
 window *_cksum_update; oracle/refgen.c ref_tcp_opt_op).  Inputs on which
 the reference never returns are marked and not run.
 
+frag.npz holds fragment side records (struct pptk_rx_frag) made by the
+reference's ip_id / ip_frag_off / ip_more_frags / ip_dont_frag and
+ipv6_const_proto_hdr_2 (oracle/refgen.c ref_frag_batch): a dedicated
+fragment set (framegen.gen_frag) with its 64-byte records, and the side
+records of the edge, fuzz and cmix sets.
+
 permit.npz additionally holds rate-limiter cases: token arrays before/after
 and per-frame verdicts of the reference's ip_permitted / ipv6_permitted
 called once per subject frame in frame order (oracle/refgen.c
@@ -253,11 +259,31 @@ def gen_tcpopt(ref):
             "after": after}
 
 
+def gen_frag(ref):
+    """Fragment side records (struct pptk_rx_frag) from the reference's own
+    getters and IPv6 walk (oracle/refgen.c ref_frag_batch): a dedicated
+    fragment set (framegen.gen_frag, with its 64-byte records too) and the
+    side records of the edge / fuzz / cmix sets."""
+    opts = make_opts(KEY, BITS4, BITS6, HASH_SIZE)
+    buf, off, lens = framegen.gen_frag()
+    out = dict(buf=buf, off=off, len=lens,
+               recs=ref.rx_batch(buf, off, lens, opts=opts, with_bucket=True)
+               .view(np.uint8).reshape(-1, 64),
+               frag=ref.frag_batch(buf, off, lens).view(np.uint8).reshape(-1, 16),
+               key=np.frombuffer(KEY, dtype=np.uint8),
+               iphash=np.array([BITS4, BITS6, HASH_SIZE], dtype=np.uint32))
+    for name in ("edge", "fuzz", "cmix"):
+        z = dict(np.load(os.path.join(HERE, f"{name}.npz")))
+        out[f"{name}_frag"] = ref.frag_batch(z["buf"], z["off"], z["len"]).view(np.uint8) \
+            .reshape(-1, 16)
+    return out
+
+
 def main():
     build()
     ref = Reference()
     opts = make_opts(KEY, BITS4, BITS6, HASH_SIZE)
-    want = set(sys.argv[1:]) or set(SETS) | {"permit", "tx", "rewrite", "mss", "tcpopt"}
+    want = set(sys.argv[1:]) or set(SETS) | {"permit", "tx", "rewrite", "mss", "tcpopt", "frag"}
     if "mss" in want:
         path = os.path.join(HERE, "mss.npz")
         np.savez_compressed(path, **gen_mss(ref))
@@ -274,6 +300,10 @@ def main():
         path = os.path.join(HERE, "tx.npz")
         np.savez_compressed(path, **gen_tx(ref))
         print(f"tx -> {os.path.getsize(path)} B")
+    if "frag" in want:
+        path = os.path.join(HERE, "frag.npz")
+        np.savez_compressed(path, **gen_frag(ref))
+        print(f"frag -> {os.path.getsize(path)} B")
     if "permit" in want:
         path = os.path.join(HERE, "permit.npz")
         np.savez_compressed(path, **gen_permit(ref))

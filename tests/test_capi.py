@@ -128,7 +128,8 @@ def test_c_dropin_program(tmp_path):
 
 
 @pytest.mark.parametrize("struct,dtname", [("pptk_rx_rec", "REC_DTYPE"),
-                                            ("pptk_rx_rec32", "REC32_DTYPE")])
+                                            ("pptk_rx_rec32", "REC32_DTYPE"),
+                                            ("pptk_rx_frag", "FRAG_DTYPE")])
 def test_record_layout_matches_header(struct, dtname):
     import pptk_amd.records as R
     dt = getattr(R, dtname)
@@ -511,6 +512,17 @@ def test_entry_points_reject_bad_arguments(lib):
     assert lib.pptk_rx_register_ring(None, None, 0) == EINVAL
     assert lib.pptk_rx_unregister_ring(None, None) == EINVAL
     assert lib.pptk_rx_last_variant(None) == -1
+    # multi-GPU part (include/pptk_rx.h "Multi-GPU")
+    uid = ctypes.create_string_buffer(128)
+    assert lib.pptk_rx_comm_uid(None) == EINVAL
+    assert lib.pptk_rx_comm_create(None, 1, 0, uid) == EINVAL
+    assert lib.pptk_rx_comm_create_all(None, 1) == EINVAL
+    nul = (vp * 2)(None, None)
+    assert lib.pptk_rx_comm_create_all(nul, 2) == EINVAL
+    assert lib.pptk_rx_comm_create_all(nul, 0) == EINVAL
+    assert lib.pptk_rx_comm_destroy(None) == EINVAL
+    assert lib.pptk_rx_comm_info(None, None, None) == EINVAL
+    assert lib.pptk_rx_allgather_hash(None, None, 1, None, None) == EINVAL
     lib.pptk_rx_ctx_destroy(None)                           # a no-op
 
 

@@ -1,7 +1,9 @@
 """World-size-2 gloo rehearsal of the multi-GPU path on CPU: each rank
-computes the records of its contiguous shard (oracle stands in for the GPU
-kernel here), the flow hashes are all-gathered, and the result must equal
-the single-process batch bit for bit."""
+takes its shard by the C-ABI's equal-shard policy (pptk_rx_shard_range),
+computes its records (the oracle stands in for the GPU kernel here), the
+flow hashes are all-gathered in place into the padded layout the RCCL path
+uses (gloo's all_gather_into_tensor stands in for pptk_rx_allgather_hash),
+and the result must equal the single-process batch bit for bit."""
 import os
 
 import numpy as np
@@ -18,25 +20,24 @@ def _worker(rank, world, port, name, q):
     import torch.distributed as dist
     from oracle.oracle import Oracle, make_opts
     from pptk_amd.records import F_PARSED
-    from pptk_amd.shard import allgather_flow_hash, shard_range
+    from pptk_amd.shard import shard_range
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         z = load_golden(name)
         n = len(z["off"])
-        first, cnt = shard_range(n, world, rank)
+        first, cnt, per = shard_range(n, world, rank)
         b4, b6, hs = (int(x) for x in z["iphash"])
         recs = Oracle().rx_batch(z["buf"], z["off"][first:first + cnt], z["len"][first:first + cnt],
                                  opts=make_opts(z["key"].tobytes(), b4, b6, hs))
         h = np.where(recs["flags"] & F_PARSED, recs["flow_hash"], 0).view(np.int64)
-        # pad to equal shard size for all_gather_into_tensor
-        per = (n + world - 1) // world
-        loc = torch.zeros(per, dtype=torch.int64)
+        # the rank's slice of the gather buffer (GatherBuffer.local), padded
+        out = torch.zeros(world * per, dtype=torch.int64)
+        loc = out[rank * per:(rank + 1) * per].clone()
         loc[:cnt] = torch.from_numpy(h.copy())
-        out = allgather_flow_hash(loc)
+        dist.all_gather_into_tensor(out, loc)
         if rank == 0:
-            parts = [out[r * per:r * per + shard_range(n, world, r)[1]] for r in range(world)]
-            q.put(torch.cat(parts).numpy().view(np.uint64))
+            q.put(out[:n].numpy().view(np.uint64))
     finally:
         dist.destroy_process_group()
 
@@ -58,14 +59,28 @@ def test_sharded_allgather_equals_single(name):
     assert np.array_equal(got, np.where(want["flags"] & F_PARSED, want["flow_hash"], 0))
 
 
-@pytest.mark.parametrize("n,world", [(10, 3), (16, 4), (1, 2), (0, 2), (134217728, 8)])
+@pytest.mark.parametrize("n,world", [(10, 3), (16, 4), (1, 2), (0, 2), (2, 4), (7, 8),
+                                     (134217728, 8), (134217727, 8)])
 def test_shard_range_partitions(n, world):
+    """pptk_rx_shard_range: contiguous, covering, equal per-rank gather size,
+    and rank r's frames sit at gathered index r * per (global order)."""
     from pptk_amd.shard import shard_range
     got = [shard_range(n, world, r) for r in range(world)]
+    per = got[0][2]
+    assert per == (n + world - 1) // world
     assert got[0][0] == 0
-    for (f0, c0), (f1, _) in zip(got, got[1:]):
-        assert f0 + c0 == f1
-    assert sum(c for _, c in got) == n
+    for (f0, c0, p0), (f1, _, _) in zip(got, got[1:]):
+        assert f0 + c0 == f1 and p0 == per
+    assert sum(c for _, c, _ in got) == n
+    for r, (f, c, _) in enumerate(got):
+        assert c <= per and (c == 0 or f == r * per)
+
+
+def test_shard_range_rejects_bad_rank():
+    from pptk_amd.shard import shard_range
+    assert shard_range(10, 0, 0) == (0, 0, 0)
+    assert shard_range(10, 2, 2) == (0, 0, 0)
+    assert shard_range(10, 2, -1) == (0, 0, 0)
 
 
 def _bench_worker(rank, world, port, q):
@@ -81,7 +96,7 @@ def _bench_worker(rank, world, port, q):
         bench.barrier(world, dev)
         mx = bench.max_over_ranks(float(rank + 1), world, dev)
         sm = bench.sum_over_ranks(float(rank + 1), world, dev)
-        g = bench.gather_bench(1024, world, dev, 3)
+        g = bench.gather_bw(1024, world, 1e-3)
         if rank == 0:
             q.put((mx, sm, g))
     finally:
@@ -89,8 +104,8 @@ def _bench_worker(rank, world, port, q):
 
 
 def test_bench_multi_rank_helpers():
-    """bench.py's N > 1 bookkeeping (barrier, max/sum over ranks, the
-    all-gather timing and its bus-bandwidth arithmetic) on gloo, world 2."""
+    """bench.py's N > 1 bookkeeping (barrier, max/sum over ranks on its gloo
+    control plane, the all-gather bandwidth arithmetic) on gloo, world 2."""
     world, port = 2, 30600 + (os.getpid() % 1000)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -102,5 +117,31 @@ def test_bench_multi_rank_helpers():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert mx == 2.0 and sm == 3.0
-    assert g["bytes_per_rank"] == 1024 * 8 and g["ms"] > 0
-    assert abs(g["busbw_gbs"] - g["algbw_gbs"] / 2) <= 0.1 + 1e-9
+    alg, bus = g
+    assert alg == round(1024 * 2 * 8 / 1e-3 / 1e9, 1) and abs(bus - alg / 2) <= 0.1
+
+
+def test_bench_launches_ranks_itself(tmp_path, monkeypatch):
+    """`python bench.py --gpus N` outside a launcher starts N ranks through
+    torch.distributed.run (the command it builds, not run here)."""
+    import subprocess
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = {}
+
+    def fake_call(cmd):
+        seen["cmd"] = cmd
+        return 0
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    with pytest.raises(SystemExit) as e:
+        bench.launch_ranks(["--gpus", "4", "--steps", "3"], 4)
+    assert e.value.code == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    bench.launch_ranks(["--gpus", "4"], 4)          # under a launcher: no-op
+    bench.launch_ranks([], 1)

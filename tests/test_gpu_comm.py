@@ -1,0 +1,142 @@
+"""The multi-GPU part of the C-ABI (include/pptk_rx.h "Multi-GPU",
+pptk_amd/csrc/rx_comm.hip) on the GPU: RCCL communicators built through the
+C-ABI (one process: pptk_rx_comm_uid + pptk_rx_comm_create, and
+pptk_rx_comm_create_all), the kernel writing flow hashes into the rank's
+slice of the gather buffer, and the in-place pptk_rx_allgather_hash, checked
+against the reference-made golden flow hashes.  One GPU on the test box, so
+the communicators have one rank; the N-rank layout is the same code with
+per-rank offsets (tests/test_dist.py rehearses N = 2 on gloo)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from pptk_amd.records import as_records
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+EINVAL = 22
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def _ctx(z):
+    from pptk_amd.rx import RxContext
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    return RxContext(0, z["key"].tobytes(), b4, b6, hs, max_frame=65535)
+
+
+def _gather_set(ctx, z, dev, world=1, rank=0):
+    from pptk_amd.shard import GatherBuffer
+    n = len(z["off"])
+    gb = GatherBuffer(n, world, rank, dev)
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    f, c = gb.first, gb.count
+    recs = ctx.batch_device(frames, c, off=off[f:f + c], lens=lens[f:f + c],
+                            max_len=int(z["len"].max()), hash_out=gb.local[:c])
+    got = gb.gather(ctx)
+    torch.cuda.synchronize()
+    return got.cpu().numpy().view(np.uint64), recs.cpu().numpy().reshape(-1)
+
+
+@pytest.mark.parametrize("name", ["edge", "fuzz", "cmix", "c1500"])
+def test_comm_create_one_rank_allgather_equals_golden(dev, name):
+    from pptk_amd.rx import comm_uid
+    z = load_golden(name)
+    ctx = _ctx(z)
+    ctx.comm_create(1, 0, comm_uid())
+    assert ctx.comm_info() == (1, 0)
+    got, recs = _gather_set(ctx, z, dev)
+    want = as_records(z["recs"])["flow_hash"]
+    assert np.array_equal(got, want)
+    assert np.array_equal(as_records(recs)["flow_hash"], want)
+    ctx.comm_destroy()
+    assert ctx.comm_info() is None
+    ctx.close()
+
+
+def test_comm_create_all_one_gpu(dev):
+    from pptk_amd.rx import comm_create_all
+    z = load_golden("cmix")
+    ctx = _ctx(z)
+    comm_create_all([ctx])
+    assert ctx.comm_info() == (1, 0)
+    got, _ = _gather_set(ctx, z, dev)
+    assert np.array_equal(got, as_records(z["recs"])["flow_hash"])
+    ctx.close()                                   # destroys the communicator too
+
+
+def test_comm_repeated_gathers_and_reuse(dev):
+    """Many batches and gathers on one communicator, then destroy and a new
+    communicator on the same context."""
+    from pptk_amd.rx import comm_uid
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    want = as_records(z["recs"])["flow_hash"]
+    for _ in range(2):
+        ctx.comm_create(1, 0, comm_uid())
+        for _ in range(5):
+            got, _ = _gather_set(ctx, z, dev)
+            assert np.array_equal(got, want)
+        ctx.comm_destroy()
+    ctx.close()
+
+
+def test_comm_contract_errors(dev):
+    from pptk_amd.rx import comm_create_all, comm_uid
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    h = torch.zeros(8, dtype=torch.int64, device=dev)
+    with pytest.raises(OSError) as e:                       # no communicator yet
+        ctx.allgather_hash(h, 8, h)
+    assert e.value.errno == EINVAL
+    uid = comm_uid()
+    for nr, r in ((0, 0), (1, 1), (2, -1)):
+        with pytest.raises(OSError) as e:
+            ctx.comm_create(nr, r, uid)
+        assert e.value.errno == EINVAL
+    ctx.comm_create(1, 0, uid)
+    with pytest.raises(OSError) as e:                       # one per context
+        ctx.comm_create(1, 0, comm_uid())
+    assert e.value.errno == EINVAL
+    with pytest.raises(OSError) as e:
+        comm_create_all([ctx])                              # already has one
+    assert e.value.errno == EINVAL
+    with pytest.raises(OSError) as e:                       # null buffers
+        ctx.allgather_hash(None, 8, h)
+    assert e.value.errno == EINVAL
+    ctx.allgather_hash(None, 0, h)                          # n == 0: nothing to do
+    ctx.comm_destroy()
+    ctx.comm_destroy()                                      # idempotent
+    other = _ctx(z)
+    with pytest.raises(OSError) as e:                       # two ranks on one GPU
+        comm_create_all([ctx, other])
+    assert e.value.errno == EINVAL
+    other.close()
+    ctx.close()
+
+
+def test_entry_points_restore_callers_device(dev):
+    """An entry point leaves the calling thread on its current device (with
+    one GPU on the box this checks the restore path runs cleanly; the
+    device switch itself needs two GPUs)."""
+    from pptk_amd.rx import lib
+    hip = ctypes.CDLL("libamdhip64.so")
+    cur = ctypes.c_int(-1)
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    ctx.batch_device(frames, 4, off=torch.from_numpy(z["off"][:4].view(np.int64)).to(dev),
+                     lens=torch.from_numpy(z["len"][:4].view(np.int16)).to(dev), max_len=1500)
+    torch.cuda.synchronize()
+    assert hip.hipGetDevice(ctypes.byref(cur)) == 0 and cur.value == 0
+    assert lib().pptk_rx_device_count() >= 1
+    ctx.close()
