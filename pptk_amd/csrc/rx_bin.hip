@@ -68,9 +68,14 @@ __global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, u
     table[threadIdx.x] = threadIdx.x < (unsigned)NB ? counts[threadIdx.x * g] : part[1023];
 }
 
+// (bdesc: optionally also the frames' descriptors in binned order -- offset
+// (or i * stride) and length at the same position as the index -- so the
+// group launches read them sequentially instead of gathering them through
+// perm: 10 bytes per frame written and later streamed, instead of two
+// scattered 8- and 2-byte reads that each fetch a whole 64-byte sector)
 __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t n,
                                                   uint64_t per_block, const uint32_t *offs,
-                                                  uint32_t *perm) {
+                                                  uint32_t *perm, BinDesc bdesc) {
   __shared__ uint32_t cursor[NB];
   __shared__ uint32_t wcnt[NWARP][NB];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -94,7 +99,12 @@ __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t 
     if (ok) {
       uint32_t before = cursor[b];
       for (int w2 = 0; w2 < wv; ++w2) before += wcnt[w2][b];
-      perm[before + rank] = (uint32_t)i;
+      const uint32_t pos = before + rank;
+      perm[pos] = (uint32_t)i;
+      if (bdesc.boff) {
+        bdesc.boff[pos] = bdesc.off ? bdesc.off[i] : i * bdesc.stride;
+        bdesc.blen[pos] = len[i];
+      }
     }
     __syncthreads();
     if (threadIdx.x < NB) {
@@ -108,9 +118,22 @@ __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t 
 
 }  // namespace
 
+// scratch: counters (NB x grid), the group table (NB + 1), then (16-byte
+// aligned) the binned descriptors: n u64 offsets and n u16 lengths
+static size_t table_end(int grid) {
+  return ((((size_t)NB * (size_t)grid + NB + 1) * sizeof(uint32_t)) + 15) & ~(size_t)15;
+}
+
 size_t bin_scratch_bytes(uint64_t n, int grid) {
-  (void)n;
-  return ((size_t)NB * (size_t)grid + NB + 1) * sizeof(uint32_t);
+  return table_end(grid) + (size_t)n * (sizeof(uint64_t) + sizeof(uint16_t));
+}
+
+uint64_t *bin_desc_off(void *scratch, int grid) {
+  return (uint64_t *)((uint8_t *)scratch + table_end(grid));
+}
+
+uint16_t *bin_desc_len(void *scratch, int grid, uint64_t n) {
+  return (uint16_t *)(bin_desc_off(scratch, grid) + n);
 }
 
 const uint32_t *bin_table(const void *scratch, int grid) {
@@ -118,7 +141,7 @@ const uint32_t *bin_table(const void *scratch, int grid) {
 }
 
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm, void *scratch,
-                      hipStream_t s, int grid) {
+                      hipStream_t s, int grid, const BinDesc &bdesc) {
   if (n == 0) return hipSuccess;
   const uint64_t per_block = ((n + grid - 1) / grid + BT - 1) / BT * BT;
   const int g = (int)((n + per_block - 1) / per_block);
@@ -127,7 +150,7 @@ hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm, void *scr
   hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, s, counts, (uint32_t)(NB * g),
                      counts + (size_t)NB * grid);
   hipLaunchKernelGGL(bin_scatter, dim3(g), dim3(BT), 0, s, len, n, per_block,
-                     (const uint32_t *)counts, perm);
+                     (const uint32_t *)counts, perm, bdesc);
   return hipGetLastError();
 }
 

@@ -575,10 +575,17 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   const hipStream_t s = (hipStream_t)stream;
-  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid);
+  // the binning also lays the descriptors out in binned order (scratch), so
+  // the group launches stream them instead of gathering them through d_perm
+  BinDesc bd{b->d_off, b->stride, bin_desc_off(d_scratch, kBinGrid),
+             bin_desc_len(d_scratch, kBinGrid, b->n)};
+  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid, bd);
   if (e != hipSuccess) return -EIO;
   RxKArgs a = batch_args(c, b);
   a.perm = d_perm;
+  a.off = bd.boff;
+  a.len = bd.blen;
+  a.by_pos = 1;
   const uint32_t *tab = bin_table(d_scratch, kBinGrid);
   const uint32_t maxlen = b->max_len ? b->max_len : 65535u;
   const int fv = forced_variant(c);
@@ -656,7 +663,8 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *c, const uint16_t *d_len, uint64_t n,
   if (n > 0xffffffffull) return -EINVAL;
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
-  return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, kBinGrid));
+  return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, kBinGrid,
+                            BinDesc{nullptr, 0, nullptr, nullptr}));
 }
 
 static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {

@@ -62,6 +62,9 @@ struct RxKArgs {
   uint64_t stride_g;
   // nullable (GATHER + perm): process perm[*range_lo .. *range_hi) only
   const uint32_t *range_lo, *range_hi;
+  // 1: off/len are indexed by processing position (binned descriptors,
+  // pptk_rx_batch_device_mixed), perm only gives the record index
+  uint32_t by_pos;
   // header rewrite (pptk_tx_rewrite_device): rw[rw_one ? 0 : i], status
   const pptk_rewrite *rw;
   uint32_t rw_one;
@@ -101,10 +104,19 @@ int rx_variant_blocks_per_cu(int variant);
 // bin_table(scratch, grid)[g] is the first position of group g in perm and
 // [kGroups] = n (device memory, written by the launch).
 constexpr int kBinGrid = 2048;   // blocks of the binning sort (scratch layout)
+// Optional binned copy of the descriptors (boff/blen null: perm only).
+struct BinDesc {
+  const uint64_t *off;   // nullable: frame i at i * stride
+  uint64_t stride;
+  uint64_t *boff;        // binned offsets (scratch), or null
+  uint16_t *blen;        // binned lengths (scratch)
+};
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm,
-                      void *scratch, hipStream_t s, int grid);
+                      void *scratch, hipStream_t s, int grid, const BinDesc &bdesc);
 size_t bin_scratch_bytes(uint64_t n, int grid);
 const uint32_t *bin_table(const void *scratch, int grid);
+uint64_t *bin_desc_off(void *scratch, int grid);
+uint16_t *bin_desc_len(void *scratch, int grid, uint64_t n);
 
 // Batched ip_permitted / ipv6_permitted (rx_permit.hip).
 struct PermitArgs {

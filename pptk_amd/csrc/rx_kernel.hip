@@ -408,16 +408,22 @@ __device__ __forceinline__ uint32_t desc_idx(const RxKArgs &a, uint64_t tile, in
 }
 
 template <bool GATHER>
-__device__ __forceinline__ Desc desc_fill(const RxKArgs &a, uint32_t idx) {
+__device__ __forceinline__ Desc desc_fill(const RxKArgs &a, uint32_t idx, uint64_t tile, int lane) {
   Desc d;
   d.idx = idx;
   const uint32_t ic = idx == 0xffffffffu ? 0u : idx;
   if constexpr (GATHER) {
-    const uint64_t o = a.off_ld[ic & a.off_msk];
-    const uint32_t l = a.len_ld[ic & a.len_msk];
+    // descriptors by frame index, or (by_pos) by processing position
+    const uint64_t pos = tile * WAVE + lane;
+    const uint32_t pc = pos < a.n ? (uint32_t)pos : 0u;
+    const uint32_t key = a.by_pos ? pc : ic;
+    const uint64_t o = a.off_ld[key & a.off_msk];
+    const uint32_t l = a.len_ld[key & a.len_msk];
     d.base = o + (uint64_t)ic * a.stride_g;
     d.len = l + a.fixed_g;
   } else {
+    (void)tile;
+    (void)lane;
     d.base = (uint64_t)ic * a.stride;
     d.len = a.fixed_len;
   }
@@ -426,7 +432,7 @@ __device__ __forceinline__ Desc desc_fill(const RxKArgs &a, uint32_t idx) {
 
 template <bool GATHER>
 __device__ __forceinline__ Desc load_desc(const RxKArgs &a, uint64_t tile, int lane) {
-  return desc_fill<GATHER>(a, desc_idx<GATHER>(a, tile, lane));
+  return desc_fill<GATHER>(a, desc_idx<GATHER>(a, tile, lane), tile, lane);
 }
 
 // One round's staged chunks for a team: S chunks per lane + the frame.
@@ -850,6 +856,10 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     if (a.range_lo) {
       const uint32_t lo = *a.range_lo, hi = *a.range_hi;
       a.perm_ld += lo;
+      if (a.by_pos) {
+        a.off_ld += lo;
+        a.len_ld += lo;
+      }
       a.n = hi > lo ? hi - lo : 0;
       // an empty group: perm_ld points one past the permutation, and even
       // the clamped descriptor loads below would read it
@@ -968,7 +978,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // the descriptors two tiles ahead are loaded BEFORE the last group issues
     // the next tile's first D rounds: the copies dc <- dn <- d2 at the tile
     // boundary then wait only for these loads, not for the rounds in flight
-    const Desc d2 = desc_fill<GATHER>(a, idx2);
+    const Desc d2 = desc_fill<GATHER>(a, idx2, tile + 2 * step, lane);
     __builtin_amdgcn_sched_barrier(0);
     group(T - (D + 1));
 

@@ -1,6 +1,7 @@
 """BENCH TOOLING: summarize rocprofv3 runs into profiles/<round>/pmc_summary.json.
 
     python tools/pmc_summary.py OUT.json cfg=DIR_FETCH,DIR_WRITE[,DIR_STATS] ...
+                                         op:NAME:REGEX:CHANGED=DIR_FETCH,DIR_WRITE ...
 
 Per config: average rx_kernel duration from the kernel trace, FETCH_SIZE and
 WRITE_SIZE per launch, and HBM traffic per launch corrected as
@@ -35,9 +36,64 @@ def counter(d, cname):
     return by[name][0], by[name][1], name
 
 
+def op_counter(d, cname, regex):
+    """Per-launch values of the kernels matching `regex` (all of them: an
+    op's launches), and their durations."""
+    import re
+    v, t, names = [], [], set()
+    for r in rows(d, "*counter_collection.csv"):
+        if re.search(regex, r["Kernel_Name"]) and r["Counter_Name"] == cname:
+            v.append(float(r["Counter_Value"]))
+            t.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            names.add(r["Kernel_Name"])
+    return v, t, sorted(names)
+
+
+def op_entry(spec):
+    """op:REGEX:CHANGED_BYTES=DIR_FETCH,DIR_WRITE -- a secondary op's HBM
+    traffic per launch and its write amplification (WRITE_SIZE bytes /
+    bytes the op must change)."""
+    head, dirs = spec.split("=")
+    _, regex, changed = head.split(":")
+    dirs = dirs.split(",")
+    f, fd, names = op_counter(dirs[0], "FETCH_SIZE", regex)
+    w, wd, _ = op_counter(dirs[1], "WRITE_SIZE", regex)
+    if not f or not w:
+        return {"error": "no matching launches", "regex": regex}
+    e = {"launches": len(f), "kernels": names,
+         "hbm_read_bytes": sum(f) / len(f) * 1024 * 2,
+         "hbm_write_bytes": sum(w) / len(w) * 1024,
+         "pmc_pass_kernel_ms": sum(fd + wd) / len(fd + wd)}
+    e["traffic_bytes"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+    # per kernel (an op made of several launches, e.g. the binned path)
+    import re
+    per = {}
+    for cname, key in (("FETCH_SIZE", 0), ("WRITE_SIZE", 1)):
+        for r in rows(dirs[key], "*counter_collection.csv"):
+            if re.search(regex, r["Kernel_Name"]) and r["Counter_Name"] == cname:
+                k = r["Kernel_Name"][:80]
+                p = per.setdefault(k, {"launches": 0, "read": 0.0, "write": 0.0})
+                if key == 0:
+                    p["launches"] += 1
+                    p["read"] += float(r["Counter_Value"]) * 1024 * 2
+                else:
+                    p["write"] += float(r["Counter_Value"]) * 1024
+    e["per_kernel"] = {k: {"launches": v["launches"],
+                           "read_bytes_per_launch": v["read"] / max(1, v["launches"]),
+                           "write_bytes_per_launch": v["write"] / max(1, v["launches"])}
+                       for k, v in per.items()}
+    e["changed_bytes"] = int(changed)
+    e["write_amplification"] = round(e["hbm_write_bytes"] / int(changed), 2)
+    return e
+
+
 def main():
     out = {}
     for arg in sys.argv[2:]:
+        if arg.startswith("op:"):
+            name = arg.split("=")[0].split(":")[1]
+            out["op_" + name] = op_entry("op:" + arg.split(":", 2)[2])
+            continue
         cfg, dirs = arg.split("=")
         dirs = dirs.split(",")
         fetch, fd, fname = counter(dirs[0], "FETCH_SIZE")
