@@ -728,6 +728,18 @@ def main():
         # (a trivial kernel moving the same bytes, tools/rwmix.hip)
         roofline["mix_sol_ms"] = box["mix_ms"]
         roofline["mix_sol_frac"] = round(box["mix_ms"] / kernel_ms, 4)
+        # the best read-roofline fraction ANY kernel moving this launch's
+        # bytes reaches on this GPU: the pool's boxes differ in what the 1 GB
+        # of record writes costs beside the 25 GB read (0.5-1.2 ms), and on
+        # the expensive-write boxes this ceiling itself is below 0.70
+        ceil = bytes_per_launch / (box["mix_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+        roofline["mix_sol_read_frac"] = round(ceil, 4)
+        if roofline["frac"] < 0.70:
+            roofline["below_target_note"] = (
+                f"read-roofline fraction {roofline['frac']} < 0.70 on this GPU: the trivial "
+                f"kernel moving the same bytes reaches only {round(ceil, 4)} here (record "
+                f"writes cost {round(box['mix_ms'] - bytes_per_launch / box.get('read_nt_gbs', 1) / 1e6, 2)} "
+                f"ms beside the read stream); the rx kernel is at {roofline['mix_sol_frac']} of it")
 
     # the same batch with compact 32-byte records (struct pptk_rx_rec32)
     rec32 = None

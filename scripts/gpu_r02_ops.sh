@@ -13,7 +13,7 @@ for op in tx rewrite mss permit binned allgather; do
 done
 N=16777216
 python tools/pmc_summary.py $O/pmc_ops.json \
-  "op:tx:^void pptk::.*rx_kernel:$((4*N))=$O/fetch_tx,$O/write_tx" \
+  "op:tx:rx_kernel:$((4*N))=$O/fetch_tx,$O/write_tx" \
   "op:rewrite:rx_rewrite_kernel:$((17*N))=$O/fetch_rewrite,$O/write_rewrite" \
   "op:mss:rx_mss_kernel:$((4*N))=$O/fetch_mss,$O/write_mss" \
   "op:permit:permit_|rocprim:$N=$O/fetch_permit,$O/write_permit" \

@@ -23,6 +23,46 @@ import bench  # noqa: E402
 N = bench.N_PER_GPU
 
 
+def gather_emul(ctx, dev, n, steps, warmup, world=8):
+    """The HBM side of the C8G all-gather on one GPU: a ring all-gather of
+    n u64 hashes per rank over `world` ranks makes every rank read and write
+    (world - 1) * n * 8 bytes of its HBM per batch (it forwards world - 1
+    chunks and lands world - 1 chunks).  Emulated by a device-to-device copy
+    of that size on a second stream beside every C1500 launch, as bench.py
+    overlaps the real gather; reports the launch rate with and without it.
+    (xGMI link time is not emulated: it overlaps the kernel.)"""
+    import time
+    import torch
+    from tools.synth import make_batch
+    b = make_batch("c1500", n, dev)
+    recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    nbytes = (world - 1) * n * 8
+    src = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    main_s = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    out = {}
+    for mode in ("alone", "with_copy", "alone", "with_copy"):
+        for k in range(warmup + steps):
+            if k == warmup:
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+            ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=recs)
+            if mode == "with_copy":
+                ev = torch.cuda.Event()
+                ev.record(main_s)
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    dst.copy_(src)
+        torch.cuda.synchronize(dev)
+        out.setdefault(mode, []).append((time.perf_counter() - t0) / steps * 1e3)
+    a, w = min(out["alone"]), min(out["with_copy"])
+    return {"ms_per_batch_alone": round(a, 4), "ms_per_batch_with_gather_traffic": round(w, 4),
+            "overlap_loss": round(1 - a / w, 4), "world": world,
+            "gather_bytes_read_and_written_per_rank": nbytes,
+            "changed_bytes_per_launch": 64 * n}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("op")
@@ -69,6 +109,8 @@ def main():
         r = {"kernel_ms": round(res["kernel_ms"], 4), "mpkts": round(res["mpkts"], 1),
              "changed_bytes_per_launch": 64 * n + 8 * n}
         dist.destroy_process_group()
+    elif op == "gather_emul":
+        r = gather_emul(ctx, dev, n, args.steps, args.warmup)
     else:
         raise SystemExit(f"unknown op {op}")
     r["op"] = op

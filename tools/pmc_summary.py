@@ -36,6 +36,39 @@ def counter(d, cname):
     return by[name][0], by[name][1], name
 
 
+def timed_launches(d, name, steps, gap_ms=20.0):
+    """From the kernel trace of the traced bench command: the launches of
+    kernel `name` split into runs (consecutive launches less than gap_ms
+    apart); the first run of 100+ launches is the config's settle + warmup +
+    timed steps, and its last `steps` launches are the ones bench.py timed.
+    Their mean / median duration is the same-run counterpart of the bench
+    line's kernel_ms."""
+    tr = [r for r in rows(d, "*kernel_trace.csv") if r["Kernel_Name"] == name]
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    runs, cur, last_end = [], [], None
+    for r in tr:
+        s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if last_end is not None and (s0 - last_end) / 1e6 > gap_ms:
+            runs.append(cur)
+            cur = []
+        cur.append((e0 - s0) / 1e6)
+        last_end = e0
+    if cur:
+        runs.append(cur)
+    run = next((r for r in runs if len(r) >= 100), max(runs, key=len) if runs else [])
+    if len(run) < steps:
+        return {}
+    t = sorted(run[-steps:])
+    ks = [r for r in rows(d, "*kernel_stats.csv") if r["Name"] == name]
+    out = {"kernel_name": name, "trace_timed_launches": steps,
+           "trace_timed_mean_ms": sum(t) / len(t), "trace_timed_median_ms": t[len(t) // 2],
+           "trace_run_launches": len(run)}
+    if ks:
+        out["kernel_stats_avg_ms_all_launches"] = float(ks[0]["AverageNs"]) / 1e6
+        out["kernel_stats_calls"] = int(ks[0]["Calls"])
+    return out
+
+
 def op_counter(d, cname, regex):
     """Per-launch values of the kernels matching `regex` (all of them: an
     op's launches), and their durations."""
@@ -53,8 +86,9 @@ def op_entry(spec):
     """op:REGEX:CHANGED_BYTES=DIR_FETCH,DIR_WRITE -- a secondary op's HBM
     traffic per launch and its write amplification (WRITE_SIZE bytes /
     bytes the op must change)."""
-    head, dirs = spec.split("=")
-    _, regex, changed = head.split(":")
+    head, dirs = spec.rsplit("=", 1)
+    head, changed = head.rsplit(":", 1)
+    regex = head.split(":", 2)[2]
     dirs = dirs.split(",")
     f, fd, names = op_counter(dirs[0], "FETCH_SIZE", regex)
     w, wd, _ = op_counter(dirs[1], "WRITE_SIZE", regex)
@@ -91,8 +125,7 @@ def main():
     out = {}
     for arg in sys.argv[2:]:
         if arg.startswith("op:"):
-            name = arg.split("=")[0].split(":")[1]
-            out["op_" + name] = op_entry("op:" + arg.split(":", 2)[2])
+            out["op_" + arg.split(":")[1]] = op_entry(arg)
             continue
         cfg, dirs = arg.split("=")
         dirs = dirs.split(",")
@@ -105,12 +138,7 @@ def main():
         e["traffic_bytes"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
         e["pmc_pass_kernel_ms"] = sum(fd + wd) / len(fd + wd)
         if len(dirs) > 2:
-            ks = [r for r in rows(dirs[2], "*kernel_stats.csv") if "rx_kernel" in r["Name"]]
-            ks.sort(key=lambda r: -int(r["Calls"]))
-            if ks:
-                e["kernel_trace_avg_ms"] = float(ks[0]["AverageNs"]) / 1e6
-                e["kernel_trace_calls"] = int(ks[0]["Calls"])
-                e["kernel_name"] = ks[0]["Name"]
+            e.update(timed_launches(dirs[2], fname, int(os.environ.get("PMC_STEPS", "20"))))
         out[cfg] = e
     json.dump(out, open(sys.argv[1], "w"), indent=1)
     print(json.dumps(out, indent=1))
