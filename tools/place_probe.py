@@ -1,0 +1,123 @@
+"""BENCH TOOLING: does the C1500 launch time depend on WHERE the record
+buffer sits in HBM relative to the frame buffer?
+
+    python tools/place_probe.py [--step-mb 16] [--count 32] [--reps 4]
+
+One frame batch; one record pool of 1 GiB + count * step MB; the same
+C1500 launch timed with its records at pool + k * step MB for k in
+0..count-1, interleaved over `reps` rounds (medians).  One JSON line."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def matrix(args):
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    bs = [make_batch("c1500", n, dev), make_batch("c1500", n, dev, first=n)]
+    rs = [torch.zeros((n, 64), dtype=torch.uint8, device=dev) for _ in range(args.matrix)]
+    torch.cuda.synchronize()
+    t = {}
+    for rep in range(args.reps + 1):
+        for bi, b in enumerate(bs):
+            for ri, r in enumerate(rs):
+                a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=r)
+                z.record()
+                torch.cuda.synchronize()
+                if rep:
+                    t.setdefault((bi, ri), []).append(a.elapsed_time(z))
+    m = [[round(sorted(t[(bi, ri)])[len(t[(bi, ri)]) // 2], 3) for ri in range(len(rs))]
+         for bi in range(len(bs))]
+    print(json.dumps({"rx_ms": m, "frames": [hex(b["frames"].data_ptr()) for b in bs],
+                      "recs": [hex(r.data_ptr()) for r in rs]}), flush=True)
+
+
+def policies(args):
+    """The slow (allocated right after the frames) and a fast record buffer,
+    each under every result-preserving store/load policy (PPTK_RX_TUNE_*
+    bits via pptk_rx_set_tuning) and the rwmix speed-of-light kernel's
+    store modes."""
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.rwmix import mix_ms
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    b = make_batch("c1500", n, dev)
+    rs = [torch.zeros((n, 64), dtype=torch.uint8, device=dev) for _ in range(6)]
+    torch.cuda.synchronize()
+    pols = {"nt_ld+nt_st": 0x21, "nt_ld+wb_st": 0x1, "nt_ld+sc1_st": 0x41, "wb_ld+nt_st": 0x20,
+            "nt_ld+nt_st+blocked": 0x121, "nt_ld+lane_st": 0x23}
+    t = {}
+    for rep in range(args.reps + 1):
+        for ri in (0, 1, 5):
+            for name, fl in pols.items():
+                ctx.set_tuning(-1, fl)
+                a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=rs[ri])
+                z.record()
+                torch.cuda.synchronize()
+                if rep:
+                    t.setdefault(f"r{ri}/{name}", []).append(a.elapsed_time(z))
+    out = {k: round(sorted(v)[len(v) // 2], 3) for k, v in t.items()}
+    for ri in (0, 1, 5):
+        for nt in (0, 1, 3, 9):
+            out[f"r{ri}/rwmix_nt{nt}"] = round(mix_ms(b["frames"], 96000, n // 64, rs[ri], 4096,
+                                                      nt=nt), 3)
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--step-mb", type=float, default=16)
+    ap.add_argument("--count", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--n", type=int, default=16 * 1024 * 1024)
+    ap.add_argument("--matrix", type=int, default=0,
+                    help="instead: 2 frame batches x this many separate 1 GiB record buffers")
+    ap.add_argument("--policies", action="store_true")
+    args = ap.parse_args()
+    if args.matrix:
+        return matrix(args)
+    if args.policies:
+        return policies(args)
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    b = make_batch("c1500", n, dev)
+    step = int(args.step_mb * (1 << 20)) // 64 * 64
+    pool = torch.zeros(n * 64 + step * args.count + 64, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t = {}
+    for rep in range(args.reps + 1):
+        for k in range(args.count):
+            r = pool[k * step: k * step + n * 64].view(n, 64)
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=r)
+            z.record()
+            torch.cuda.synchronize()
+            if rep:
+                t.setdefault(k, []).append(a.elapsed_time(z))
+    med = [round(sorted(v)[len(v) // 2], 3) for _, v in sorted(t.items())]
+    print(json.dumps({"step_bytes": step, "rx_ms": med, "frames": hex(b["frames"].data_ptr()),
+                      "pool": hex(pool.data_ptr())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
