@@ -837,6 +837,11 @@ def main():
         print(json.dumps(line), flush=True)
     if dist_on(ws):
         import torch.distributed as dist
+        # every rank tears its RCCL communicator down at the same point,
+        # after the last collective, before the control plane goes away
+        barrier(ws, dev)
+        if gbs:
+            ctx.comm_destroy()
         dist.destroy_process_group()
 
 

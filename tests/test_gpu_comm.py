@@ -140,3 +140,34 @@ def test_entry_points_restore_callers_device(dev):
     assert hip.hipGetDevice(ctypes.byref(cur)) == 0 and cur.value == 0
     assert lib().pptk_rx_device_count() >= 1
     ctx.close()
+
+
+@pytest.mark.parametrize("frames,scaling", [(1 << 20, "weak"), ((1 << 20) + 77, "strong")])
+def test_bench_one_rank_rccl_path(tmp_path, frames, scaling):
+    """bench.py's multi-GPU path end to end on one GPU (PPTK_BENCH_FORCE_DIST:
+    a one-rank RCCL communicator through the C-ABI, the gloo control plane,
+    the double-buffered in-place gather on a second stream, the gathered-hash
+    parity check), small batch; strong scaling with a frame count that is not
+    a multiple of 64."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, PPTK_BENCH_FORCE_DIST="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(29600 + os.getpid() % 300))
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--frames", str(frames),
+                          "--scaling", scaling, "--steps", "3", "--warmup", "1", "--no-secondary",
+                          "--no-cpu", "--no-rec32", "--no-membench", "--settle", "0.1"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["config"]["rccl_ranks"] == 1
+    assert line["config"]["global_frames"] == frames
+    g = line["allgather"]
+    assert g["rccl_ranks"] == 1 and g["bytes_per_rank"] == frames * 8
+    assert g["gathered_check"]["own_slice_equals_records"]
+    assert g["gathered_check"]["sampled_mismatches"] == 0
+    p = line["parity"]
+    assert p["oracle_sample"]["mismatches"] == 0 and all(
+        v for k, v in p["full_batch"].items() if k != "corrupted")
