@@ -410,17 +410,18 @@ def test_host_batch_worker_pool_large_chunks(cfg, dev):
     """Chunks big enough that the worker pool splits both the frame gather
     and the record copy-out (>= 2 MiB of records per chunk), over repeated
     calls on one context and then from two contexts on two host threads at
-    once: every record equals the device-resident path's."""
+    once: every record equals the CPU oracle's."""
     import threading
+    from oracle.oracle import Oracle, make_opts
     from pptk_amd.rx import RxContext, ldp_packets
     from tools.synth import make_batch
     n = 200_000 if cfg == "c64" else 70_000
     b = make_batch(cfg, n, dev)
     stride = b["stride"]
     ring = b["frames"][: n * stride + 64].cpu().numpy()
-    ref = RxContext(0, bytes(range(1, 17))).batch_device(b["frames"], n, stride=stride,
-                                                         fixed_len=b["fixed_len"])
-    want = ref.cpu().numpy().reshape(-1).view(np.uint8).reshape(n, 64)
+    want = Oracle().rx_batch(ring, None, None, stride=stride, fixed_len=b["fixed_len"], n=n,
+                             opts=make_opts(bytes(range(1, 17))), nthreads=8)
+    want = want.view(np.uint8).reshape(n, 64)
     pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
                        np.full(n, b["fixed_len"], np.uint16))
     ctxs = [RxContext(0, bytes(range(1, 17)), max_batch=65536, max_frame=1518,
@@ -475,16 +476,24 @@ def test_large_fresh_batches_vs_oracle(seed, oracle_lib, dev):
 @pytest.mark.parametrize("layout", ["fixed", "offsets"])
 def test_autotune_keeps_records(layout, dev):
     """pptk_rx_autotune picks one of the interchangeable shapes for a
-    C1500-class batch; later batches launch it and their records are the
-    automatic variant's, bit for bit."""
+    C1500-class batch; later batches launch it and their records equal the
+    CPU oracle's, bit for bit."""
+    from oracle.oracle import Oracle, make_opts
     from pptk_amd.rx import RxContext, VARIANTS
     from tools.synth import make_batch
     n = 1 << 17
     b = make_batch("c1500" if layout == "fixed" else "cmix", n, dev)
     kw = (dict(stride=b["stride"], fixed_len=b["fixed_len"]) if "off" not in b else
           dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]))
-    ref = RxContext(0, bytes(range(1, 17)))
-    want = ref.batch_device(b["frames"], n, **kw).cpu()
+    host = b["frames"].cpu().numpy()
+    opts = make_opts(bytes(range(1, 17)))
+    if "off" in b:
+        w = Oracle().rx_batch(host, b["off"].cpu().numpy().view(np.uint64),
+                              b["lens"].cpu().numpy().view(np.uint16), opts=opts, nthreads=8)
+    else:
+        w = Oracle().rx_batch(host, None, None, stride=b["stride"], fixed_len=b["fixed_len"],
+                              n=n, opts=opts, nthreads=8)
+    want = torch.from_numpy(w.view(np.uint8).reshape(n, 64).copy())
     ctx = RxContext(0, bytes(range(1, 17)))
     name = ctx.autotune(b["frames"], n, reps=2, **kw)
     assert name in ("T16S6", "T32S3", "T32S3D7", "T16S7L")
@@ -496,3 +505,40 @@ def test_autotune_keeps_records(layout, dev):
     ctx.batch_device(b["frames"], n, **kw)
     torch.cuda.synchronize()
     assert VARIANTS[ctx._L.pptk_rx_last_variant(ctx._ctx)] == "T16S2"
+
+
+def test_host_batch_error_paths(dev):
+    """pptk_rx_batch's per-packet and contract error paths on hardware: a
+    NULL frame pointer comes back MALFORMED-only (no fault, no error), the
+    other frames of the batch are exact; a NULL packet table or record array
+    with num > 0 and a negative num are -EINVAL; num == 0 is a no-op; an
+    unknown ring cannot be unregistered; a batch still works afterwards."""
+    import ctypes
+    from pptk_amd.records import F_MALFORMED
+    from pptk_amd.rx import ldp_packets
+    z = load_golden("cmix")
+    ctx = _ctx(z)
+    buf = np.ascontiguousarray(z["buf"])
+    pkts = ldp_packets(buf, z["off"], z["len"])
+    holes = [0, 7, len(pkts) - 1]
+    for i in holes:
+        pkts[i].data = None
+    got = ctx.batch_host(pkts)
+    want = np.array(z["recs"]).reshape(-1).view(np.uint8).reshape(-1, 64).copy()
+    from pptk_amd.records import as_records
+    for i in holes:
+        assert got["flags"][i] == F_MALFORMED
+    keep = np.setdiff1d(np.arange(len(pkts)), holes)
+    assert not diff_records(got[keep], as_records(want)[keep])
+    L, c = ctx._L, ctx._ctx
+    recs = np.zeros(4, dtype=got.dtype)
+    rp = ctypes.c_void_p(recs.ctypes.data)
+    assert L.pptk_rx_batch(c, None, 4, rp) == -22
+    assert L.pptk_rx_batch(c, ctypes.cast(pkts, ctypes.c_void_p), 4, None) == -22
+    assert L.pptk_rx_batch(c, ctypes.cast(pkts, ctypes.c_void_p), -1, rp) == -22
+    assert L.pptk_rx_batch(c, None, 0, None) == 0
+    other = np.zeros(4096, np.uint8)
+    assert L.pptk_rx_unregister_ring(c, ctypes.c_void_p(other.ctypes.data)) == -22
+    pkts2 = ldp_packets(buf, z["off"][:64], z["len"][:64])
+    assert not diff_records(ctx.batch_host(pkts2), z["recs"][:64])
+    ctx.close()
