@@ -120,8 +120,37 @@ def gather_bw(per, ws, seconds):
     return round(alg, 1), round(alg * (ws - 1) / ws, 1)
 
 
+PLACE_CANDIDATES = 6
+
+
+def placed_records(ctx, b, n, dev, compact, kw, ncand=PLACE_CANDIDATES, spacer=None):
+    """The record buffer, placed (pptk_rx_place_records): ncand candidate
+    buffers allocated with `spacer` bytes (default 4x the buffer, 256 MiB ..
+    4 GiB) allocated between consecutive ones, so that they land apart in
+    HBM; the batch timed into each, the fastest kept.  Returns (recs,
+    placement report)."""
+    import torch
+    rb = 32 if compact else 64
+    if spacer is None:
+        spacer = min(4 << 30, max(256 << 20, 4 * n * rb))
+    free, _ = torch.cuda.mem_get_info(dev)
+    while ncand > 1 and ncand * n * rb + (ncand - 1) * spacer > 0.6 * free:
+        ncand -= 1
+    cands, spacers = [], []
+    for k in range(ncand):
+        if k:
+            spacers.append(torch.empty(spacer, dtype=torch.uint8, device=dev))
+        cands.append(torch.empty((n, rb), dtype=torch.uint8, device=dev))
+    best, ms = ctx.place_records(b["frames"], n, cands, compact=compact, **kw)
+    recs = cands[best]
+    del cands, spacers
+    torch.cuda.empty_cache()
+    return recs, {"candidates": ncand, "spacer_bytes": spacer, "candidate_ms": ms,
+                  "chosen": best}
+
+
 def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SETTLE_S,
-               compact=False, batch=None, autotune=True, first=None):
+               compact=False, batch=None, autotune=True, first=None, place=True):
     """Generate this rank's shard of config `cfg` (n frames from global frame
     `first`, default rank * n) or reuse `batch`, time `steps` launches.
     gbs: two shard.GatherBuffer (double-buffered all-gather of the flow
@@ -132,13 +161,21 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
     first = rank * n if first is None else first
     b = batch if batch is not None else make_batch(cfg, n, dev, first=first)
     torch.cuda.synchronize(dev)
-    recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
     if "off" in b:
         # mixed sizes: per-frame offset/length arrays, frames in batch order
         # (the binned order is measured separately: DESIGN.md)
         kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
     else:
         kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
+    placement = None
+    if place:
+        # where the record buffer sits relative to the frames changes what
+        # the memory charges for the record writes by up to 25 % (DESIGN.md
+        # section 7): pick a well-placed buffer, untimed, as a long-lived
+        # rx ring would be allocated once
+        recs, placement = placed_records(ctx, b, n, dev, compact, kw)
+    else:
+        recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
     if autotune:
         # pick this GPU's fastest interchangeable kernel shape for the batch
         # (pptk_rx_autotune: results identical, untimed, before the settle)
@@ -208,7 +245,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
     res = {
         "n": n, "bytes": b["bytes"], "rec_bytes": n * (32 if compact else 64), "wall_s": wall,
         "ms_per_step": wall / steps * 1e3, "kernel_ms": kernel_ms,
-        "mpkts": n_all * steps / wall / 1e6, "variant": variant,
+        "mpkts": n_all * steps / wall / 1e6, "variant": variant, "placement": placement,
     }
     # size-independent parity on the full batch: every frame parsed, and the
     # checksum verdicts equal what the generator planted
@@ -321,7 +358,8 @@ def summary(r, n):
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                          "rw_achieved": round(rw, 1), "rw_frac": round(rw / HBM_PEAK_GBS, 4)},
             "full_batch_check": r.get("full_batch_check"),
-            "oracle_sample": r.get("oracle_sample")}
+            "oracle_sample": r.get("oracle_sample"),
+            "record_placement": r.get("placement")}
 
 
 def oracle_sample(b, recs, n, dev, k=4096, compact=False):
@@ -662,6 +700,8 @@ def main():
                     help="skip the in-process HBM read/copy ceiling probe")
     ap.add_argument("--settle", type=float, default=SETTLE_S,
                     help="seconds of untimed launches before the warmup steps")
+    ap.add_argument("--no-place", action="store_true",
+                    help="one record buffer as allocated, no placement probe")
     args = ap.parse_args()
     launch_ranks(sys.argv[1:], args.gpus)
 
@@ -683,15 +723,16 @@ def main():
     check = not args.no_check
 
     primary_cfg = args.only or "c1500"
+    place = not args.no_place
     prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, gbs, check,
-                      args.settle, first=first)
+                      args.settle, first=first, place=place)
     log(f"[rank {rank}] {primary_cfg}: {prim['mpkts']:.1f} Mpkts/s, kernel {prim['kernel_ms']:.3f} ms")
     nog = gat = None
     if gbs:
         # same launches without the collective: the kernel-only duration the
         # roofline uses, and the rate "without the gather" 
         nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None, False,
-                         args.settle, batch=prim["_batch"], first=first)
+                         args.settle, batch=prim["_batch"], first=first, place=place)
         del nog["_batch"], nog["_recs"]
         nog["mpkts"] = n_total * args.steps / nog["wall_s"] / 1e6
         gat = gather_bench(ctx, gbs[0], ws, dev, args.steps)
@@ -745,7 +786,8 @@ def main():
     rec32 = None
     if not args.no_rec32:
         r32 = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None,
-                         check, args.settle, compact=True, batch=prim["_batch"], first=first)
+                         check, args.settle, compact=True, batch=prim["_batch"], first=first,
+                         place=place)
         rec32 = summary(r32, n)
         del r32["_batch"], r32["_recs"]
         log(f"[rank {rank}] {primary_cfg} rec32: {rec32['value']} Mpkts/s")
@@ -769,7 +811,7 @@ def main():
     if not args.no_secondary and args.only is None:
         for cfg in ("c64", "cmix"):
             r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None, check,
-                           args.settle, first=first)
+                           args.settle, first=first, place=place)
             secondary[cfg] = summary(r, n)
             if not args.no_membench:
                 sol = mix_sol(r["_batch"], r["_recs"], n)
@@ -781,7 +823,8 @@ def main():
                                                         args.warmup)
             if cfg == "c64" and not args.no_rec32:
                 r32 = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None,
-                                 check, args.settle, compact=True, batch=r["_batch"], first=first)
+                                 check, args.settle, compact=True, batch=r["_batch"], first=first,
+                                 place=place)
                 secondary[cfg]["rec32"] = summary(r32, n)
                 del r32["_batch"], r32["_recs"]
             if cfg == "c64" and rank == 0 and ws == 1 and not args.no_cpu:
@@ -822,6 +865,7 @@ def main():
                        "rccl_ranks": ctx.comm_info()[0] if gbs else None,
                        "key": "01..10"},
             "roofline": roofline,
+            "record_placement": prim.get("placement"),
             "cpu_baseline": cpu,
             "value_no_gather": None if nog is None else round(nog["mpkts"], 1),
             "rec32": rec32,

@@ -399,6 +399,23 @@ void pptk_rx_shard_range(uint64_t n, int nranks, int rank, uint64_t *first, uint
 int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint64_t n,
                            uint64_t *d_out, void *stream);
 
+/* Record-buffer placement.  What the memory charges for the record writes
+ * beside the frame-read stream depends on where the record buffer sits
+ * physically relative to the frame buffer: the same launch into two 1 GiB
+ * record buffers allocated at different moments can take 4.15 or 5.13 ms
+ * (C1500), with identical bytes moved.  For long-lived
+ * rings: allocate a few candidate record buffers (any allocator; spread
+ * apart, e.g. with a few GB allocated between them), and let this run the
+ * batch `b` into each (`reps` timed launches after one warm-up, candidates
+ * interleaved) and return in *best the index of the fastest; keep that one,
+ * free the others.  The candidates replace b->d_recs (or b->d_recs32 for a
+ * compact batch) and receive the batch's records; everything else of `b` is
+ * used as given.  Synchronous; ncand 1..64, reps 1..100.  ms (nullable)
+ * receives each candidate's median launch time. */
+int pptk_rx_place_records(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *b,
+                          void *const *d_cands, int ncand, int reps, int *best, float *ms,
+                          void *stream);
+
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);
 

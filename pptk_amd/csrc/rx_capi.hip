@@ -476,6 +476,65 @@ int pptk_rx_autotune(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b, i
   return rc;
 }
 
+int pptk_rx_place_records(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
+                          void *const *cands, int ncand, int reps, int *best, float *ms_out,
+                          void *stream) {
+  if (!c || !b || !cands || !best || ncand < 1 || ncand > 64 || reps < 1 || reps > 100)
+    return -EINVAL;
+  for (int k = 0; k < ncand; ++k)
+    if (!cands[k]) return -EINVAL;
+  pptk_rx_dev_batch t = *b;
+  const bool c32 = b->d_recs32 != nullptr;
+  t.d_recs = c32 ? nullptr : (pptk_rx_rec *)cands[0];
+  t.d_recs32 = c32 ? (pptk_rx_rec32 *)cands[0] : nullptr;
+  int rc = check_batch(c, &t);
+  if (rc || b->n == 0) {
+    if (rc == 0) *best = 0;
+    return rc;
+  }
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return -EIO;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  std::vector<std::vector<float>> ms((size_t)ncand);
+  // candidates interleaved round by round, so that clock drift during the
+  // probe falls on all of them alike; round 0 is the warm-up
+  for (int r = 0; r <= reps && rc == 0; ++r) {
+    for (int k = 0; k < ncand && rc == 0; ++k) {
+      if (c32) t.d_recs32 = (pptk_rx_rec32 *)cands[k];
+      else t.d_recs = (pptk_rx_rec *)cands[k];
+      if (hipEventRecord(e0, s) != hipSuccess) rc = -EIO;
+      if (rc == 0) rc = pptk_rx_batch_device(c, &t, stream);
+      if (rc == 0 && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess))
+        rc = -EIO;
+      float x = 0.f;
+      if (rc == 0 && r > 0 && hipEventElapsedTime(&x, e0, e1) == hipSuccess)
+        ms[(size_t)k].push_back(x);
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc) return rc;
+  int bi = 0;
+  float bm = 1e30f;
+  for (int k = 0; k < ncand; ++k) {
+    std::vector<float> &v = ms[(size_t)k];
+    std::sort(v.begin(), v.end());
+    const float med = v.empty() ? 1e30f : v[v.size() / 2];
+    if (ms_out) ms_out[k] = med;
+    if (med < bm) {
+      bm = med;
+      bi = k;
+    }
+  }
+  *best = bi;
+  return 0;
+}
+
 int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,
                          const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
                          uint64_t n, uint32_t max_len, void *stream) {

@@ -46,7 +46,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_rewrite_device",
-           "pptk_tcp_mss_clamp_device", "pptk_rx_autotune",
+           "pptk_tcp_mss_clamp_device", "pptk_rx_autotune", "pptk_rx_place_records",
            # multi-GPU (RCCL)
            "pptk_rx_device_count", "pptk_rx_comm_uid", "pptk_rx_comm_create",
            "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
@@ -98,6 +98,12 @@ def lib(path=None):
         if hasattr(L, "pptk_rx_autotune"):             # absent from older A/B builds
             L.pptk_rx_autotune.argtypes = [vp, ctypes.POINTER(RxDevBatch), ctypes.c_int, vp]
             L.pptk_rx_autotune.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_place_records"):        # absent from older A/B builds
+            L.pptk_rx_place_records.argtypes = [vp, ctypes.POINTER(RxDevBatch), ctypes.POINTER(vp),
+                                                ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_float), vp]
+            L.pptk_rx_place_records.restype = ctypes.c_int
         if hasattr(L, "pptk_tcp_mss_clamp_device"):    # absent from older A/B builds
             L.pptk_tcp_mss_clamp_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64,
                                                     ctypes.c_uint32, ctypes.c_uint64,
@@ -246,6 +252,26 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_autotune failed ({rc})")
         return self.tuned_variant(frames, n, off, lens, stride, fixed_len, max_len, compact)
+
+    def place_records(self, frames, n, cands, off=None, lens=None, stride=0, fixed_len=0,
+                      max_len=0, compact=False, reps=3, stream=None):
+        """pptk_rx_place_records: run the batch into each candidate record
+        buffer (torch uint8 CUDA tensors of n x 64 or n x 32 bytes) and
+        return (index of the fastest, per-candidate median ms)."""
+        import torch
+        arr = (ctypes.c_void_p * max(1, len(cands)))(*[t.data_ptr() for t in cands])
+        c0 = cands[0].data_ptr() if cands else None
+        b = RxDevBatch(frames.data_ptr(), None if off is None else off.data_ptr(),
+                       None if lens is None else lens.data_ptr(), None, stride, fixed_len,
+                       max_len, n, None if compact else c0, None, c0 if compact else None)
+        best = ctypes.c_int(-1)
+        ms = (ctypes.c_float * max(1, len(cands)))()
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = self._L.pptk_rx_place_records(self._ctx, ctypes.byref(b), arr, len(cands), reps,
+                                           ctypes.byref(best), ms, ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_place_records failed ({rc})")
+        return best.value, [round(x, 4) for x in ms[:len(cands)]]
 
     def tuned_variant(self, frames, n, off=None, lens=None, stride=0, fixed_len=0, max_len=0,
                       compact=False):

@@ -542,3 +542,29 @@ def test_host_batch_error_paths(dev):
     pkts2 = ldp_packets(buf, z["off"][:64], z["len"][:64])
     assert not diff_records(ctx.batch_host(pkts2), z["recs"][:64])
     ctx.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_place_records(compact, dev):
+    """pptk_rx_place_records runs the batch into every candidate record
+    buffer, returns the fastest's index and per-candidate times; every
+    candidate holds the exact records afterwards."""
+    z = load_golden("cmix")
+    n = len(z["off"])
+    ctx = _ctx(z)
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    rb = 32 if compact else 64
+    cands = [torch.zeros((n, rb), dtype=torch.uint8, device=dev) for _ in range(3)]
+    best, ms = ctx.place_records(frames, n, cands, off=off, lens=lens, max_len=1500,
+                                 compact=compact, reps=2)
+    assert 0 <= best < 3 and len(ms) == 3 and ms[best] == min(ms) and all(m > 0 for m in ms)
+    want = to_rec32(z["recs"]) if compact else z["recs"]
+    for c in cands:
+        d = diff_records(c.cpu().numpy().reshape(-1), want,
+                         dtype=REC32_DTYPE if compact else as_records(z["recs"]).dtype)
+        assert not d, d
+    with pytest.raises(OSError):
+        ctx.place_records(frames, n, [], off=off, lens=lens)
+    ctx.close()

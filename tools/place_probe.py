@@ -22,7 +22,9 @@ def matrix(args):
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
-    bs = [make_batch("c1500", n, dev), make_batch("c1500", n, dev, first=n)]
+    bs = [make_batch("c1500", n, dev)]
+    if args.batches > 1:
+        bs.append(make_batch("c1500", n, dev, first=n))
     rs = [torch.zeros((n, 64), dtype=torch.uint8, device=dev) for _ in range(args.matrix)]
     torch.cuda.synchronize()
     t = {}
@@ -79,6 +81,42 @@ def policies(args):
     print(json.dumps(out), flush=True)
 
 
+def orders(args):
+    """Allocation-order experiment: a record buffer allocated BEFORE the
+    frame batch, six after it, and one arena holding both (frames copied
+    into its first 24 GB, records right after) -- which placements are
+    slow, and is any allocation strategy reliably fast?"""
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    rb = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    b = make_batch("c1500", n, dev)
+    ra = [torch.zeros((n, 64), dtype=torch.uint8, device=dev) for _ in range(6)]
+    fb = n * 1500
+    arena = torch.empty(fb + 64 + n * 64 + (2 << 20), dtype=torch.uint8, device=dev)
+    arena[:fb + 64].copy_(b["frames"][:fb + 64])
+    off = (fb + 64 + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+    arec = arena[off:off + n * 64].view(n, 64)
+    torch.cuda.synchronize()
+    cases = {"before": (b["frames"], rb), "arena": (arena, arec)}
+    cases.update({f"after{k}": (b["frames"], r) for k, r in enumerate(ra)})
+    cases["arena_frames+before"] = (arena, rb)
+    t = {}
+    for rep in range(args.reps + 1):
+        for name, (fr, r) in cases.items():
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ctx.batch_device(fr, n, stride=1500, fixed_len=1500, recs=r)
+            z.record()
+            torch.cuda.synchronize()
+            if rep:
+                t.setdefault(name, []).append(a.elapsed_time(z))
+    print(json.dumps({k: round(sorted(v)[len(v) // 2], 3) for k, v in t.items()}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-mb", type=float, default=16)
@@ -88,11 +126,15 @@ def main():
     ap.add_argument("--matrix", type=int, default=0,
                     help="instead: 2 frame batches x this many separate 1 GiB record buffers")
     ap.add_argument("--policies", action="store_true")
+    ap.add_argument("--orders", action="store_true")
+    ap.add_argument("--batches", type=int, default=2)
     args = ap.parse_args()
     if args.matrix:
         return matrix(args)
     if args.policies:
         return policies(args)
+    if args.orders:
+        return orders(args)
     import torch
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch
