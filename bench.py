@@ -316,12 +316,14 @@ def mix_sol(b, recs, n):
     return round(ms, 4), f"{ntiles} tiles x {rb} B read + {wb} B written, grid-strided, no compute"
 
 
-def binned_bench(ctx, b, n, dev, steps, warmup):
+def binned_bench(ctx, b, n, dev, steps, warmup, recs=None):
     """The binned CMIX path BASELINE.json names (configs[3], "lanes binned
     by length"): pptk_rx_batch_device_mixed -- the device length binning
-    plus one launch per length group -- timed per batch, whole call."""
+    plus one launch per length group -- timed per batch, whole call (into
+    `recs`, the batch-order run's placed record buffer, when given)."""
     import torch
-    recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    if recs is None:
+        recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     perm = torch.empty(n, dtype=torch.int32, device=dev)
     scratch = torch.empty(ctx._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8, device=dev)
     kw = dict(max_len=b["max_len"], recs=recs, perm=perm, scratch=scratch)
@@ -820,7 +822,7 @@ def main():
                     secondary[cfg]["roofline"]["mix_sol_frac"] = round(sol[0] / r["kernel_ms"], 4)
             if cfg == "cmix":
                 secondary[cfg]["binned"] = binned_bench(ctx, r["_batch"], n, dev, args.steps,
-                                                        args.warmup)
+                                                        args.warmup, recs=r["_recs"])
             if cfg == "c64" and not args.no_rec32:
                 r32 = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None,
                                  check, args.settle, compact=True, batch=r["_batch"], first=first,
