@@ -120,19 +120,20 @@ def gather_bw(per, ws, seconds):
     return round(alg, 1), round(alg * (ws - 1) / ws, 1)
 
 
-PLACE_CANDIDATES = 6
+PLACE_CANDIDATES = 8
 
 
 def placed_records(ctx, b, n, dev, compact, kw, ncand=PLACE_CANDIDATES, spacer=None):
     """The record buffer, placed (pptk_rx_place_records): ncand candidate
-    buffers allocated with `spacer` bytes (default 4x the buffer, 256 MiB ..
-    4 GiB) allocated between consecutive ones, so that they land apart in
-    HBM; the batch timed into each, the fastest kept.  Returns (recs,
-    placement report)."""
+    buffers allocated with `spacer` bytes (default 6x the buffer, 256 MiB ..
+    6 GiB) allocated between consecutive ones, so that they land apart in
+    HBM (the slow and fast placements come in runs of several GB,
+    DESIGN.md section 7); the batch timed into each, the fastest kept.
+    Returns (recs, placement report)."""
     import torch
     rb = 32 if compact else 64
     if spacer is None:
-        spacer = min(4 << 30, max(256 << 20, 4 * n * rb))
+        spacer = min(6 << 30, max(256 << 20, 6 * n * rb))
     free, _ = torch.cuda.mem_get_info(dev)
     while ncand > 1 and ncand * n * rb + (ncand - 1) * spacer > 0.6 * free:
         ncand -= 1

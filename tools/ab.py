@@ -10,6 +10,7 @@ lib names come from AB_LIBS (name=path,...), default = pptk_amd/libpptkrx.so.
 Generates the batch once, then times every setting in interleaved rounds
 (A B C A B C ...) so that clock and thermal drift hit all settings alike;
 prints one JSON line with the median kernel ms and GB/s per setting.
+AB_PLACE=1 times into placed record buffers (bench.placed_records).
 AB_BIN=1 processes mixed batches in length-binned order (pptk_rx_bin_device,
 timed inside each launch's window); AB_MIXED=1 through
 pptk_rx_batch_device_mixed (binning + one launch per length group)."""
@@ -53,9 +54,16 @@ def main():
     b = make_batch(cfg, n, dev)
     kw = (dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]) if "off" in b
           else dict(stride=b["stride"], fixed_len=b["fixed_len"]))
-    recs64 = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-    recs32 = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     ctxs = {k: RxContext(0, bytes(range(1, 17)), lib_path=v) for k, v in libs.items()}
+    placement = None
+    if os.environ.get("AB_PLACE"):
+        # well-placed record buffers (bench.placed_records), as bench.py uses
+        import bench
+        recs64, placement = bench.placed_records(ctxs[""], b, n, dev, False, kw)
+        recs32, _ = bench.placed_records(ctxs[""], b, n, dev, True, kw)
+    else:
+        recs64 = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        recs32 = torch.empty((n, 32), dtype=torch.uint8, device=dev)
 
     mixed = bool(os.environ.get("AB_MIXED")) and "off" in b
     if mixed:
@@ -96,7 +104,7 @@ def main():
                 torch.cuda.synchronize()
                 times[s].append(e0.elapsed_time(e1))
     out = {"cfg": cfg, "frames": n, "binned": binned, "mixed": mixed,
-           "box": measure(b["frames"])}
+           "box": measure(b["frames"]), "placement": placement}
     for s, t in times.items():
         ms = float(np.median(t))
         key = ":".join(str(x) for x in s[:3] if x != "") + (":c" if s[3] else "")
