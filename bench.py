@@ -120,7 +120,7 @@ def gather_bw(per, ws, seconds):
     return round(alg, 1), round(alg * (ws - 1) / ws, 1)
 
 
-PLACE_CANDIDATES = 8
+PLACE_CANDIDATES = 12
 
 
 def placed_records(ctx, b, n, dev, compact, kw, ncand=PLACE_CANDIDATES, spacer=None):

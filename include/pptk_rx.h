@@ -204,8 +204,11 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *ctx, const uint16_t *d_len,
  * b->d_perm is ignored (d_perm receives the processing order).  b->max_len
  * (when nonzero) is a hint: the groups above it are folded into the group
  * that holds it (one launch fewer each; a wrong hint changes speed only).
- * Records land at d_recs[i] for frame i.  d_perm holds n u32, d_scratch pptk_rx_bin_scratch_bytes(n)
- * bytes; both stay in use until the stream reaches the end of the call. */
+ * Records land at d_recs[i] for frame i.  d_perm holds n u32, d_scratch
+ * pptk_rx_bin_scratch_bytes(n) bytes (the binning's counters and group table,
+ * and the frames' descriptors laid out in binned order, which the group
+ * launches stream); both stay in use until the stream reaches the end of
+ * the call. */
 int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *ctx,
                                const struct pptk_rx_dev_batch *b, uint32_t *d_perm,
                                void *d_scratch, void *stream);
