@@ -11,7 +11,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -160,7 +159,6 @@ void **ctx_comm_slot(pptk_rx_ctx *c) { return &c->comm; }
 
 static int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
 
-
 // An integer environment knob, read once (the callers keep it in a function-
 // local static: initialised once, thread-safe, as rx threads may race on
 // their first batches).
@@ -282,11 +280,6 @@ static int pick_variant(uint32_t span) {
   return RX_T64S2;
 }
 
-// Memory policy (PPTK_RX_TUNE_*), from in-process A/B runs (DESIGN.md
-// "Measurement log"): non-temporal record stores always (C64 0.468 -> 0.463
-// ms, CMIX 3.05 -> 2.97 ms); non-temporal frame loads only for fixed-stride
-// batches with the streaming variants (C1500 4.47 -> 4.25 ms; they cost 14 %
-// on C64 and 10 % on offset-described CMIX).  PPTK_RX_TUNE overrides.
 // The result-preserving memory-policy bits (pptk_rx.h).  The kernels also
 // know diagnostic bits that skip work (record stores, the per-frame phase,
 // half the record bytes, tx writes) for profiling; they are accepted only by
@@ -300,6 +293,11 @@ static constexpr uint32_t kTuneMask = PPTK_RX_TUNE_NT_LOADS | PPTK_RX_TUNE_NO_ST
                                       PPTK_RX_TUNE_BLOCKED;
 #endif
 
+// Memory policy (PPTK_RX_TUNE_*), from in-process A/B runs (DESIGN.md
+// "Measurement log"): non-temporal record stores always (C64 0.468 -> 0.463
+// ms, CMIX 3.05 -> 2.97 ms); non-temporal frame loads only for fixed-stride
+// batches with the streaming variants (C1500 4.47 -> 4.25 ms; they cost 14 %
+// on C64 and 10 % on offset-described CMIX).  PPTK_RX_TUNE overrides.
 static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
   static const long tune = env_long("PPTK_RX_TUNE", -1);
   if (c->forced_flags >= 0) return (uint32_t)c->forced_flags & kTuneMask;

@@ -568,3 +568,18 @@ def test_place_records(compact, dev):
     with pytest.raises(OSError):
         ctx.place_records(frames, n, [], off=off, lens=lens)
     ctx.close()
+
+
+def test_tuning_rejects_diagnostic_bits(dev):
+    """The product library accepts only the result-preserving tuning bits:
+    the diagnostic ones (skip record stores 0x8, skip the per-frame phase
+    0x10, half the record bytes 0x80, skip tx writes 0x200) are -EINVAL."""
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    for bad in (0x8, 0x10, 0x80, 0x200, 0x21 | 0x8):
+        with pytest.raises(OSError) as e:
+            ctx.set_tuning(-1, bad)
+        assert e.value.errno == 22
+    for good in (0x1, 0x2, 0x20, 0x40, 0x100, 0x163):
+        ctx.set_tuning(-1, good)
+    ctx.close()
