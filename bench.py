@@ -773,9 +773,10 @@ def main():
         roofline["mix_sol_ms"] = box["mix_ms"]
         roofline["mix_sol_frac"] = round(box["mix_ms"] / kernel_ms, 4)
         # the best read-roofline fraction ANY kernel moving this launch's
-        # bytes reaches on this GPU: the pool's boxes differ in what the 1 GB
-        # of record writes costs beside the 25 GB read (0.5-1.2 ms), and on
-        # the expensive-write boxes this ceiling itself is below 0.70
+        # bytes into these buffers reaches on this GPU: what the 1 GB of
+        # record writes costs beside the 25 GB read (0.2-1.2 ms) follows the
+        # record buffer's placement (placed_records), and with a badly placed
+        # buffer this ceiling itself is below 0.70
         ceil = bytes_per_launch / (box["mix_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
         roofline["mix_sol_read_frac"] = round(ceil, 4)
         if roofline["frac"] < 0.70:

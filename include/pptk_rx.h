@@ -346,7 +346,8 @@ int pptk_rx_last_variant(const struct pptk_rx_ctx *ctx);
  * and let later device batches of the same automatic variant and layout
  * (fixed-stride or offset-described) use the fastest (another shape must
  * beat the automatic one by 1 % to replace it).  The best shape
- * depends on the GPU (how expensive its record writes are);
+ * depends on how expensive the record writes are (which follows where the
+ * record buffer sits, see pptk_rx_place_records);
  * results never change.  Synchronous; reps 1..100.
  * pptk_rx_set_tuning's forced variant still takes precedence. */
 int pptk_rx_autotune(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *batch, int reps,

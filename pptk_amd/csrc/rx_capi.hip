@@ -411,10 +411,11 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
 
 // Interchangeable shapes per automatic variant (same frame capacity, same
 // results: every variant is parity-tested on every fixture).  Which is
-// fastest depends on the GPU: on boxes whose record writes are expensive
-// (the read/write-mix speed of light ~4.8 ms for C1500) T32S3D7 ran C1500
-// 6 % faster than T16S6; T16S6 was chosen on boxes where the mix costs
-// ~4.0 ms.  The 1536-byte class is the one measured.
+// fastest depends on what the record writes cost (which follows the record
+// buffer's placement): where they are expensive (the
+// read/write-mix speed of light ~4.8 ms for C1500) T32S3D7 ran C1500 6 %
+// faster than T16S6; T16S6 was chosen where the mix costs ~4.0 ms.  The
+// 1536-byte class is the one measured.
 static int autotune_candidates(int variant, int cand[8]) {
   int n = 0;
   cand[n++] = variant;
