@@ -120,38 +120,64 @@ def gather_bw(per, ws, seconds):
     return round(alg, 1), round(alg * (ws - 1) / ws, 1)
 
 
-PLACE_CANDIDATES = 12
+PLACE_FRAMES = 3          # frame-buffer candidates (a fresh synthetic batch)
+PLACE_RECORDS = 8         # record-buffer candidates
 
 
-def placed_records(ctx, b, n, dev, compact, kw, ncand=PLACE_CANDIDATES, spacer=None):
-    """The record buffer, placed (pptk_rx_place_records): ncand candidate
-    buffers allocated with `spacer` bytes (default 6x the buffer, 256 MiB ..
-    6 GiB) allocated between consecutive ones, so that they land apart in
-    HBM (the slow and fast placements come in runs of several GB,
-    DESIGN.md section 7); the batch timed into each, the fastest kept.
-    Returns (recs, placement report)."""
+def _spaced(dev, count, nbytes, spacer, hold):
+    """count buffers of nbytes, each allocated after a spacer of `spacer`
+    bytes (kept in `hold`) so that they land apart in HBM."""
+    import torch
+    out = []
+    for _ in range(count):
+        if spacer:
+            hold.append(torch.empty(spacer, dtype=torch.uint8, device=dev))
+        out.append(torch.empty(nbytes, dtype=torch.uint8, device=dev))
+    return out
+
+
+def placed_buffers(ctx, b, n, dev, compact, kw, frames=True, nf=PLACE_FRAMES,
+                   nr=PLACE_RECORDS):
+    """Place the batch's buffers (pptk_rx_place_buffers): what the memory
+    charges for the record writes beside the frame reads depends on where
+    the frame buffer and the record buffer sit physically (the same launch:
+    4.15-4.3 ms or 4.5-5.1 ms).  Frame candidates (with
+    frames=True: the batch as generated plus nf - 1 copies, each allocated
+    behind a spacer so that they land apart) times record candidates (nr,
+    behind spacers too); the batch timed on every pair, the fastest pair
+    kept -- b["frames"] is replaced by the chosen copy.  Untimed, once per
+    batch, as a long-lived rx ring would be set up.  Returns (recs, report)."""
     import torch
     rb = 32 if compact else 64
-    if spacer is None:
-        spacer = min(6 << 30, max(256 << 20, 6 * n * rb))
+    fbytes = b["frames"].numel()
+    spacer_r = min(4 << 30, max(256 << 20, 4 * n * rb))
+    spacer_f = min(8 << 30, max(1 << 30, fbytes // 2))
     free, _ = torch.cuda.mem_get_info(dev)
-    while ncand > 1 and ncand * n * rb + (ncand - 1) * spacer > 0.6 * free:
-        ncand -= 1
-    cands, spacers = [], []
-    for k in range(ncand):
-        if k:
-            spacers.append(torch.empty(spacer, dtype=torch.uint8, device=dev))
-        cands.append(torch.empty((n, rb), dtype=torch.uint8, device=dev))
-    best, ms = ctx.place_records(b["frames"], n, cands, compact=compact, **kw)
-    recs = cands[best]
-    del cands, spacers
+    if not frames:
+        nf = 1
+    while nf > 1 and (nf - 1) * (fbytes + spacer_f) + nr * (n * rb + spacer_r) > 0.5 * free:
+        nf -= 1
+    while nr > 1 and (nf - 1) * (fbytes + spacer_f) + nr * (n * rb + spacer_r) > 0.5 * free:
+        nr -= 1
+    hold = []
+    fc = [b["frames"]]
+    for t in _spaced(dev, nf - 1, fbytes, spacer_f, hold):
+        t.copy_(b["frames"])
+        fc.append(t)
+    rc = [t.view(n, rb) for t in _spaced(dev, nr, n * rb, spacer_r, hold)]
+    fi, ri, ms = ctx.place_buffers(fc, n, rc, compact=compact, **kw)
+    b["frames"] = fc[fi]
+    recs = rc[ri]
+    report = {"frame_candidates": nf, "record_candidates": nr, "chosen": [fi, ri],
+              "chosen_ms": ms[fi * nr + ri], "as_allocated_ms": ms[0],
+              "pair_ms": [ms[k * nr:(k + 1) * nr] for k in range(nf)]}
+    del fc, rc, hold
     torch.cuda.empty_cache()
-    return recs, {"candidates": ncand, "spacer_bytes": spacer, "candidate_ms": ms,
-                  "chosen": best}
+    return recs, report
 
 
 def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SETTLE_S,
-               compact=False, batch=None, autotune=True, first=None, place=True):
+               compact=False, batch=None, autotune=True, first=None, place=True, recs=None):
     """Generate this rank's shard of config `cfg` (n frames from global frame
     `first`, default rank * n) or reuse `batch`, time `steps` launches.
     gbs: two shard.GatherBuffer (double-buffered all-gather of the flow
@@ -169,12 +195,14 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
     else:
         kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
     placement = None
-    if place:
-        # where the record buffer sits relative to the frames changes what
-        # the memory charges for the record writes by up to 25 % (DESIGN.md
-        # section 7): pick a well-placed buffer, untimed, as a long-lived
-        # rx ring would be allocated once
-        recs, placement = placed_records(ctx, b, n, dev, compact, kw)
+    if recs is not None:
+        pass                      # the caller's (already placed) record buffer
+    elif place:
+        # where the frame and record buffers sit changes what the memory
+        # charges for the record writes by up to 25 %:
+        # pick a well-placed pair, untimed, as a long-lived rx ring would be
+        # set up once (a reused batch keeps its frames: records only)
+        recs, placement = placed_buffers(ctx, b, n, dev, compact, kw, frames=batch is None)
     else:
         recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
     if autotune:
@@ -734,8 +762,10 @@ def main():
     if gbs:
         # same launches without the collective: the kernel-only duration the
         # roofline uses, and the rate "without the gather" 
+        # (into the primary run's record buffer: the same placement, so the
+        # difference is the collective's alone)
         nog = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None, False,
-                         args.settle, batch=prim["_batch"], first=first, place=place)
+                         args.settle, batch=prim["_batch"], first=first, recs=prim["_recs"])
         del nog["_batch"], nog["_recs"]
         nog["mpkts"] = n_total * args.steps / nog["wall_s"] / 1e6
         gat = gather_bench(ctx, gbs[0], ws, dev, args.steps)
@@ -775,7 +805,7 @@ def main():
         # the best read-roofline fraction ANY kernel moving this launch's
         # bytes into these buffers reaches on this GPU: what the 1 GB of
         # record writes costs beside the 25 GB read (0.2-1.2 ms) follows the
-        # record buffer's placement (placed_records), and with a badly placed
+        # buffers' placement (placed_buffers), and with a badly placed
         # buffer this ceiling itself is below 0.70
         ceil = bytes_per_launch / (box["mix_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
         roofline["mix_sol_read_frac"] = round(ceil, 4)

@@ -403,19 +403,31 @@ void pptk_rx_shard_range(uint64_t n, int nranks, int rank, uint64_t *first, uint
 int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint64_t n,
                            uint64_t *d_out, void *stream);
 
-/* Record-buffer placement.  What the memory charges for the record writes
- * beside the frame-read stream depends on where the record buffer sits
- * physically relative to the frame buffer: the same launch into two 1 GiB
- * record buffers allocated at different moments can take 4.15 or 5.13 ms
- * (C1500), with identical bytes moved.  For long-lived
- * rings: allocate a few candidate record buffers (any allocator; spread
- * apart, e.g. with a few GB allocated between them), and let this run the
- * batch `b` into each (`reps` timed launches after one warm-up, candidates
- * interleaved) and return in *best the index of the fastest; keep that one,
- * free the others.  The candidates replace b->d_recs (or b->d_recs32 for a
- * compact batch) and receive the batch's records; everything else of `b` is
- * used as given.  Synchronous; ncand 1..64, reps 1..100.  ms (nullable)
- * receives each candidate's median launch time. */
+/* Buffer placement.  What the memory charges for the record writes beside
+ * the frame-read stream depends on where the frame buffer and the record
+ * buffer sit physically: the same C1500 launch, same kernel, same bytes,
+ * takes 4.15-4.3 ms or 4.5-5.1 ms depending on the frame buffer, the record
+ * buffer, or the pair.  For long-lived rings, set up
+ * once: allocate a few candidate buffers (any allocator; spread apart, e.g.
+ * with a few GB allocated between them), frame candidates each holding the
+ * same representative batch, and let this run the batch on every (frames,
+ * records) pair -- `reps` timed launches after one warm-up, pairs
+ * interleaved -- and return the fastest pair in *best_frames / *best_recs;
+ * keep those, free the others.  The frame candidates replace b->d_frames
+ * (offsets in b->d_off are relative to it, so one descriptor array serves
+ * all), the record candidates b->d_recs (b->d_recs32 for a compact batch)
+ * and receive the batch's records; the rest of `b` is used as given.
+ * Synchronous; nframes 1..16, nrecs 1..64, nframes * nrecs <= 256, reps
+ * 1..100.  ms (nullable) receives nframes * nrecs median launch times,
+ * frames-major. */
+int pptk_rx_place_buffers(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *b,
+                          const uint8_t *const *d_frames, int nframes, void *const *d_recs,
+                          int nrecs, int reps, int *best_frames, int *best_recs, float *ms,
+                          void *stream);
+
+/* The record buffer alone (the frames as given in b->d_frames): as
+ * pptk_rx_place_buffers with one frame candidate; *best = the record
+ * candidate's index, ms = ncand median times. */
 int pptk_rx_place_records(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *b,
                           void *const *d_cands, int ncand, int reps, int *best, float *ms,
                           void *stream);

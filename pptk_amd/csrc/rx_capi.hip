@@ -475,20 +475,24 @@ int pptk_rx_autotune(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b, i
   return rc;
 }
 
-int pptk_rx_place_records(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
-                          void *const *cands, int ncand, int reps, int *best, float *ms_out,
-                          void *stream) {
-  if (!c || !b || !cands || !best || ncand < 1 || ncand > 64 || reps < 1 || reps > 100)
+int pptk_rx_place_buffers(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
+                          const uint8_t *const *fr, int nf, void *const *rc_, int nr, int reps,
+                          int *best_f, int *best_r, float *ms_out, void *stream) {
+  if (!c || !b || !fr || !rc_ || !best_f || !best_r || nf < 1 || nf > 16 || nr < 1 ||
+      nr > 64 || nf * nr > 256 || reps < 1 || reps > 100)
     return -EINVAL;
-  for (int k = 0; k < ncand; ++k)
-    if (!cands[k]) return -EINVAL;
+  for (int k = 0; k < nf; ++k)
+    if (!fr[k]) return -EINVAL;
+  for (int k = 0; k < nr; ++k)
+    if (!rc_[k]) return -EINVAL;
   pptk_rx_dev_batch t = *b;
   const bool c32 = b->d_recs32 != nullptr;
-  t.d_recs = c32 ? nullptr : (pptk_rx_rec *)cands[0];
-  t.d_recs32 = c32 ? (pptk_rx_rec32 *)cands[0] : nullptr;
+  t.d_frames = fr[0];
+  t.d_recs = c32 ? nullptr : (pptk_rx_rec *)rc_[0];
+  t.d_recs32 = c32 ? (pptk_rx_rec32 *)rc_[0] : nullptr;
   int rc = check_batch(c, &t);
   if (rc || b->n == 0) {
-    if (rc == 0) *best = 0;
+    if (rc == 0) *best_f = *best_r = 0;
     return rc;
   }
   DeviceScope dg(c->device);
@@ -499,39 +503,51 @@ int pptk_rx_place_records(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch 
     return -EIO;
   }
   const hipStream_t s = (hipStream_t)stream;
-  std::vector<std::vector<float>> ms((size_t)ncand);
-  // candidates interleaved round by round, so that clock drift during the
-  // probe falls on all of them alike; round 0 is the warm-up
+  const int np = nf * nr;
+  std::vector<std::vector<float>> ms((size_t)np);
+  // pairs interleaved round by round, so that clock drift during the probe
+  // falls on all of them alike; round 0 is the warm-up
   for (int r = 0; r <= reps && rc == 0; ++r) {
-    for (int k = 0; k < ncand && rc == 0; ++k) {
-      if (c32) t.d_recs32 = (pptk_rx_rec32 *)cands[k];
-      else t.d_recs = (pptk_rx_rec *)cands[k];
+    for (int p = 0; p < np && rc == 0; ++p) {
+      t.d_frames = fr[p / nr];
+      if (c32) t.d_recs32 = (pptk_rx_rec32 *)rc_[p % nr];
+      else t.d_recs = (pptk_rx_rec *)rc_[p % nr];
       if (hipEventRecord(e0, s) != hipSuccess) rc = -EIO;
       if (rc == 0) rc = pptk_rx_batch_device(c, &t, stream);
       if (rc == 0 && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess))
         rc = -EIO;
       float x = 0.f;
       if (rc == 0 && r > 0 && hipEventElapsedTime(&x, e0, e1) == hipSuccess)
-        ms[(size_t)k].push_back(x);
+        ms[(size_t)p].push_back(x);
     }
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (rc) return rc;
-  int bi = 0;
+  int bp = 0;
   float bm = 1e30f;
-  for (int k = 0; k < ncand; ++k) {
-    std::vector<float> &v = ms[(size_t)k];
+  for (int p = 0; p < np; ++p) {
+    std::vector<float> &v = ms[(size_t)p];
     std::sort(v.begin(), v.end());
     const float med = v.empty() ? 1e30f : v[v.size() / 2];
-    if (ms_out) ms_out[k] = med;
+    if (ms_out) ms_out[p] = med;
     if (med < bm) {
       bm = med;
-      bi = k;
+      bp = p;
     }
   }
-  *best = bi;
+  *best_f = bp / nr;
+  *best_r = bp % nr;
   return 0;
+}
+
+int pptk_rx_place_records(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
+                          void *const *cands, int ncand, int reps, int *best, float *ms_out,
+                          void *stream) {
+  if (!b || !best) return -EINVAL;
+  const uint8_t *f0 = b->d_frames;
+  int bf = 0;
+  return pptk_rx_place_buffers(c, b, &f0, 1, cands, ncand, reps, &bf, best, ms_out, stream);
 }
 
 int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,

@@ -47,6 +47,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_rewrite_device",
            "pptk_tcp_mss_clamp_device", "pptk_rx_autotune", "pptk_rx_place_records",
+           "pptk_rx_place_buffers",
            # multi-GPU (RCCL)
            "pptk_rx_device_count", "pptk_rx_comm_uid", "pptk_rx_comm_create",
            "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
@@ -104,6 +105,13 @@ def lib(path=None):
                                                 ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_float), vp]
             L.pptk_rx_place_records.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_place_buffers"):        # absent from older A/B builds
+            L.pptk_rx_place_buffers.argtypes = [vp, ctypes.POINTER(RxDevBatch), ctypes.POINTER(vp),
+                                                ctypes.c_int, ctypes.POINTER(vp), ctypes.c_int,
+                                                ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_float), vp]
+            L.pptk_rx_place_buffers.restype = ctypes.c_int
         if hasattr(L, "pptk_tcp_mss_clamp_device"):    # absent from older A/B builds
             L.pptk_tcp_mss_clamp_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64,
                                                     ctypes.c_uint32, ctypes.c_uint64,
@@ -272,6 +280,31 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_place_records failed ({rc})")
         return best.value, [round(x, 4) for x in ms[:len(cands)]]
+
+    def place_buffers(self, frame_cands, n, rec_cands, off=None, lens=None, stride=0,
+                      fixed_len=0, max_len=0, compact=False, reps=3, stream=None):
+        """pptk_rx_place_buffers: the batch (the same bytes in every frame
+        candidate) on every (frames, records) pair; returns (frame index,
+        record index, median ms per pair, frames-major)."""
+        import torch
+        nf, nr = len(frame_cands), len(rec_cands)
+        fa = (ctypes.c_void_p * max(1, nf))(*[t.data_ptr() for t in frame_cands])
+        ra = (ctypes.c_void_p * max(1, nr))(*[t.data_ptr() for t in rec_cands])
+        f0 = frame_cands[0].data_ptr() if nf else None
+        r0 = rec_cands[0].data_ptr() if nr else None
+        b = RxDevBatch(f0, None if off is None else off.data_ptr(),
+                       None if lens is None else lens.data_ptr(), None, stride, fixed_len,
+                       max_len, n, None if compact else r0, None, r0 if compact else None)
+        bf, br = ctypes.c_int(-1), ctypes.c_int(-1)
+        ms = (ctypes.c_float * max(1, nf * nr))()
+        dev = frame_cands[0].device if nf else torch.device("cuda", self.device)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        rc = self._L.pptk_rx_place_buffers(self._ctx, ctypes.byref(b), fa, nf, ra, nr, reps,
+                                           ctypes.byref(bf), ctypes.byref(br), ms,
+                                           ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_place_buffers failed ({rc})")
+        return bf.value, br.value, [round(x, 4) for x in ms[:nf * nr]]
 
     def tuned_variant(self, frames, n, off=None, lens=None, stride=0, fixed_len=0, max_len=0,
                       compact=False):

@@ -583,3 +583,25 @@ def test_tuning_rejects_diagnostic_bits(dev):
     for good in (0x1, 0x2, 0x20, 0x40, 0x100, 0x163):
         ctx.set_tuning(-1, good)
     ctx.close()
+
+
+def test_place_buffers(dev):
+    """pptk_rx_place_buffers times the batch on every (frames, records) pair
+    of candidates (frame candidates hold the same bytes) and returns the
+    fastest pair; every record candidate holds the exact records."""
+    z = load_golden("fuzz")
+    n = len(z["off"])
+    ctx = _ctx(z)
+    f0 = torch.from_numpy(z["buf"]).to(dev)
+    frames = [f0, f0.clone(), f0.clone()]
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    recs = [torch.zeros((n, 64), dtype=torch.uint8, device=dev) for _ in range(2)]
+    fi, ri, ms = ctx.place_buffers(frames, n, recs, off=off, lens=lens, max_len=1500, reps=2)
+    assert 0 <= fi < 3 and 0 <= ri < 2 and len(ms) == 6 and ms[fi * 2 + ri] == min(ms)
+    for r in recs:
+        d = diff_records(r.cpu().numpy().reshape(-1), z["recs"])
+        assert not d, d
+    with pytest.raises(OSError):
+        ctx.place_buffers([], n, recs, off=off, lens=lens)
+    ctx.close()

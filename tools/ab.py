@@ -10,7 +10,7 @@ lib names come from AB_LIBS (name=path,...), default = pptk_amd/libpptkrx.so.
 Generates the batch once, then times every setting in interleaved rounds
 (A B C A B C ...) so that clock and thermal drift hit all settings alike;
 prints one JSON line with the median kernel ms and GB/s per setting.
-AB_PLACE=1 times into placed record buffers (bench.placed_records).
+AB_PLACE=1 times on placed frame and record buffers (bench.placed_buffers).
 AB_BIN=1 processes mixed batches in length-binned order (pptk_rx_bin_device,
 timed inside each launch's window); AB_MIXED=1 through
 pptk_rx_batch_device_mixed (binning + one launch per length group)."""
@@ -57,10 +57,11 @@ def main():
     ctxs = {k: RxContext(0, bytes(range(1, 17)), lib_path=v) for k, v in libs.items()}
     placement = None
     if os.environ.get("AB_PLACE"):
-        # well-placed record buffers (bench.placed_records), as bench.py uses
+        # well-placed frame and record buffers (bench.placed_buffers), as
+        # bench.py uses
         import bench
-        recs64, placement = bench.placed_records(ctxs[""], b, n, dev, False, kw)
-        recs32, _ = bench.placed_records(ctxs[""], b, n, dev, True, kw)
+        recs64, placement = bench.placed_buffers(ctxs[""], b, n, dev, False, kw)
+        recs32, _ = bench.placed_buffers(ctxs[""], b, n, dev, True, kw, frames=False)
     else:
         recs64 = torch.empty((n, 64), dtype=torch.uint8, device=dev)
         recs32 = torch.empty((n, 32), dtype=torch.uint8, device=dev)

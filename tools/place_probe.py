@@ -22,10 +22,19 @@ def matrix(args):
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
+    hold = []
     bs = [make_batch("c1500", n, dev)]
-    if args.batches > 1:
-        bs.append(make_batch("c1500", n, dev, first=n))
-    rs = [torch.zeros((n, 64), dtype=torch.uint8, device=dev) for _ in range(args.matrix)]
+    for k in range(1, args.batches):
+        if args.spacer_gb:
+            hold.append(torch.empty(int(args.spacer_gb * (1 << 30)), dtype=torch.uint8,
+                                    device=dev))
+        bs.append(make_batch("c1500", n, dev, first=k * n))
+    rs = []
+    for _ in range(args.matrix):
+        if args.spacer_gb:
+            hold.append(torch.empty(int(args.spacer_gb * (1 << 30)), dtype=torch.uint8,
+                                    device=dev))
+        rs.append(torch.zeros((n, 64), dtype=torch.uint8, device=dev))
     torch.cuda.synchronize()
     t = {}
     for rep in range(args.reps + 1):
@@ -128,6 +137,9 @@ def main():
     ap.add_argument("--policies", action="store_true")
     ap.add_argument("--orders", action="store_true")
     ap.add_argument("--batches", type=int, default=2)
+    ap.add_argument("--spacer-gb", type=float, default=0.0,
+                    help="matrix: allocate this many GB before every batch after the first "
+                         "and before every record buffer")
     args = ap.parse_args()
     if args.matrix:
         return matrix(args)
