@@ -113,6 +113,16 @@ def sum_over_ranks(x, ws, dev=None):
     return _reduce(x, ws, dist.ReduceOp.SUM)
 
 
+def per_rank(x, ws):
+    """Every rank's value of x (gloo all_gather_object), rank order."""
+    if not dist_on(ws):
+        return [x]
+    import torch.distributed as dist
+    out = [None] * ws
+    dist.all_gather_object(out, x)
+    return out
+
+
 def gather_bw(per, ws, seconds):
     """All-gather bandwidths (RCCL convention): algorithmic = bytes received
     per rank / time, bus = algorithmic * (ws - 1) / ws."""
@@ -783,6 +793,8 @@ def main():
             box["mix_ms"], box["mix_desc"] = sol
         log(f"[rank {rank}] box HBM: {box}")
 
+    # every rank's kernel time (the scaling curve's per-GPU view)
+    per_rank_ms = per_rank(round((nog or prim)["kernel_ms"], 4), ws)
     bytes_per_launch = prim["bytes"]
     # with N > 1 the primary run's event pair also spans the wait on the
     # previous batch's gather, so the kernel duration comes from the run
@@ -900,6 +912,7 @@ def main():
                        "key": "01..10"},
             "roofline": roofline,
             "record_placement": prim.get("placement"),
+            "per_rank_kernel_ms": per_rank_ms,
             "cpu_baseline": cpu,
             "value_no_gather": None if nog is None else round(nog["mpkts"], 1),
             "rec32": rec32,

@@ -97,8 +97,9 @@ def _bench_worker(rank, world, port, q):
         mx = bench.max_over_ranks(float(rank + 1), world, dev)
         sm = bench.sum_over_ranks(float(rank + 1), world, dev)
         g = bench.gather_bw(1024, world, 1e-3)
+        pr = bench.per_rank(float(rank) + 0.5, world)
         if rank == 0:
-            q.put((mx, sm, g))
+            q.put((mx, sm, g, pr))
     finally:
         dist.destroy_process_group()
 
@@ -112,11 +113,11 @@ def test_bench_multi_rank_helpers():
     procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    mx, sm, g = q.get(timeout=120)
+    mx, sm, g, pr = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert mx == 2.0 and sm == 3.0
+    assert mx == 2.0 and sm == 3.0 and pr == [0.5, 1.5]
     alg, bus = g
     assert alg == round(1024 * 2 * 8 / 1e-3 / 1e9, 1) and abs(bus - alg / 2) <= 0.1
 
