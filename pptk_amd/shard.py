@@ -37,12 +37,18 @@ class GatherBuffer:
     `device`, and `local`, this rank's slice, which the rx kernel fills
     (d_hash) before the in-place all-gather."""
 
-    def __init__(self, n_total, world, rank, device):
+    def __init__(self, n_total, world, rank, device, inplace=True, out=None):
         import torch
         self.first, self.count, self.per = shard_range(n_total, world, rank)
         self.n_total, self.world, self.rank = n_total, world, rank
-        self.out = torch.zeros(world * self.per, dtype=torch.int64, device=device)
-        self.local = self.out[rank * self.per: rank * self.per + self.per]
+        if out is None:
+            out = torch.zeros(world * self.per, dtype=torch.int64, device=device)
+        # (a caller-placed buffer: bench.placed_gather)
+        self.out = out.view(torch.int64)[:world * self.per]
+        if inplace:
+            self.local = self.out[rank * self.per: rank * self.per + self.per]
+        else:   # (experiments: a separate send buffer, so even one rank copies)
+            self.local = torch.zeros(self.per, dtype=torch.int64, device=device)
 
     def gather(self, ctx, stream=None):
         """pptk_rx_allgather_hash of `per` hashes per rank, in place."""

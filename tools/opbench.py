@@ -6,7 +6,10 @@ OP: tx (pptk_tx_cksum_device on C1500), tx_cmix, rewrite (pptk_tx_rewrite_device
 on C64), mss (pptk_tcp_mss_clamp_device, 16 M SYNs), permit
 (pptk_rx_permit_device over 16 M C64 records), binned (CMIX through
 pptk_rx_batch_device_mixed), allgather (a one-rank communicator's in-place
-pptk_rx_allgather_hash after every C1500 launch).  Uses bench.py's own
+pptk_rx_allgather_hash after every C1500 launch), allgather_copy (the same
+with a separate send buffer: one rank's collective then copies 128 MiB per
+batch beside the rx grid), gather_emul (the HBM traffic of an 8-rank gather,
+emulated by a device copy).  Uses bench.py's own
 measurement functions; prints one JSON line with the timing and
 `changed_bytes_per_launch` (the bytes the op must write), the denominator
 of the write-amplification ratio WRITE_SIZE / changed bytes."""
@@ -63,6 +66,52 @@ def gather_emul(ctx, dev, n, steps, warmup, world=8):
             "changed_bytes_per_launch": 64 * n}
 
 
+def gather_emul_place(ctx, dev, n, steps, warmup, world=8, ncand=6):
+    """Does the destination of the gather's writes matter like the record
+    buffer's does?  The emulated 8-rank gather traffic (a device copy of
+    7 x 128 MiB beside every C1500 launch, frames and records placed as
+    bench.py places them) into each of `ncand` destination buffers
+    allocated 4 GB apart; ms per batch for each, and without the copy."""
+    import time
+    import torch
+    import bench
+    from tools.synth import make_batch
+    b = make_batch("c1500", n, dev)
+    kw = dict(stride=1500, fixed_len=1500)
+    recs, place = bench.placed_buffers(ctx, b, n, dev, False, kw)
+    nbytes = (world - 1) * n * 8
+    src = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    hold, dsts = [], []
+    for _ in range(ncand):
+        hold.append(torch.empty(4 << 30, dtype=torch.uint8, device=dev))
+        dsts.append(torch.empty(nbytes, dtype=torch.uint8, device=dev))
+    main_s = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+
+    def run(dst):
+        for k in range(warmup + steps):
+            if k == warmup:
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+            ctx.batch_device(b["frames"], n, recs=recs, **kw)
+            if dst is not None:
+                ev = torch.cuda.Event()
+                ev.record(main_s)
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    dst.copy_(src)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / steps * 1e3
+    res = {"alone": [], "dst": [[] for _ in dsts]}
+    for _ in range(2):
+        res["alone"].append(run(None))
+        for i, d in enumerate(dsts):
+            res["dst"][i].append(run(d))
+    return {"ms_alone": round(min(res["alone"]), 4),
+            "ms_with_copy_per_dst": [round(min(v), 4) for v in res["dst"]],
+            "placement": place["chosen_ms"], "changed_bytes_per_launch": 64 * n}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("op")
@@ -95,7 +144,7 @@ def main():
         b = make_batch("cmix", n, dev)
         r = bench.binned_bench(ctx, b, n, dev, args.steps, args.warmup)
         r["changed_bytes_per_launch"] = 64 * n
-    elif op == "allgather":
+    elif op in ("allgather", "allgather_copy"):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
         os.environ["PPTK_BENCH_FORCE_DIST"] = "1"
@@ -103,14 +152,22 @@ def main():
         from pptk_amd.shard import GatherBuffer, join
         dist.init_process_group("gloo", rank=0, world_size=1)
         join(ctx, 1, 0)
-        gbs = [GatherBuffer(n, 1, 0, dev) for _ in range(2)]
+        # allgather_copy: a separate send buffer, so the one-rank collective
+        # really moves the 128 MiB (an RCCL copy beside the rx grid)
+        gbs = [GatherBuffer(n, 1, 0, dev, inplace=op == "allgather") for _ in range(2)]
         res = bench.run_config("c1500", n, ctx, dev, 1, 0, args.steps, args.warmup, gbs, False,
                                settle=0.3, first=0)
+        nog = bench.run_config("c1500", n, ctx, dev, 1, 0, args.steps, args.warmup, None, False,
+                               settle=0.3, first=0, batch=res["_batch"], recs=res["_recs"])
         r = {"kernel_ms": round(res["kernel_ms"], 4), "mpkts": round(res["mpkts"], 1),
+             "mpkts_no_gather": round(nog["mpkts"], 1),
+             "overlap_loss": round(1 - res["mpkts"] / nog["mpkts"], 4),
              "changed_bytes_per_launch": 64 * n + 8 * n}
         dist.destroy_process_group()
     elif op == "gather_emul":
         r = gather_emul(ctx, dev, n, args.steps, args.warmup)
+    elif op == "gather_emul_place":
+        r = gather_emul_place(ctx, dev, n, args.steps, args.warmup)
     else:
         raise SystemExit(f"unknown op {op}")
     r["op"] = op
