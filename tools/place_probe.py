@@ -126,6 +126,53 @@ def orders(args):
     print(json.dumps({k: round(sorted(v)[len(v) // 2], 3) for k, v in t.items()}), flush=True)
 
 
+def flags(args):
+    """Record buffers from hipExtMallocWithFlags with each allocation flag
+    (default, fine-grained, uncached, contiguous), several of each, the same
+    C1500 launch into each: does an allocation kind avoid the slow class?"""
+    import ctypes
+    import torch
+    from pptk_amd.rx import RxContext, RxDevBatch
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    b = make_batch("c1500", n, dev)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
+                                          ctypes.c_uint]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    kinds = {"default": 0, "finegrained": 1, "uncached": 3, "contiguous": 4}
+    bufs = []
+    for rep in range(3):
+        for name, fl in kinds.items():
+            p = ctypes.c_void_p()
+            rc = hip.hipExtMallocWithFlags(ctypes.byref(p), n * 64, fl)
+            bufs.append((f"{name}{rep}", p if rc == 0 else None, rc))
+    s = torch.cuda.current_stream(dev)
+    t = {}
+    for rnd in range(args.reps + 1):
+        for name, p, rc in bufs:
+            if p is None:
+                continue
+            bb = RxDevBatch(b["frames"].data_ptr(), None, None, None, 1500, 1500, 1500, n,
+                            p.value, None, None, None)
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            r = ctx._L.pptk_rx_batch_device(ctx._ctx, ctypes.byref(bb),
+                                             ctypes.c_void_p(s.cuda_stream))
+            z.record()
+            torch.cuda.synchronize()
+            if r == 0 and rnd:
+                t.setdefault(name, []).append(a.elapsed_time(z))
+    out = {k: round(sorted(v)[len(v) // 2], 3) for k, v in t.items()}
+    out["alloc_errors"] = {name: rc for name, p, rc in bufs if p is None}
+    for _, p, _ in bufs:
+        if p is not None:
+            hip.hipFree(p)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-mb", type=float, default=16)
@@ -136,6 +183,7 @@ def main():
                     help="instead: 2 frame batches x this many separate 1 GiB record buffers")
     ap.add_argument("--policies", action="store_true")
     ap.add_argument("--orders", action="store_true")
+    ap.add_argument("--flags", action="store_true")
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--spacer-gb", type=float, default=0.0,
                     help="matrix: allocate this many GB before every batch after the first "
@@ -147,6 +195,8 @@ def main():
         return policies(args)
     if args.orders:
         return orders(args)
+    if args.flags:
+        return flags(args)
     import torch
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch
