@@ -173,6 +173,88 @@ def flags(args):
     print(json.dumps(out), flush=True)
 
 
+def keep(args):
+    """Does a placed pair stay fast?  Frames + 8 record candidates behind 4 GB
+    spacers, each timed; then the best is re-timed (a) with everything still
+    allocated, (b) after the other candidates and the spacers are freed
+    (empty_cache), (c) over a sustained run of 300 launches."""
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    b = make_batch("c1500", n, dev)
+    hold, rs = [], []
+    for _ in range(8):
+        hold.append(torch.empty(4 << 30, dtype=torch.uint8, device=dev))
+        rs.append(torch.empty((n, 64), dtype=torch.uint8, device=dev))
+
+    def t(r, k=5):
+        ts = []
+        for _ in range(k + 1):
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=r)
+            z.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(z))
+        return round(sorted(ts[1:])[k // 2], 3)
+    cand = [t(r) for r in rs]
+    bi = min(range(8), key=lambda i: cand[i])
+    wi = max(range(8), key=lambda i: cand[i])
+    out = {"candidates": cand, "best": bi, "best_again": t(rs[bi]), "worst_again": t(rs[wi])}
+    best, worst = rs[bi], rs[wi]
+    del hold, rs
+    torch.cuda.empty_cache()
+    out["best_after_free"] = t(best)
+    out["worst_after_free"] = t(worst)
+    sus = []
+    for k in range(300):
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=best)
+        z.record()
+        if k % 50 == 49:
+            torch.cuda.synchronize()
+            sus.append(round(a.elapsed_time(z), 3))
+    torch.cuda.synchronize()
+    out["best_sustained_every50"] = sus
+    print(json.dumps(out), flush=True)
+
+
+def benchpath(args):
+    """bench.placed_buffers as bench.py calls it, then a sustained run on
+    the chosen pair: is the probe's time what the sustained run gets?"""
+    import torch
+    import bench
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    b = make_batch("c1500", n, dev)
+    kw = dict(stride=1500, fixed_len=1500)
+    out = {}
+    for mode in ("pairs", "records"):
+        recs, rep = bench.placed_buffers(ctx, b, n, dev, False, kw, frames=mode == "pairs")
+        sus = []
+        for k in range(200):
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ctx.batch_device(b["frames"], n, recs=recs, **kw)
+            z.record()
+            if k % 40 == 39:
+                torch.cuda.synchronize()
+                sus.append(round(a.elapsed_time(z), 3))
+        torch.cuda.synchronize()
+        out[mode] = {"chosen": rep["chosen"], "probe_ms": rep["chosen_ms"],
+                     "as_allocated": rep["as_allocated_ms"], "sustained": sus}
+        del recs
+        torch.cuda.empty_cache()
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-mb", type=float, default=16)
@@ -184,6 +266,8 @@ def main():
     ap.add_argument("--policies", action="store_true")
     ap.add_argument("--orders", action="store_true")
     ap.add_argument("--flags", action="store_true")
+    ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--benchpath", action="store_true")
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--spacer-gb", type=float, default=0.0,
                     help="matrix: allocate this many GB before every batch after the first "
@@ -197,6 +281,10 @@ def main():
         return orders(args)
     if args.flags:
         return flags(args)
+    if args.keep:
+        return keep(args)
+    if args.benchpath:
+        return benchpath(args)
     import torch
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch

@@ -39,8 +39,10 @@ def counter(d, cname):
 def timed_launches(d, name, steps, gap_ms=20.0):
     """From the kernel trace of the traced bench command: the launches of
     kernel `name` split into runs (consecutive launches less than gap_ms
-    apart); the first run of 100+ launches is the config's settle + warmup +
-    timed steps, and its last `steps` launches are the ones bench.py timed.
+    apart); the first run at least half as long as the longest one is the
+    config's settle + warmup + timed steps (the placement probe's and the
+    autotune's runs are far shorter than the 1.5 s settle), and its last
+    `steps` launches are the ones bench.py timed.
     Their mean / median duration is the same-run counterpart of the bench
     line's kernel_ms."""
     tr = [r for r in rows(d, "*kernel_trace.csv") if r["Kernel_Name"] == name]
@@ -55,7 +57,8 @@ def timed_launches(d, name, steps, gap_ms=20.0):
         last_end = e0
     if cur:
         runs.append(cur)
-    run = next((r for r in runs if len(r) >= 100), max(runs, key=len) if runs else [])
+    longest = max((len(r) for r in runs), default=0)
+    run = next((r for r in runs if 2 * len(r) >= longest), [])
     if len(run) < steps:
         return {}
     t = sorted(run[-steps:])
