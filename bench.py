@@ -132,6 +132,23 @@ def gather_bw(per, ws, seconds):
 
 PLACE_FRAMES = 3          # frame-buffer candidates (a fresh synthetic batch)
 PLACE_RECORDS = 8         # record-buffer candidates
+# Freed device memory is scrubbed by the driver in the background (SOCCLK
+# at 1.2 GHz while it runs, `tools/clock_probe.py --free-gb`): ~1 s after
+# freeing 16 GB, ~2 s after 64 GB, ~4 s after 128 GB, and the rx launches
+# beside it run up to 9 % slower.  The settle after a placement probe lasts
+# until the scrub of what the probe freed is over, at this (conservative)
+# rate.
+SCRUB_BYTES_PER_S = 20e9
+
+
+def release(dev):
+    """Return the caching allocator's free blocks to the driver; returns
+    (bytes released, when), the input of the scrub wait."""
+    import torch
+    torch.cuda.synchronize(dev)
+    before = torch.cuda.memory_reserved(dev)
+    torch.cuda.empty_cache()
+    return max(0, before - torch.cuda.memory_reserved(dev)), time.perf_counter()
 
 
 def _spaced(dev, count, nbytes, spacer, hold):
@@ -182,7 +199,7 @@ def placed_buffers(ctx, b, n, dev, compact, kw, frames=True, nf=PLACE_FRAMES,
               "chosen_ms": ms[fi * nr + ri], "as_allocated_ms": ms[0],
               "pair_ms": [ms[k * nr:(k + 1) * nr] for k in range(nf)]}
     del fc, rc, hold
-    torch.cuda.empty_cache()
+    report["freed_bytes"], report["_freed_at"] = release(dev)
     return recs, report
 
 
@@ -238,9 +255,10 @@ def placed_gather(ctx, b, recs, kw, n_total, ws, rank, dev, ncand=8, steps=4):
            for k in range(2)]
     for g in gbs:
         g.out.zero_()
-    del hold
-    torch.cuda.empty_cache()
-    return gbs, {"candidates": ncand, "candidate_ms": ms, "chosen": best}
+    del hold, cands, src
+    freed, at = release(dev)
+    return gbs, {"candidates": ncand, "candidate_ms": ms, "chosen": best,
+                 "freed_bytes": freed, "_freed_at": at}
 
 
 def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SETTLE_S,
@@ -310,9 +328,17 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
     # before the W warmup steps, so the K timed steps see steady state.  The
     # settle launches issue no collective: their number depends on each
     # rank's clock, and ranks must issue the same sequence of all-gathers.
+    # After a placement probe the settle also outlasts the driver's scrub of
+    # the candidates it freed (SCRUB_BYTES_PER_S).
     t_settle = time.perf_counter()
+    settle_end = t_settle + settle
+    for rep in (placement, gplace):
+        if rep and "_freed_at" in rep:
+            scrub_end = rep.pop("_freed_at") + rep["freed_bytes"] / SCRUB_BYTES_PER_S
+            settle_end = max(settle_end, scrub_end)
+            rep["scrub_wait_s"] = round(max(0.0, scrub_end - t_settle), 2)
     k = 0
-    while time.perf_counter() - t_settle < settle:
+    while time.perf_counter() < settle_end:
         step(k, collective=False)
         k += 1
         if k % 16 == 0:

@@ -419,7 +419,9 @@ int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint
  * and receive the batch's records; the rest of `b` is used as given.
  * Synchronous; nframes 1..16, nrecs 1..64, nframes * nrecs <= 256, reps
  * 1..100.  ms (nullable) receives nframes * nrecs median launch times,
- * frames-major. */
+ * frames-major.  Freeing the candidates not kept makes the driver scrub that
+ * memory in the background (~30 GB/s measured); batches beside the scrub
+ * run up to 9 % slower, so a latency-sensitive ring starts after it. */
 int pptk_rx_place_buffers(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *b,
                           const uint8_t *const *d_frames, int nframes, void *const *d_recs,
                           int nrecs, int reps, int *best_frames, int *best_recs, float *ms,

@@ -178,6 +178,68 @@ def test_mixed_length_groups(name, shift, max_len, dev):
     assert np.array_equal(perm, np.argsort(_group_of(z["len"]), kind="stable"))
 
 
+class _HipBuf:
+    """A device buffer of exactly `nbytes` from its own hipMalloc (not the
+    torch caching allocator, which keeps the bytes past a tensor mapped)."""
+
+    def __init__(self, nbytes):
+        import ctypes
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._p = ctypes.c_void_p()
+        assert self._hip.hipMalloc(ctypes.byref(self._p), ctypes.c_size_t(nbytes)) == 0
+        self.nbytes = nbytes
+
+    def data_ptr(self):
+        return self._p.value
+
+    def numpy(self, dtype):
+        import ctypes
+        out = np.empty(self.nbytes // np.dtype(dtype).itemsize, dtype)
+        assert self._hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), self._p,
+                                   ctypes.c_size_t(self.nbytes), 2) == 0   # D2H
+        return out
+
+    def free(self):
+        self._hip.hipFree(self._p)
+
+
+def test_mixed_empty_trailing_groups_perm_own_allocation(dev):
+    """Advisor round 1: with max_len = 0 every length group is launched, and
+    an empty trailing group's range starts at n -- one past the permutation.
+    The permutation here is its own page-sized hipMalloc (1 024 entries) and
+    no frame is longer than 1 009 bytes, so the last two groups are empty:
+    their launches must return before reading any descriptor."""
+    import framegen
+    from oracle.oracle import Oracle, make_opts
+    rng = np.random.default_rng(1009)
+    n = 1024
+    sizes = rng.integers(60, 1010, n)
+    frames = [_frame_of_len(framegen, rng, int(L)) for L in sizes]
+    off = np.cumsum([0] + [len(f) for f in frames[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(off[-1]) + len(frames[-1]) + 64, np.uint8)
+    for i, f in enumerate(frames):
+        buf[int(off[i]):int(off[i]) + len(f)] = np.frombuffer(f, np.uint8)
+    lens = np.array([len(f) for f in frames], np.uint16)
+    key = bytes(range(1, 17))
+    want = Oracle().rx_batch(buf, off, lens, opts=make_opts(key, 24, 48, 1 << 12))
+    z = {"key": np.frombuffer(key, np.uint8), "iphash": np.array([24, 48, 1 << 12])}
+    ctx = _ctx(z)
+    _keep, fr = _upload(buf, dev)
+    perm = _HipBuf(4 * n)
+    try:
+        recs = ctx.batch_device_mixed(fr, n, torch.from_numpy(off.view(np.int64)).to(dev),
+                                      torch.from_numpy(lens.view(np.int16)).to(dev),
+                                      max_len=0, perm=perm)
+        torch.cuda.synchronize()
+        got_perm = perm.numpy(np.uint32)
+    finally:
+        torch.cuda.synchronize()
+        perm.free()
+    d = diff_records(recs.cpu().numpy().reshape(-1), want)
+    assert not d, d
+    assert np.array_equal(got_perm, np.argsort(_group_of(lens), kind="stable"))
+
+
 def _frame_of_len(fg, rng, L):
     """A frame of exactly L bytes: IPv4/IPv6 TCP/UDP when it fits, else the
     truncated head of one (malformed)."""
