@@ -784,6 +784,29 @@ static size_t direct_max_bytes() {
   return v < 0 ? 0 : (size_t)v;
 }
 
+// Bulky staged chunks go down by DMA, but their descriptors and records do
+// not: the kernel reads the 10-byte descriptors from the pinned staging and
+// writes the records into pinned memory over PCIe ("split" chunks), so the
+// copy engine runs nothing but the frame copies back to back -- the two
+// descriptor copies and the record copy cost ~0.18 ms of copy-engine time
+// per 65 536-frame chunk beside its 2.2 ms frame copy (DESIGN.md
+// "End-to-end").  PPTK_RX_SPLIT=0 restores the copies (A/B).
+static bool split_chunks() {
+  static const long v = env_long("PPTK_RX_SPLIT", 1);
+  return v != 0;
+}
+
+// A registered ring's chunk whose frames lie densely in the ring (frame
+// bytes >= this fraction of the span they cover) and whose span is above
+// the direct threshold is copied down by DMA as one span instead of being
+// read in place by the kernel: the copy engine moves ~56 GB/s over PCIe,
+// the kernel's own reads of host memory ~40 (DESIGN.md "End-to-end").
+// PPTK_RX_RING_DMA_PCT (percent; 0 = always, > 100 = never) overrides.
+static double ring_dma_density() {
+  static const long v = env_long("PPTK_RX_RING_DMA_PCT", 75);
+  return v / 100.0;
+}
+
 // The context's worker pool (nullptr with gather_threads <= 1).  If the
 // threads cannot be started the batch runs on the calling thread alone (and
 // later batches try again): no exception leaves the C ABI.
@@ -892,16 +915,16 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   // D2H), the host gathers chunk k+1 into the other slot.  In a registered
   // ring the kernel reads the frames in place over PCIe and only the 10-byte
   // descriptors go down.
-  size_t k = 0;
-  for (size_t first = 0; first < (size_t)num && rc == 0; first += chunk, ++k) {
+  size_t k = 0, cnt = 0;
+  for (size_t first = 0; first < (size_t)num && rc == 0; first += cnt, ++k) {
     RxSlot &sl = c->slot[k & 1];
     if ((rc = retire(sl, pool)) != 0) break;
-    const size_t cnt = std::min(chunk, (size_t)num - first);
+    cnt = std::min(chunk, (size_t)num - first);
     if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes)) != 0) break;
     // descriptors (and staging offsets) first, serially; then the frame
     // bytes, split over opts.gather_threads threads (the host memcpy is the
     // staged path's bottleneck, see DESIGN.md "End-to-end")
-    size_t pos = 0;
+    size_t pos = 0, lo = SIZE_MAX, hi = 0, fbytes = 0;
     uint32_t maxlen = 0;
     for (size_t i = 0; i < cnt; ++i) {
       const struct ldp_packet &pk = pkts[first + i];
@@ -909,13 +932,23 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
       const uint32_t sz = ok ? pk.sz : 0u;
       sl.h_len[i] = (uint16_t)sz;
       if (ring) {
-        sl.h_off[i] = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
+        const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
+        sl.h_off[i] = o;
+        lo = std::min<size_t>(lo, o);
+        hi = std::max<size_t>(hi, o + ((sz + 15) & ~(size_t)15));
+        fbytes += sz;
       } else {
         sl.h_off[i] = pos;
         pos += (sz + 15) & ~(size_t)15;
       }
       maxlen = std::max(maxlen, sz);
     }
+    // a dense ring chunk goes down as one span (offsets rebased onto it)
+    const bool ring_dma = ring && hi > lo && hi - lo > direct_max_bytes() &&
+                          hi - lo + 16 <= sl.cap_bytes &&
+                          (double)fbytes >= ring_dma_density() * (double)(hi - lo);
+    if (ring_dma)
+      for (size_t i = 0; i < cnt; ++i) sl.h_off[i] -= lo;
     if (!ring) {
       const struct ldp_packet *cp = pkts + first;
       auto gather = [&sl, cp](size_t lo, size_t hi) {
@@ -931,26 +964,33 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
       }
     }
     hipStream_t s = sl.stream;
-    const bool direct = ring ? direct_max_bytes() > 0 : pos <= direct_max_bytes();
-    if (!direct &&
-        ((!ring && hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
-                                  hipMemcpyHostToDevice, s) != hipSuccess) ||
-         hipMemcpyAsync(sl.d_off, sl.h_off, cnt * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-         hipMemcpyAsync(sl.d_len, sl.h_len, cnt * 2, hipMemcpyHostToDevice, s) != hipSuccess)) {
+    const bool direct =
+        ring ? direct_max_bytes() > 0 && !ring_dma : pos <= direct_max_bytes();
+    // descriptors and records over PCIe, frames by DMA
+    const bool split = !direct && (ring_dma || !ring) && split_chunks();
+    const bool pcie = direct || split;
+    if ((!direct && !ring &&
+         hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
+                        hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (ring_dma && hipMemcpyAsync(sl.d_frames, ring->host + lo, hi - lo,
+                                    hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (!pcie &&
+         (hipMemcpyAsync(sl.d_off, sl.h_off, cnt * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipMemcpyAsync(sl.d_len, sl.h_len, cnt * 2, hipMemcpyHostToDevice, s) != hipSuccess))) {
       rc = -EIO;
       break;
     }
     pptk_rx_dev_batch b;
     memset(&b, 0, sizeof(b));
-    b.d_frames = ring ? ring->dev : direct ? sl.hd_frames : sl.d_frames;
-    b.d_off = direct ? sl.hd_off : sl.d_off;
-    b.d_len = direct ? sl.hd_len : sl.d_len;
+    b.d_frames = ring && !ring_dma ? ring->dev : direct ? sl.hd_frames : sl.d_frames;
+    b.d_off = pcie ? sl.hd_off : sl.d_off;
+    b.d_len = pcie ? sl.hd_len : sl.d_len;
     b.max_len = maxlen;
     b.n = cnt;
-    b.d_recs = direct ? sl.hd_recs : sl.d_recs;
+    b.d_recs = pcie ? sl.hd_recs : sl.d_recs;
     if ((rc = pptk_rx_batch_device(c, &b, s)) != 0) break;
-    if ((!direct && hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
-                        hipSuccess) ||
+    if ((!pcie && hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
+                      hipSuccess) ||
         hipEventRecord(sl.done, s) != hipSuccess) {
       rc = -EIO;
       break;

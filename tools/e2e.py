@@ -25,7 +25,7 @@ def main():
     chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     dev = torch.device("cuda", 0)
     out = {"frames": n, "chunk": chunk}
-    for cfg in ("c1500", "c64"):
+    for cfg in os.environ.get("E2E_CFGS", "c1500,c64").split(","):
         b = make_batch(cfg, n, dev)
         stride = b["stride"]
         ring = b["frames"][: n * stride + 64].cpu().numpy()     # pageable host "ring"
