@@ -10,6 +10,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -255,6 +256,43 @@ def benchpath(args):
     print(json.dumps(out), flush=True)
 
 
+def txplace(args):
+    """Does the tx kernel (checksums set in place: the writes land in the
+    frame buffer itself) depend on where the frame buffer sits?  The same
+    C1500 batch copied into `--batches` buffers allocated behind 8 GB
+    spacers; tx timed on each, interleaved rounds, median per buffer."""
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    b = make_batch("c1500", n, dev)
+    kw = dict(stride=1500, fixed_len=1500)
+    hold, fr = [], [b["frames"]]
+    for _ in range(max(1, args.batches) - 1):
+        hold.append(torch.empty(8 << 30, dtype=torch.uint8, device=dev))
+        t = torch.empty_like(b["frames"])
+        t.copy_(b["frames"])
+        fr.append(t)
+    del hold
+    torch.cuda.synchronize()
+    time.sleep(4.0)                     # the scrub of the freed spacers
+    ms = [[] for _ in fr]
+    for _ in range(5):
+        for i, f in enumerate(fr):
+            for k in range(4):
+                a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                ctx.tx_cksum_device(f, n, **kw)
+                z.record()
+                torch.cuda.synchronize()
+                if k:
+                    ms[i].append(a.elapsed_time(z))
+    print(json.dumps({"tx_ms_per_frame_buffer": [round(sorted(v)[len(v) // 2], 4) for v in ms]}),
+          flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-mb", type=float, default=16)
@@ -268,6 +306,7 @@ def main():
     ap.add_argument("--flags", action="store_true")
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--benchpath", action="store_true")
+    ap.add_argument("--txplace", action="store_true")
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--spacer-gb", type=float, default=0.0,
                     help="matrix: allocate this many GB before every batch after the first "
@@ -285,6 +324,8 @@ def main():
         return keep(args)
     if args.benchpath:
         return benchpath(args)
+    if args.txplace:
+        return txplace(args)
     import torch
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch
