@@ -29,6 +29,7 @@ struct RxSlot {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   size_t cap_pkts = 0, cap_bytes = 0;
+  size_t dev_cap = 0;   // d_frames bytes (grown for registered-ring spans)
   uint8_t *h_frames = nullptr, *d_frames = nullptr;
   uint64_t *h_off = nullptr, *d_off = nullptr;
   uint16_t *h_len = nullptr, *d_len = nullptr;
@@ -768,7 +769,23 @@ static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {
   }
   sl.cap_pkts = pkts;
   sl.cap_bytes = bytes;
+  sl.dev_cap = bytes;
   return 0;
+}
+
+// Room for a registered-ring span of `bytes` in the slot's device frame
+// buffer (the slot is idle: its last chunk was retired).  Sparse rings
+// (e.g. 2 KB netmap slots) have spans longer than max_batch * max_frame;
+// grown up to 4x the staging size, once.
+static bool fit_span(RxSlot &sl, size_t bytes) {
+  if (bytes <= sl.dev_cap) return true;
+  if (bytes > 4 * sl.cap_bytes) return false;
+  uint8_t *p = nullptr;
+  if (hipMalloc((void **)&p, bytes) != hipSuccess) return false;
+  (void)hipFree(sl.d_frames);
+  sl.d_frames = p;
+  sl.dev_cap = bytes;
+  return true;
 }
 
 // Chunks run "direct" -- the kernel reads the descriptors (and staged
@@ -799,11 +816,13 @@ static bool split_chunks() {
 // A registered ring's chunk whose frames lie densely in the ring (frame
 // bytes >= this fraction of the span they cover) and whose span is above
 // the direct threshold is copied down by DMA as one span instead of being
-// read in place by the kernel: the copy engine moves ~56 GB/s over PCIe,
-// the kernel's own reads of host memory ~40 (DESIGN.md "End-to-end").
+// read in place by the kernel: a dense span moves ~48 GB/s of frames that
+// way, the kernel's own reads of host memory ~37-38, so the break-even is
+// near 80 % (1500-byte frames in 2 KB netmap slots, 73 %, measured 37 GB/s
+// by DMA against 38 in place; DESIGN.md "End-to-end").
 // PPTK_RX_RING_DMA_PCT (percent; 0 = always, > 100 = never) overrides.
 static double ring_dma_density() {
-  static const long v = env_long("PPTK_RX_RING_DMA_PCT", 75);
+  static const long v = env_long("PPTK_RX_RING_DMA_PCT", 80);
   return v / 100.0;
 }
 
@@ -945,8 +964,8 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
     }
     // a dense ring chunk goes down as one span (offsets rebased onto it)
     const bool ring_dma = ring && hi > lo && hi - lo > direct_max_bytes() &&
-                          hi - lo + 16 <= sl.cap_bytes &&
-                          (double)fbytes >= ring_dma_density() * (double)(hi - lo);
+                          (double)fbytes >= ring_dma_density() * (double)(hi - lo) &&
+                          fit_span(sl, hi - lo + 16);
     if (ring_dma)
       for (size_t i = 0; i < cnt; ++i) sl.h_off[i] -= lo;
     if (!ring) {

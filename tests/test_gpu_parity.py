@@ -506,35 +506,30 @@ def test_host_batch_worker_pool_large_chunks(cfg, dev):
         ctxs[k].close()
 
 
-@pytest.mark.parametrize("gap", [0, 1500, 7])
-def test_registered_ring_span_dma(gap, dev):
-    """A registered ring holding 70 000 C1500 frames `gap` bytes apart:
-    dense chunks (gap 0 or 7) go down as one DMA span with rebased offsets,
-    a sparse one (gap 1500: half the span is frames) is read in place by the
-    kernel; the short last chunk runs direct.  Every record equals the CPU
-    oracle's, and the same through staging."""
-    from oracle.oracle import Oracle, make_opts
-    from pptk_amd.rx import RxContext, ldp_packets
-    from tools.synth import make_batch
-    n, L = 70_000, 1500
-    b = make_batch("c1500", n, dev)
-    src = b["frames"][: n * L].cpu().numpy().reshape(n, L)
-    step = L + gap
-    ring = np.zeros(n * step + 4096 + 3, dtype=np.uint8)[3:]   # odd base address
-    view = np.lib.stride_tricks.as_strided(ring, (n, L), (step, 1))
-    view[:] = src
-    off = np.arange(n, dtype=np.uint64) * step
-    lens = np.full(n, L, np.uint16)
-    want = Oracle().rx_batch(ring, off, lens, opts=make_opts(bytes(range(1, 17))), nthreads=8)
-    want = want.view(np.uint8).reshape(n, 64)
-    ctx = RxContext(0, bytes(range(1, 17)), max_batch=65536, max_frame=1518, gather_threads=8)
-    pkts = ldp_packets(ring, off, lens)
-    assert np.array_equal(ctx.batch_host(pkts).view(np.uint8).reshape(n, 64), want)
-    ctx.register_ring(ring)
-    for _ in range(2):
-        assert np.array_equal(ctx.batch_host(pkts).view(np.uint8).reshape(n, 64), want)
-    ctx.unregister_ring(ring)
-    ctx.close()
+@pytest.mark.parametrize("gap,pct", [(0, None), (7, None), (1500, None), (548, 70)])
+def test_registered_ring_span_dma(gap, pct, dev):
+    """A registered ring holding 70 000 C1500 frames `gap` bytes apart
+    (tests/ringcase.py): dense chunks (gap 0 or 7) go down as one DMA span
+    with rebased offsets; a sparse ring (gap 1500: half the span is frames)
+    is read in place by the kernel; with the threshold lowered to 70 %
+    (PPTK_RX_RING_DMA_PCT, read once per process: a child process) 2 KB
+    netmap-style slots (gap 548: 73 % frames) go down by DMA too, into a
+    device buffer grown for the longer span.  The short last chunk runs
+    direct.  Every record equals the CPU oracle's, and the same through
+    staging."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    if pct is None:
+        sys.path.insert(0, here)
+        import ringcase
+        ringcase.run(gap)
+        return
+    env = dict(os.environ, PPTK_RX_RING_DMA_PCT=str(pct))
+    r = subprocess.run([sys.executable, os.path.join(here, "ringcase.py"), str(gap)],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 @pytest.mark.parametrize("seed", [0, 1])

@@ -29,6 +29,14 @@ def main():
         b = make_batch(cfg, n, dev)
         stride = b["stride"]
         ring = b["frames"][: n * stride + 64].cpu().numpy()     # pageable host "ring"
+        slot = int(os.environ.get("E2E_SLOT", "0"))
+        if slot > stride:
+            # netmap-style fixed slots: frame i at i * slot (E2E_SLOT bytes)
+            packed = ring
+            ring = np.zeros(n * slot + 64, np.uint8)
+            np.lib.stride_tricks.as_strided(ring, (n, stride), (slot, 1))[:] = \
+                packed[: n * stride].reshape(n, stride)
+            out["slot"] = slot
         ref = torch.empty((n, 64), dtype=torch.uint8, device=dev)
         gt = int(os.environ.get("E2E_GATHER_THREADS", "8"))
         ctx = RxContext(0, bytes(range(1, 17)), max_batch=chunk, max_frame=1518,
@@ -36,7 +44,7 @@ def main():
         out["gather_threads"] = gt
         ctx.batch_device(b["frames"], n, stride=stride, fixed_len=b["fixed_len"], recs=ref)
         want = ref.cpu().numpy()
-        pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
+        pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * max(stride, slot),
                            np.full(n, b["fixed_len"], np.uint16))
         res = {}
         for mode in os.environ.get("E2E_MODES", "staged,ring").split(","):
