@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <condition_variable>
 #include <functional>
@@ -826,6 +828,28 @@ static double ring_dma_density() {
   return v / 100.0;
 }
 
+// Copy one frame into 16-byte-aligned pinned staging with non-temporal
+// stores: the lines go to memory without being read for ownership first
+// and without staying dirty in the host caches, where the copy engine's
+// reads of the staging would have to snoop them.  The bytes past the frame
+// up to the next 16-byte boundary are zero (the kernel never uses them).
+// PPTK_RX_NT_GATHER=0: plain memcpy (A/B).
+static bool nt_gather() {
+  static const long v = env_long("PPTK_RX_NT_GATHER", 1);
+  return v != 0;
+}
+
+static void stage_frame(uint8_t *dst, const uint8_t *src, size_t n) {
+  size_t k = 0;
+  for (; k + 16 <= n; k += 16)
+    _mm_stream_si128((__m128i *)(dst + k), _mm_loadu_si128((const __m128i *)(src + k)));
+  if (k < n) {
+    alignas(16) uint8_t t[16] = {0};
+    memcpy(t, src + k, n - k);
+    _mm_stream_si128((__m128i *)(dst + k), _mm_load_si128((const __m128i *)t));
+  }
+}
+
 // The context's worker pool (nullptr with gather_threads <= 1).  If the
 // threads cannot be started the batch runs on the calling thread alone (and
 // later batches try again): no exception leaves the C ABI.
@@ -970,9 +994,17 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
       for (size_t i = 0; i < cnt; ++i) sl.h_off[i] -= lo;
     if (!ring) {
       const struct ldp_packet *cp = pkts + first;
-      auto gather = [&sl, cp](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i)
-          if (sl.h_len[i]) memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
+      const bool nt = nt_gather();
+      auto gather = [&sl, cp, nt](size_t lo, size_t hi) {
+        if (nt) {
+          for (size_t i = lo; i < hi; ++i)
+            if (sl.h_len[i])
+              stage_frame(sl.h_frames + sl.h_off[i], (const uint8_t *)cp[i].data, sl.h_len[i]);
+          _mm_sfence();   // this thread's streaming stores before the copy is queued
+        } else {
+          for (size_t i = lo; i < hi; ++i)
+            if (sl.h_len[i]) memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
+        }
       };
       if (!pool || cnt < 1024) {
         gather(0, cnt);
