@@ -141,6 +141,8 @@ struct pptk_rx_ctx {
   pptk_rx_opts opts{};
   RxKArgs tmpl{};      // key/iphash part of the kernel arguments
   void *d_zero = nullptr;  // 64 zeroed device bytes (RxKArgs::zero)
+  uint64_t *d_txside = nullptr;   // two-pass tx: 8 B per frame (grown on demand)
+  uint64_t txside_n = 0;
   int ncu = 256;
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
@@ -218,6 +220,7 @@ int pptk_rx_ctx_create(struct pptk_rx_ctx **out, const struct pptk_rx_opts *opts
   }
   if (hipMalloc(&c->d_zero, 64) != hipSuccess || hipMemset(c->d_zero, 0, 64) != hipSuccess) {
     (void)hipFree(c->d_zero);
+  (void)hipFree(c->d_txside);
     delete c;
     return -ENOMEM;
   }
@@ -553,6 +556,17 @@ int pptk_rx_place_records(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch 
   return pptk_rx_place_buffers(c, b, &f0, 1, cands, ncand, reps, &bf, best, ms_out, stream);
 }
 
+// Tx in two passes (fixed-stride batches): the streaming pass records each
+// frame's checksum fields in a side array (8 B per frame) and a second
+// kernel writes them, so that the 2-byte field writes do not land beside
+// the 25 GB read stream (DESIGN.md "Secondary kernels").
+// PPTK_TX_TWO_PASS=0: the fields are stored in place by the streaming pass
+// (A/B).
+static bool tx_two_pass() {
+  static const long v = env_long("PPTK_TX_TWO_PASS", 1);
+  return v != 0;
+}
+
 int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,
                          const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
                          uint64_t n, uint32_t max_len, void *stream) {
@@ -579,6 +593,15 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
   }
   const uint32_t maxlen = d_len ? (max_len ? max_len : 65535u) : fixed_len;
   int variant = pick_variant(maxlen + mmax);
+  const bool two_pass = !d_off && tx_two_pass();
+  if (two_pass) {
+    // the streaming pass of a two-pass batch moves what the receive
+    // transform moves minus most of the writes: pptk_rx_autotune's choice
+    // for this shape applies (T32S3D7 5.14 ms vs T16S6 5.30 on C1500,
+    // DESIGN.md "Secondary kernels")
+    const int tv = c->tuned[0][variant];
+    if (tv >= 0 && tv != RX_L4) variant = tv;
+  }
   const int fv = forced_variant(c);
   if (fv >= 0 && fv != RX_L4) variant = fv;   // the lane kernel has no tx mode
   RxKArgs a = batch_args(c, &b);
@@ -587,7 +610,29 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
   a.tune = c->forced_flags >= 0 ? (uint32_t)c->forced_flags & kTuneMask
                                 : pick_tune(c, variant, d_off || d_len) &
                                       ~(uint32_t)PPTK_RX_TUNE_NT_LOADS;
-  return hip_err(launch_rx(variant, a, grid_for(c, variant, n), (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  if (two_pass) {
+    // Fixed-stride batches: the streaming pass writes nothing into the
+    // frames (so it may use non-temporal loads, as the receive transform
+    // does); the fields go to the context's side array and a second pass
+    // writes them.  Offset-described batches keep the in-place stores:
+    // their streaming pass is slower with non-temporal loads, and the
+    // fields stored beside it cost less than the second pass.
+    if (c->forced_flags < 0)
+      a.tune = pick_tune(c, variant, false);
+    if (c->txside_n < n) {
+      uint64_t *p = nullptr;
+      if (hipMalloc((void **)&p, n * 8) != hipSuccess) return -ENOMEM;
+      (void)hipFree(c->d_txside);   // (synchronous: earlier tx batches are done with it)
+      c->d_txside = p;
+      c->txside_n = n;
+    }
+    a.txside = c->d_txside;
+    hipError_t e = launch_rx(variant, a, grid_for(c, variant, n), s);
+    if (e == hipSuccess) e = launch_tx_apply(c->d_txside, d_frames, d_off, stride, n, s);
+    return hip_err(e);
+  }
+  return hip_err(launch_rx(variant, a, grid_for(c, variant, n), s));
 }
 
 int pptk_tx_rewrite_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,

@@ -52,6 +52,10 @@ struct RxKArgs {
   uint32_t tune;         // A/B knobs (PPTK_RX_TUNE): bit0 nt frame loads, bit1 no LDS record staging
   const void *zero;      // >= 16 zeroed device bytes (owned by the context)
   uint8_t *frames_w;     // tx batches: frames (writable) whose checksums are set
+  // tx, two passes: the fields go to txside[i] (u16 offset, u16 value, twice;
+  // offset 0xffff = none) instead of the frames, and launch_tx_apply writes
+  // them after the streaming pass
+  uint64_t *txside;
   // Derived by launch_rx for the GATHER kernels: branch-free descriptor
   // loads.  An absent array is read at index 0 of `zero` (msk = 0) and its
   // arithmetic stand-in (identity, i * stride_g, fixed_g) is added instead.
@@ -96,6 +100,10 @@ constexpr int kGroupVariant[kGroups] = {RX_T4S2, RX_T8S2, RX_T16S2, RX_T16S4, RX
                                         RX_T64S2};
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
+// tx second pass: frames[base(i) + off] = value (big-endian) for the
+// fields txside[i] names; base(i) = off ? off[i] : i * stride
+hipError_t launch_tx_apply(const uint64_t *txside, uint8_t *frames, const uint64_t *off,
+                           uint64_t stride, uint64_t n, hipStream_t s);
 hipError_t launch_rewrite(const RxKArgs &a, int grid, hipStream_t s);
 hipError_t launch_mss_clamp(const RxKArgs &a, int grid, hipStream_t s);
 int rx_variant_blocks_per_cu(int variant);

@@ -468,8 +468,10 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
   return b;
 }
 
-// Tx: store the checksum fields txp[k] (frame offsets, -1 = none) with
-// values txv[k], network byte order.  Each field is a 2-byte write into a
+// Tx, in place (offset-described batches; fixed-stride ones run in two
+// passes through RxKArgs::txside and tx_apply_kernel): store the checksum
+// fields txp[k] (frame offsets, -1 = none) with values txv[k], network byte
+// order.  Each field is a 2-byte write into a
 // line this wave read long before, so every field costs the memory a whole
 // write granule; writing 16/32/64-byte granules around the fields from the
 // patched LDS image instead was measured no faster, nor were
@@ -494,7 +496,22 @@ struct LaneRec {
   uint64_t fh;
   uint32_t flags;
   u32x4 frag;   // struct pptk_rx_frag (only when RxKArgs::frag is set)
+  uint64_t tx;  // two-pass tx: the txside entry (only when RxKArgs::txside is set)
 };
+
+constexpr uint64_t kTxNone = 0x0000ffff0000ffffull;   // no field to set
+
+// The txside entry of a frame: (offset, value) of the IPv4 header checksum
+// field and of the L4 checksum field, 0xffff offsets for none.
+__device__ __forceinline__ uint64_t tx_entry(const int txp[2], const uint32_t txv[2]) {
+  uint64_t e = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t f = txp[k] < 0 ? 0xffffull : ((uint64_t)txp[k] | ((uint64_t)txv[k] << 16));
+    e |= f << (32 * k);
+  }
+  return e;
+}
 
 // struct pptk_rx_frag (include/pptk_rx.h) of a parsed frame: the IPv4
 // fragment fields (ip_id :1093, ip_frag_off :1124, ip_more_frags :1023,
@@ -545,6 +562,7 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
   const Parse p = parse_frame(v, len);
   if (a.frag)
     o.frag = frag_words(v, p);
+  o.tx = kTxNone;
   uint32_t flags = p.flags;
   const uint32_t l3 = p.l3, rs = p.rs, re = p.re, proto = p.proto;
   uint32_t *w = o.w;
@@ -623,7 +641,9 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
       if (proto == 17 && (v.le32((int)rs + 4) >> 16) == 0)
         flags |= PPTK_RX_F_UDP_ZERO;
     }
-    if (a.frames_w && !(a.tune & 512u))   // bit 9: diagnostics, no tx writes
+    if (a.txside)
+      o.tx = tx_entry(txp, txv);
+    else if (a.frames_w && !(a.tune & 512u))   // bit 9: diagnostics, no tx writes
       tx_store(a, base, txp, txv);
     uint32_t bucket = 0;
     if (a.recs || a.recs32 || a.hash) {   // tx batches need no hashes
@@ -1002,6 +1022,8 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
                            16 * IMGC - m};
       LaneRec o;
       lane_generic(a, v, dc.len, dc.base, my_sum, tailc, o);
+      if (a.txside)
+        a.txside[dc.idx] = o.tx;   // two-pass tx: 8 B per frame, coalesced in batch order
       // park the record in LDS (every lane's image reads are behind us in
       // program order) for the coalesced store below
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
@@ -1445,6 +1467,42 @@ int blocks_per_cu() {
   X(RX_T16S4, 16, 4, 3, 4)
 
 }  // namespace
+
+// Two-pass tx, second pass: one thread per frame writes the (at most two)
+// checksum fields the streaming pass left in txside -- the only writes of
+// the operation, issued without a read stream beside them.
+__global__ __launch_bounds__(256) void tx_apply_kernel(const uint64_t *__restrict__ side,
+                                                       uint8_t *__restrict__ frames,
+                                                       const uint64_t *__restrict__ off,
+                                                       uint64_t stride, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = side[i];
+    const uint64_t base = off ? off[i] : i * stride;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t f = (uint32_t)(e >> (32 * k));
+      const uint32_t o = f & 0xffffu;
+      if (o == 0xffffu) continue;
+      uint8_t *p = frames + base + o;
+      if (((uintptr_t)p & 1u) == 0) {
+        *(uint16_t *)p = (uint16_t)bswap16(f >> 16);   // network order
+      } else {
+        p[0] = (uint8_t)(f >> 24);
+        p[1] = (uint8_t)(f >> 16);
+      }
+    }
+  }
+}
+
+hipError_t launch_tx_apply(const uint64_t *txside, uint8_t *frames, const uint64_t *off,
+                           uint64_t stride, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(tx_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, txside, frames,
+                     off, stride, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s) {
   if (variant == RX_L4) {

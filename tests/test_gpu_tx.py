@@ -64,12 +64,39 @@ def test_tx_matches_reference(name, shift, dev):
     assert not big[:shift].any().item() and not frames[buf_in.size:].any().item()
 
 
-@pytest.mark.parametrize("stride", [64])
-def test_tx_fixed_stride(stride, dev):
+@pytest.mark.parametrize("shift", [0, 5, 6])
+def test_tx_fixed_stride(shift, dev):
+    """Fixed-stride batches run in two passes (streaming pass -> side array
+    -> field writes; 16-bit stores at even addresses, byte stores at odd
+    ones): every variant, even and odd frame addresses."""
+    from pptk_amd.rx import lib
     z, buf_in, buf_out = _case("c64")
-    assert np.all(z["off"] == np.arange(len(z["off"]), dtype=np.uint64) * stride)
-    _, frames = _tx(_ctx(), z, buf_in, dev, 5, stride=stride)
-    assert np.array_equal(frames[:buf_in.size].cpu().numpy(), buf_out)
+    assert np.all(z["off"] == np.arange(len(z["off"]), dtype=np.uint64) * 64)
+    ctx = _ctx()
+    for v in [-1] + list(range(lib().pptk_rx_variant_count())):
+        ctx.set_tuning(v, -1 if v < 0 else v % 4)
+        big, frames = _tx(ctx, z, buf_in, dev, shift, stride=64)
+        assert np.array_equal(frames[:buf_in.size].cpu().numpy(), buf_out), f"variant {v}"
+        assert not big[:shift].any().item() and not frames[buf_in.size:].any().item()
+
+
+def test_tx_c1500_fixed_stride_vs_oracle(dev):
+    """20 000 C1500 frames (fixed stride 1500, ~1 % corrupted checksums)
+    through the two-pass tx against the CPU restatement's tx_batch, twice
+    (the second call reuses the context's side array)."""
+    from oracle.oracle import Oracle
+    from tools.synth import make_batch
+    n = 20_000
+    b = make_batch("c1500", n, dev)
+    host = b["frames"][: n * 1500].cpu().numpy().copy()
+    want = Oracle().tx_batch(host, stride=1500, fixed_len=1500, n=n)
+    assert (want != host).any()
+    ctx = _ctx()
+    for _ in range(2):
+        fr = torch.from_numpy(host).to(dev)
+        ctx.tx_cksum_device(fr, n, stride=1500, fixed_len=1500)
+        torch.cuda.synchronize()
+        assert np.array_equal(fr.cpu().numpy(), want)
 
 
 def test_tx_every_variant(dev):
@@ -99,3 +126,17 @@ def test_tx_then_rx_verifies(name, dev):
     assert v4.sum() > 10 and ((fl[v4] & F_IP_OK) != 0).all()
     l4 = (fl & F_L4) != 0
     assert l4.sum() > 10 and ((fl[l4] & F_L4_OK) != 0).all()
+
+
+def test_tx_in_place_mode(dev):
+    """PPTK_TX_TWO_PASS=0 (the streaming pass stores the fields itself, no
+    side array): the same bytes as the reference, in a child process since
+    the switch is read once per process (tests/txcase.py)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PPTK_TX_TWO_PASS="0")
+    r = subprocess.run([sys.executable, os.path.join(here, "txcase.py")], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
