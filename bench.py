@@ -130,7 +130,7 @@ def gather_bw(per, ws, seconds):
     return round(alg, 1), round(alg * (ws - 1) / ws, 1)
 
 
-PLACE_FRAMES = 3          # frame-buffer candidates (a fresh synthetic batch)
+PLACE_FRAMES = 4          # frame-buffer candidates (a fresh synthetic batch)
 PLACE_RECORDS = 8         # record-buffer candidates
 # Freed device memory is scrubbed by the driver in the background (SOCCLK
 # at 1.2 GHz while it runs, `tools/clock_probe.py --free-gb`): ~1 s after
@@ -164,7 +164,7 @@ def _spaced(dev, count, nbytes, spacer, hold):
 
 
 def placed_buffers(ctx, b, n, dev, compact, kw, frames=True, nf=PLACE_FRAMES,
-                   nr=PLACE_RECORDS):
+                   nr=PLACE_RECORDS, autotune=True):
     """Place the batch's buffers (pptk_rx_place_buffers): what the memory
     charges for the record writes beside the frame reads depends on where
     the frame buffer and the record buffer sit physically (the same launch:
@@ -182,9 +182,9 @@ def placed_buffers(ctx, b, n, dev, compact, kw, frames=True, nf=PLACE_FRAMES,
     free, _ = torch.cuda.mem_get_info(dev)
     if not frames:
         nf = 1
-    while nf > 1 and (nf - 1) * (fbytes + spacer_f) + nr * (n * rb + spacer_r) > 0.5 * free:
+    while nf > 1 and (nf - 1) * (fbytes + spacer_f) + nr * (n * rb + spacer_r) > 0.6 * free:
         nf -= 1
-    while nr > 1 and (nf - 1) * (fbytes + spacer_f) + nr * (n * rb + spacer_r) > 0.5 * free:
+    while nr > 1 and (nf - 1) * (fbytes + spacer_f) + nr * (n * rb + spacer_r) > 0.6 * free:
         nr -= 1
     hold = []
     fc = [b["frames"]]
@@ -192,6 +192,10 @@ def placed_buffers(ctx, b, n, dev, compact, kw, frames=True, nf=PLACE_FRAMES,
         t.copy_(b["frames"])
         fc.append(t)
     rc = [t.view(n, rb) for t in _spaced(dev, nr, n * rb, spacer_r, hold)]
+    if autotune:
+        # the probe times the shape later batches will run (pptk_rx_autotune
+        # on the as-allocated pair; run_config tunes again on the chosen one)
+        ctx.autotune(fc[0], n, recs=rc[0], compact=compact, reps=9, **kw)
     fi, ri, ms = ctx.place_buffers(fc, n, rc, compact=compact, **kw)
     b["frames"] = fc[fi]
     recs = rc[ri]
@@ -288,7 +292,8 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
         # charges for the record writes by up to 25 %:
         # pick a well-placed pair, untimed, as a long-lived rx ring would be
         # set up once (a reused batch keeps its frames: records only)
-        recs, placement = placed_buffers(ctx, b, n, dev, compact, kw, frames=batch is None)
+        recs, placement = placed_buffers(ctx, b, n, dev, compact, kw, frames=batch is None,
+                                         autotune=autotune)
     else:
         recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
     gplace = None
