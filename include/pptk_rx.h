@@ -247,7 +247,10 @@ int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *ctx, uint32_t *d_tokens,
  * located exactly as pptk_rx_batch_device parses.  Frames the receive
  * transform would not parse are left untouched.  After it, the receive
  * transform verifies every such frame (IP_OK / L4_OK).  Layout arguments as
- * in pptk_rx_dev_batch; max_len is a tuning hint.  Asynchronous. */
+ * in pptk_rx_dev_batch; max_len is a tuning hint.  Asynchronous.
+ * Fixed-stride batches run in two passes (checksums into a side array of 8
+ * bytes per frame that the context allocates on first use and keeps, then
+ * the field writes); PPTK_TX_TWO_PASS=0 stores the fields in place. */
 int pptk_tx_cksum_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint64_t *d_off,
                          const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
                          uint64_t n, uint32_t max_len, void *stream);
