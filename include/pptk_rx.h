@@ -255,6 +255,15 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint6
                          const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
                          uint64_t n, uint32_t max_len, void *stream);
 
+/* The two-pass side array from the caller: `frames` * 8 bytes of device
+ * memory (8-byte aligned) that the context uses instead of allocating its
+ * own, e.g. a buffer placed like a record ring (its writes beside the
+ * frame reads cost what record writes cost: pptk_rx_place_records).  The
+ * buffer must stay valid until the context is destroyed or another buffer
+ * (or NULL: back to the context's own) is set; batches larger than
+ * `frames` make the context allocate its own again. */
+int pptk_tx_set_side_buffer(struct pptk_rx_ctx *ctx, void *d_side, uint64_t frames);
+
 /* Header rewrite with incremental checksum update (NAT / forwarding),
  * reference iphdr/ipcksum.h:213-393: per frame, in this order,
  *   PPTK_RW_DECR_TTL  ip_decr_ttl_cksum_update          (:374-393)

@@ -143,6 +143,7 @@ struct pptk_rx_ctx {
   void *d_zero = nullptr;  // 64 zeroed device bytes (RxKArgs::zero)
   uint64_t *d_txside = nullptr;   // two-pass tx: 8 B per frame (grown on demand)
   uint64_t txside_n = 0;
+  bool txside_owned = true;       // false: the caller's (pptk_tx_set_side_buffer)
   int ncu = 256;
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
@@ -220,7 +221,6 @@ int pptk_rx_ctx_create(struct pptk_rx_ctx **out, const struct pptk_rx_opts *opts
   }
   if (hipMalloc(&c->d_zero, 64) != hipSuccess || hipMemset(c->d_zero, 0, 64) != hipSuccess) {
     (void)hipFree(c->d_zero);
-  (void)hipFree(c->d_txside);
     delete c;
     return -ENOMEM;
   }
@@ -272,6 +272,7 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
   free_staging(c);
   delete c->pool;
   (void)hipFree(c->d_zero);
+  if (c->txside_owned) (void)hipFree(c->d_txside);
   for (const RxRing &r : c->rings) (void)hipHostUnregister(r.host);
   delete c;
 }
@@ -623,9 +624,11 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
     if (c->txside_n < n) {
       uint64_t *p = nullptr;
       if (hipMalloc((void **)&p, n * 8) != hipSuccess) return -ENOMEM;
-      (void)hipFree(c->d_txside);   // (synchronous: earlier tx batches are done with it)
+      if (c->txside_owned)
+        (void)hipFree(c->d_txside);   // (synchronous: earlier tx batches are done with it)
       c->d_txside = p;
       c->txside_n = n;
+      c->txside_owned = true;
     }
     a.txside = c->d_txside;
     hipError_t e = launch_rx(variant, a, grid_for(c, variant, n), s);
@@ -633,6 +636,17 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
     return hip_err(e);
   }
   return hip_err(launch_rx(variant, a, grid_for(c, variant, n), s));
+}
+
+int pptk_tx_set_side_buffer(struct pptk_rx_ctx *c, void *d_side, uint64_t frames) {
+  if (!c || (!d_side && frames) || ((uintptr_t)d_side & 7u)) return -EINVAL;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
+  if (c->txside_owned) (void)hipFree(c->d_txside);
+  c->d_txside = (uint64_t *)d_side;
+  c->txside_n = d_side ? frames : 0;
+  c->txside_owned = d_side == nullptr;
+  return 0;
 }
 
 int pptk_tx_rewrite_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_t *d_off,

@@ -45,7 +45,8 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
-           "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_rewrite_device",
+           "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_set_side_buffer",
+           "pptk_tx_rewrite_device",
            "pptk_tcp_mss_clamp_device", "pptk_rx_autotune", "pptk_rx_place_records",
            "pptk_rx_place_buffers",
            # multi-GPU (RCCL)
@@ -92,6 +93,9 @@ def lib(path=None):
             L.pptk_tx_cksum_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
                                                ctypes.c_uint64, ctypes.c_uint32, vp]
             L.pptk_tx_cksum_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_tx_set_side_buffer"):      # absent from older A/B builds
+            L.pptk_tx_set_side_buffer.argtypes = [vp, vp, ctypes.c_uint64]
+            L.pptk_tx_set_side_buffer.restype = ctypes.c_int
         if hasattr(L, "pptk_tx_rewrite_device"):       # absent from older A/B builds
             L.pptk_tx_rewrite_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp]
@@ -378,6 +382,16 @@ class RxContext:
                                           fixed_len, n, max_len, ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise OSError(-rc, f"pptk_tx_cksum_device failed ({rc})")
+
+    def tx_set_side_buffer(self, buf):
+        """pptk_tx_set_side_buffer: `buf` (a CUDA tensor of >= 8 bytes per
+        frame, kept alive by the caller) as the two-pass tx side array, or
+        None for the context's own."""
+        nbytes = 0 if buf is None else buf.numel() * buf.element_size()
+        rc = self._L.pptk_tx_set_side_buffer(self._ctx, _dp(buf), nbytes // 8)
+        if rc != 0:
+            raise OSError(-rc, f"pptk_tx_set_side_buffer failed ({rc})")
+        self._tx_side = buf
 
     def tx_rewrite_device(self, frames, n, rw, off=None, lens=None, stride=0, fixed_len=0,
                           status=None, stream=None):

@@ -293,6 +293,47 @@ def txplace(args):
           flush=True)
 
 
+def txside(args):
+    """Two-pass tx on placed frames: does the side array's placement matter
+    like a record buffer's?  The side array as the context allocates it,
+    the placed record buffer, and six fresh buffers 4 GB apart; tx timed on
+    each (interleaved rounds, median)."""
+    import torch
+    import bench
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    b = make_batch("c1500", n, dev)
+    kw = dict(stride=1500, fixed_len=1500)
+    recs, rep = bench.placed_buffers(ctx, b, n, dev, False, kw)
+    hold, cands = [], []
+    for _ in range(6):
+        hold.append(torch.empty(4 << 30, dtype=torch.uint8, device=dev))
+        cands.append(torch.empty(n * 8, dtype=torch.uint8, device=dev))
+    del hold
+    torch.cuda.synchronize()
+    time.sleep(max(4.0, rep.get("freed_bytes", 0) / 20e9 + 2.0))
+    sides = [None, recs] + cands
+    ms = [[] for _ in sides]
+    for _ in range(4):
+        for i, sd in enumerate(sides):
+            ctx.tx_set_side_buffer(sd)
+            for k in range(4):
+                a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                ctx.tx_cksum_device(b["frames"], n, **kw)
+                z.record()
+                torch.cuda.synchronize()
+                if k:
+                    ms[i].append(a.elapsed_time(z))
+    med = [round(sorted(v)[len(v) // 2], 4) for v in ms]
+    print(json.dumps({"placement_chosen_ms": rep["chosen_ms"], "tx_ms_own_side": med[0],
+                      "tx_ms_side_in_records": med[1], "tx_ms_side_candidates": med[2:]}),
+          flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-mb", type=float, default=16)
@@ -307,6 +348,7 @@ def main():
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--benchpath", action="store_true")
     ap.add_argument("--txplace", action="store_true")
+    ap.add_argument("--txside", action="store_true")
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--spacer-gb", type=float, default=0.0,
                     help="matrix: allocate this many GB before every batch after the first "
@@ -326,6 +368,8 @@ def main():
         return benchpath(args)
     if args.txplace:
         return txplace(args)
+    if args.txside:
+        return txside(args)
     import torch
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch
