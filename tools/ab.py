@@ -4,8 +4,9 @@ on one batch.
     python tools/ab.py c1500 3:1 3:0 6:1 ...        (variant:flags pairs)
     AB_LIBS=old=build/ab_old/libpptkrx.so python tools/ab.py cmix 3:33 old:3:33
 
-A setting is [lib:]variant:flags[:c]; variant or flags -1 = automatic choice;
-a trailing :c writes compact 32-byte records;
+A setting is [lib:]variant:flags[:c][:m]; variant or flags -1 = automatic
+choice; a trailing :c writes compact 32-byte records, :m runs that setting
+through pptk_rx_batch_device_mixed (mixed batches; as AB_MIXED=1 does for all);
 lib names come from AB_LIBS (name=path,...), default = pptk_amd/libpptkrx.so.
 Generates the batch once, then times every setting in interleaved rounds
 (A B C A B C ...) so that clock and thermal drift hit all settings alike;
@@ -25,14 +26,17 @@ sys.path.insert(0, ROOT)
 
 
 def parse_setting(a):
-    """[lib:]variant:flags[:c] -> (lib, variant, flags, compact)."""
+    """[lib:]variant:flags[:c][:m] -> (lib, variant, flags, compact, mixed)."""
     p = a.split(":")
+    mixed = p[-1] == "m"
+    if mixed:
+        p = p[:-1]
     compact = p[-1] == "c"
     if compact:
         p = p[:-1]
     if len(p) == 2:
-        return ("", int(p[0]), int(p[1]), compact)
-    return (p[0], int(p[1]), int(p[2]), compact)
+        return ("", int(p[0]), int(p[1]), compact, mixed)
+    return (p[0], int(p[1]), int(p[2]), compact, mixed)
 
 
 def main():
@@ -67,14 +71,14 @@ def main():
         recs32 = torch.empty((n, 32), dtype=torch.uint8, device=dev)
 
     mixed = bool(os.environ.get("AB_MIXED")) and "off" in b
-    if mixed:
+    if (mixed or any(st[4] for st in settings)) and "off" in b:
         perm = torch.empty(n, dtype=torch.int32, device=dev)
         scratch = torch.empty(ctxs[""]._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
                               device=dev)
 
-    def launch(ctx, compact):
+    def launch(ctx, compact, mix=False):
         recs = recs32 if compact else recs64
-        if mixed:
+        if (mixed or mix) and "off" in b:
             ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], recs=recs64,
                                    max_len=b["max_len"], perm=perm, scratch=scratch)
         elif binned and "off" in b:
@@ -90,7 +94,7 @@ def main():
         for s in settings:
             ctx = ctxs[s[0]]
             ctx.set_tuning(s[1], s[2])
-            launch(ctx, s[3])
+            launch(ctx, s[3], s[4])
             torch.cuda.synchronize()
             if s not in same:       # every setting must give the same records
                 r = recs32 if s[3] else recs64
@@ -100,7 +104,7 @@ def main():
             for _ in range(reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                launch(ctx, s[3])
+                launch(ctx, s[3], s[4])
                 e1.record()
                 torch.cuda.synchronize()
                 times[s].append(e0.elapsed_time(e1))
@@ -108,7 +112,8 @@ def main():
            "box": measure(b["frames"]), "placement": placement}
     for s, t in times.items():
         ms = float(np.median(t))
-        key = ":".join(str(x) for x in s[:3] if x != "") + (":c" if s[3] else "")
+        key = ":".join(str(x) for x in s[:3] if x != "") + (":c" if s[3] else "") + \
+            (":m" if s[4] else "")
         out[key] = {"ms": round(ms, 4), "gbs": round(b["bytes"] / ms / 1e6, 1),
                     "mpkts": round(n / ms / 1e3, 1), "same_records": same[s]}
     print(json.dumps(out))
