@@ -32,6 +32,7 @@
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "rx_internal.h"
 
@@ -41,20 +42,25 @@ namespace {
 
 constexpr int PT = 256;
 
+// flags and src_bucket of record i: one 16-byte load of the record's
+// bytes 48..63 (64-byte records: flags at 54, src_bucket at 56) or 16..31
+// (compact: flags at 20, src_bucket at 28) -- the 32-byte sector both fields
+// share, in one instruction instead of two narrow strided loads
 __device__ __forceinline__ void rec_fields(const PermitArgs &a, uint64_t i, uint32_t &flags,
                                            uint32_t &bucket) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   if (a.recs32) {
-    const uint8_t *r = (const uint8_t *)a.recs32 + i * 32u;
-    flags = *(const uint16_t *)(r + 20);
-    bucket = *(const uint32_t *)(r + 28);
+    const u32x4 q = __builtin_nontemporal_load((const u32x4 *)((const uint8_t *)a.recs32 + i * 32u) + 1);
+    flags = q.y & 0xffffu;
+    bucket = q.w;
   } else {
-    const uint8_t *r = (const uint8_t *)a.recs + i * 64u;
-    flags = *(const uint16_t *)(r + 54);
-    bucket = *(const uint32_t *)(r + 56);
+    const u32x4 q = __builtin_nontemporal_load((const u32x4 *)((const uint8_t *)a.recs + i * 64u) + 3);
+    flags = q.y >> 16;
+    bucket = q.z;
   }
 }
 
-__global__ __launch_bounds__(PT) void permit_keys(PermitArgs a, uint32_t *keys, uint32_t *vals) {
+__global__ __launch_bounds__(PT) void permit_keys(PermitArgs a, uint32_t *keys) {
   const uint64_t i = (uint64_t)blockIdx.x * PT + threadIdx.x;
   if (i >= a.n) return;
   uint32_t flags, bucket;
@@ -62,21 +68,42 @@ __global__ __launch_bounds__(PT) void permit_keys(PermitArgs a, uint32_t *keys, 
   const bool v6 = flags & PPTK_RX_F_IPV6;
   bool subj = (flags & PPTK_RX_F_PARSED) && (a.family == 6 ? v6 : !v6);
   if (a.subject) subj = subj && a.subject[i];
-  keys[i] = subj ? bucket : a.hash_size;
-  vals[i] = (uint32_t)i;
-  if (!subj) a.verdict[i] = 2;
+  keys[i] = subj ? bucket : a.hash_size;   // (verdict 2, written by permit_verdicts)
 }
 
 // Run boundaries of the sorted keys: first[b] and end[b] of every bucket
-// present (non-subject keys, == hash_size, sort last and are skipped).
+// present (non-subject keys, == hash_size, sort last and are skipped).  Four
+// keys per thread (one 16-byte load); the neighbours across a thread's
+// edge come from the adjacent lanes, or from memory at a wave's edge.
+__device__ __forceinline__ void bound_at(const PermitArgs &a, uint32_t *first, uint32_t *end,
+                                         uint64_t p, uint32_t prev, uint32_t b, uint32_t next) {
+  if (b >= a.hash_size) return;
+  if (p == 0 || prev != b) first[b] = (uint32_t)p;
+  if (p + 1 == a.n || next != b) end[b] = (uint32_t)(p + 1);
+}
+
 __global__ __launch_bounds__(PT) void permit_bounds(PermitArgs a, const uint32_t *skeys,
                                                     uint32_t *first, uint32_t *end) {
-  const uint64_t p = (uint64_t)blockIdx.x * PT + threadIdx.x;
-  if (p >= a.n) return;
-  const uint32_t b = skeys[p];
-  if (b >= a.hash_size) return;
-  if (p == 0 || skeys[p - 1] != b) first[b] = (uint32_t)p;
-  if (p + 1 == a.n || skeys[p + 1] != b) end[b] = (uint32_t)(p + 1);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t t = (uint64_t)blockIdx.x * PT + threadIdx.x;
+  const uint64_t p = 4 * t;
+  const int lane = threadIdx.x & 63;
+  const bool whole = p + 4 <= a.n;
+  u32x4 q = (u32x4){0u, 0u, 0u, 0u};
+  if (whole) q = *(const u32x4 *)(skeys + p);
+  // neighbours (every lane takes part in the shuffles)
+  uint32_t prev = __shfl_up(q.w, 1), next = __shfl_down(q.x, 1);
+  if (!whole) {
+    for (uint64_t k = p; k < a.n; ++k)    // the ragged last group
+      bound_at(a, first, end, k, k ? skeys[k - 1] : 0u, skeys[k], k + 1 < a.n ? skeys[k + 1] : 0u);
+    return;
+  }
+  if (lane == 0 && p > 0) prev = skeys[p - 1];
+  if ((lane == 63 || p + 8 > a.n) && p + 4 < a.n) next = skeys[p + 4];   // (lane + 1: ragged)
+  bound_at(a, first, end, p, prev, q.x, q.y);
+  bound_at(a, first, end, p + 1, q.x, q.y, q.z);
+  bound_at(a, first, end, p + 2, q.y, q.z, q.w);
+  bound_at(a, first, end, p + 3, q.z, q.w, next);
 }
 
 // lim[b] per bucket: frames of b with index < lim[b] are permitted (the run
@@ -91,14 +118,28 @@ __global__ __launch_bounds__(PT) void permit_limits(PermitArgs a, const uint32_t
 }
 
 // Verdicts in frame order (coalesced stores; the sorted-order pass this
-// replaces scattered one byte per frame: 0.22 ms per 16 M frames).
+// replaces scattered one byte per frame: 0.22 ms per 16 M frames), the
+// non-subject frames' 2 included.  Four frames per thread: one 16-byte key
+// load, one 4-byte verdict store when the verdict array's alignment allows.
+__device__ __forceinline__ uint32_t verdict_of(const PermitArgs &a, const uint32_t *lim,
+                                               uint64_t i, uint32_t b) {
+  return b >= a.hash_size ? 2u : ((uint32_t)i < lim[b] ? 1u : 0u);   // key hash_size: not subject
+}
+
 __global__ __launch_bounds__(PT) void permit_verdicts(PermitArgs a, const uint32_t *keys,
                                                       const uint32_t *lim) {
-  const uint64_t i = (uint64_t)blockIdx.x * PT + threadIdx.x;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t i = 4 * ((uint64_t)blockIdx.x * PT + threadIdx.x);
   if (i >= a.n) return;
-  const uint32_t b = keys[i];
-  if (b >= a.hash_size) return;       // non-subject: verdict 2 already
-  a.verdict[i] = (uint32_t)i < lim[b] ? 1 : 0;
+  if (i + 4 <= a.n && ((uintptr_t)(a.verdict + i) & 3u) == 0) {
+    const u32x4 q = *(const u32x4 *)(keys + i);
+    *(uint32_t *)(a.verdict + i) = verdict_of(a, lim, i, q.x) | verdict_of(a, lim, i + 1, q.y) << 8 |
+                                   verdict_of(a, lim, i + 2, q.z) << 16 |
+                                   verdict_of(a, lim, i + 3, q.w) << 24;
+    return;
+  }
+  for (uint64_t k = i; k < i + 4 && k < a.n; ++k)
+    a.verdict[k] = (uint8_t)verdict_of(a, lim, k, keys[k]);
 }
 
 __global__ __launch_bounds__(PT) void permit_consume(PermitArgs a, const uint32_t *first,
@@ -121,6 +162,16 @@ __global__ __launch_bounds__(PT) void tokens_refill(uint32_t *tokens, uint32_t s
   tokens[b] = t >= initial ? initial : t;
 }
 
+// Onesweep with 9-bit digits: the keys (log2(hash_size) + 1 bits, 17 for
+// 2^16 buckets) sort in two passes instead of the default 8-bit digits'
+// three; the values are the frame indices, read from a counting iterator
+// (no index array is written).
+using SortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 16>,
+                                        rocprim::kernel_config<512, 16>, 9,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
 int key_bits(uint32_t hash_size) {
   int b = 0;
   while ((1ull << b) <= hash_size) ++b;   // keys 0 .. hash_size inclusive
@@ -130,17 +181,17 @@ int key_bits(uint32_t hash_size) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct PermitScratch {
-  uint32_t *keys, *vals, *skeys, *svals, *first, *end, *lim;
+  uint32_t *keys, *skeys, *svals, *first, *end, *lim;
   void *tmp;
   size_t tmp_bytes, total;
 };
 
 hipError_t layout(uint64_t n, uint32_t hash_size, void *base, PermitScratch &s) {
   size_t sort_tmp = 0;
-  hipError_t e = rocprim::radix_sort_pairs(nullptr, sort_tmp, (uint32_t *)nullptr,
-                                           (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                           (uint32_t *)nullptr, (size_t)n, 0,
-                                           (unsigned)key_bits(hash_size));
+  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
+      nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
+      rocprim::counting_iterator<uint32_t>(0), (uint32_t *)nullptr, (size_t)n, 0,
+      (unsigned)key_bits(hash_size));
   if (e != hipSuccess) return e;
   uint8_t *p = (uint8_t *)base;
   size_t off = 0;
@@ -150,7 +201,6 @@ hipError_t layout(uint64_t n, uint32_t hash_size, void *base, PermitScratch &s) 
     return q;
   };
   s.keys = (uint32_t *)take(n * 4);
-  s.vals = (uint32_t *)take(n * 4);
   s.skeys = (uint32_t *)take(n * 4);
   s.svals = (uint32_t *)take(n * 4);
   s.first = (uint32_t *)take((size_t)hash_size * 8);   // first[hash_size], then end[]
@@ -178,16 +228,18 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   hipError_t e = layout(a.n, a.hash_size, scratch, s);
   if (e != hipSuccess) return e;
   if ((e = hipMemsetAsync(s.first, 0, (size_t)a.hash_size * 8, st)) != hipSuccess) return e;
-  hipLaunchKernelGGL(permit_keys, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.keys, s.vals);
+  hipLaunchKernelGGL(permit_keys, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.keys);
   size_t tb = s.tmp_bytes;
-  e = rocprim::radix_sort_pairs(s.tmp, tb, s.keys, s.skeys, s.vals, s.svals, (size_t)a.n, 0,
-                                (unsigned)key_bits(a.hash_size), st);
+  e = rocprim::radix_sort_pairs<SortConfig>(s.tmp, tb, s.keys, s.skeys,
+                                            rocprim::counting_iterator<uint32_t>(0), s.svals,
+                                            (size_t)a.n, 0, (unsigned)key_bits(a.hash_size), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(permit_bounds, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.skeys, s.first,
-                     s.end);
+  hipLaunchKernelGGL(permit_bounds, dim3(blocks((a.n + 3) / 4)), dim3(PT), 0, st, a, s.skeys,
+                     s.first, s.end);
   hipLaunchKernelGGL(permit_limits, dim3(blocks(a.hash_size)), dim3(PT), 0, st, a, s.svals,
                      s.first, s.end, s.lim);
-  hipLaunchKernelGGL(permit_verdicts, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.keys, s.lim);
+  hipLaunchKernelGGL(permit_verdicts, dim3(blocks((a.n + 3) / 4)), dim3(PT), 0, st, a, s.keys,
+                     s.lim);
   hipLaunchKernelGGL(permit_consume, dim3(blocks(a.hash_size)), dim3(PT), 0, st, a, s.first,
                      s.end);
   return hipGetLastError();

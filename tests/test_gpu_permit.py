@@ -125,3 +125,33 @@ def test_permit_rejects_disabled_family(dev):
     tok = torch.zeros(64, dtype=torch.int32, device=dev)
     with pytest.raises(OSError):
         ctx.permit_device(recs, 6, tok)
+
+
+@pytest.mark.parametrize("n", [(1 << 20) + 3, 4097])
+def test_permit_ragged_batch_unaligned_verdicts(n, dev):
+    """A frame count that is not a multiple of 4 (the bounds and verdict
+    passes take four frames per thread, the ragged rest one by one), on the
+    onesweep (> 1 M) and the small-batch sort paths, into a verdict array
+    that starts at an odd address (byte stores instead of 4-byte ones):
+    GPU == frame-by-frame restatement."""
+    from oracle.oracle import Oracle
+    from pptk_amd.records import F_IPV6, F_PARSED
+    rng = np.random.default_rng(n)
+    hs = 1 << 16
+    r = np.zeros(n, dtype=REC_DTYPE)
+    r["flags"] = np.where(rng.random(n) < 0.95, F_PARSED, 0) | np.where(rng.random(n) < 0.1,
+                                                                        F_IPV6, 0)
+    r["src_bucket"] = np.minimum(rng.zipf(1.5, n) - 1, hs - 1)
+    tok_h = rng.integers(0, 50, hs).astype(np.uint32)
+    ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+    recs = torch.from_numpy(r.view(np.uint8).reshape(n, 64)).to(dev)
+    tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
+    vbuf = torch.full((n + 8,), 0xEE, dtype=torch.uint8, device=dev)
+    v = ctx.permit_device(recs, 4, tok, verdict=vbuf[1:n + 1])
+    vh, th = Oracle().permit_batch(r, 4, None, tok_h)
+    torch.cuda.synchronize()
+    got = vbuf.cpu().numpy()
+    assert np.array_equal(got[1:n + 1], vh)
+    assert got[0] == 0xEE and (got[n + 1:] == 0xEE).all()
+    assert np.array_equal(tok.cpu().numpy().view(np.uint32), th)
+    assert v.data_ptr() == vbuf.data_ptr() + 1
