@@ -25,6 +25,15 @@
 
 using namespace pptk;
 
+// One part of a host chunk's descriptors (pptk_rx_batch): the staging bytes
+// its frames take and where they start, a ring chunk's span and frame bytes,
+// the longest frame.
+struct PartDesc {
+  size_t bytes = 0, base = 0;
+  size_t lo = SIZE_MAX, hi = 0, fbytes = 0;
+  uint32_t maxlen = 0;
+};
+
 // One half of the host-batch double buffer: pinned staging, device copies,
 // and the chunk currently in flight on its stream.
 struct RxSlot {
@@ -44,6 +53,7 @@ struct RxSlot {
   pptk_rx_rec *out = nullptr;   // caller's records of the chunk in flight
   size_t count = 0;
   bool busy = false;
+  std::vector<PartDesc> parts;  // pptk_rx_batch's per-part descriptor sums
 };
 
 // The context's host worker threads (opts.gather_threads - 1 of them, started
@@ -924,7 +934,9 @@ static WorkerPool *pool_of(pptk_rx_ctx *c) {
   return c->pool;
 }
 
-// Copy n bytes, split over the pool when it pays (a few MB and up).
+// Copy n bytes, split over the pool when it pays (a few MB and up; 256 KB
+// pieces measured slower than 1 MB ones on C64 chunks: the pool's per-item
+// cost).
 static void copy_out(WorkerPool *pool, void *dst, const void *src, size_t n) {
   constexpr size_t kPiece = 1u << 20;
 #ifdef PPTK_RX_SERIAL_COPYOUT
@@ -1023,56 +1035,86 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
     if ((rc = retire(sl, pool)) != 0) break;
     cnt = std::min(chunk, (size_t)num - first);
     if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes)) != 0) break;
-    // descriptors (and staging offsets) first, serially; then the frame
-    // bytes, split over opts.gather_threads threads (the host memcpy is the
-    // staged path's bottleneck, see DESIGN.md "End-to-end")
+    // Descriptors, then the frame bytes.  On one thread (no pool, or a
+    // small chunk) both in one pass.  With the pool, both in parallel over
+    // parts of the chunk: a first pass writes the lengths (and a ring's
+    // offsets) and sums each part's staging bytes, a serial prefix over the
+    // parts gives each part its staging base, and a second pass writes the
+    // staging offsets while it gathers the frames (a serial descriptor pass
+    // had cost a 65 536-frame C64 chunk as much as the whole parallel
+    // gather, DESIGN.md "End-to-end").
+    const struct ldp_packet *cp = pkts + first;
+    const bool nt = nt_gather();
+    auto stage = [&sl, cp, nt](size_t i) {
+      if (nt) stage_frame(sl.h_frames + sl.h_off[i], (const uint8_t *)cp[i].data, sl.h_len[i]);
+      else memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
+    };
+    // one part: lengths (+ ring offsets / span) and, for staged chunks, the
+    // staging bytes it needs; with `base` given, also the staging offsets
+    // and the gather
+    auto describe = [&sl, cp, ring, maxf, nt, &stage](size_t i0, size_t i1, size_t base,
+                                                      bool gather, PartDesc &d) {
+      size_t pos = base;
+      for (size_t i = i0; i < i1; ++i) {
+        const struct ldp_packet &pk = cp[i];
+        const bool ok = pk.data && pk.sz <= maxf;
+        const uint32_t sz = ok ? pk.sz : 0u;
+        sl.h_len[i] = (uint16_t)sz;
+        if (ring) {
+          const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
+          sl.h_off[i] = o;
+          d.lo = std::min<size_t>(d.lo, o);
+          d.hi = std::max<size_t>(d.hi, o + ((sz + 15) & ~(size_t)15));
+          d.fbytes += sz;
+        } else if (gather) {
+          sl.h_off[i] = pos;
+          if (sz) stage(i);
+        }
+        pos += (sz + 15) & ~(size_t)15;
+        d.maxlen = std::max(d.maxlen, sz);
+      }
+      d.bytes = pos - base;
+      // this thread's streaming stores, before the copy is queued
+      if (gather && nt) _mm_sfence();
+    };
+    const size_t nparts = pool && cnt >= 4096 ? std::min<size_t>((cnt + 1023) / 1024, 64 * pool->size())
+                                              : 1;
+    std::vector<PartDesc> &parts = sl.parts;
+    parts.assign(nparts, PartDesc{});
+    const bool staged = !ring;
+    if (nparts == 1) {
+      describe(0, cnt, 0, staged, parts[0]);
+    } else {
+      pool->parallel_for(nparts, [&](size_t t) {
+        describe(cnt * t / nparts, cnt * (t + 1) / nparts, 0, false, parts[t]);
+      });
+      if (staged) {
+        size_t run = 0;
+        for (PartDesc &d : parts) {
+          const size_t b = d.bytes;
+          d.base = run;
+          run += b;
+        }
+        pool->parallel_for(nparts, [&](size_t t) {
+          PartDesc d2{};
+          describe(cnt * t / nparts, cnt * (t + 1) / nparts, parts[t].base, true, d2);
+        });
+      }
+    }
     size_t pos = 0, lo = SIZE_MAX, hi = 0, fbytes = 0;
     uint32_t maxlen = 0;
-    for (size_t i = 0; i < cnt; ++i) {
-      const struct ldp_packet &pk = pkts[first + i];
-      const bool ok = pk.data && pk.sz <= maxf;
-      const uint32_t sz = ok ? pk.sz : 0u;
-      sl.h_len[i] = (uint16_t)sz;
-      if (ring) {
-        const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
-        sl.h_off[i] = o;
-        lo = std::min<size_t>(lo, o);
-        hi = std::max<size_t>(hi, o + ((sz + 15) & ~(size_t)15));
-        fbytes += sz;
-      } else {
-        sl.h_off[i] = pos;
-        pos += (sz + 15) & ~(size_t)15;
-      }
-      maxlen = std::max(maxlen, sz);
+    for (const PartDesc &d : parts) {
+      pos += d.bytes;
+      lo = std::min(lo, d.lo);
+      hi = std::max(hi, d.hi);
+      fbytes += d.fbytes;
+      maxlen = std::max(maxlen, d.maxlen);
     }
-    // a dense ring chunk goes down as one span (offsets rebased onto it)
+    // a dense ring chunk goes down as one span; the kernel sees the span's
+    // buffer shifted down by `lo`, so the ring offsets stay as they are
     const bool ring_dma = ring && hi > lo && hi - lo > direct_max_bytes() &&
                           (double)fbytes >= ring_dma_density() * (double)(hi - lo) &&
                           fit_span(sl, hi - lo + 16);
-    if (ring_dma)
-      for (size_t i = 0; i < cnt; ++i) sl.h_off[i] -= lo;
-    if (!ring) {
-      const struct ldp_packet *cp = pkts + first;
-      const bool nt = nt_gather();
-      auto gather = [&sl, cp, nt](size_t lo, size_t hi) {
-        if (nt) {
-          for (size_t i = lo; i < hi; ++i)
-            if (sl.h_len[i])
-              stage_frame(sl.h_frames + sl.h_off[i], (const uint8_t *)cp[i].data, sl.h_len[i]);
-          _mm_sfence();   // this thread's streaming stores before the copy is queued
-        } else {
-          for (size_t i = lo; i < hi; ++i)
-            if (sl.h_len[i]) memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
-        }
-      };
-      if (!pool || cnt < 1024) {
-        gather(0, cnt);
-      } else {
-        // pieces of ~256 frames, taken by the workers in turn
-        const size_t parts = std::min<size_t>((cnt + 255) / 256, 64 * pool->size());
-        pool->parallel_for(parts, [&](size_t t) { gather(cnt * t / parts, cnt * (t + 1) / parts); });
-      }
-    }
     hipStream_t s = sl.stream;
     const bool direct =
         ring ? direct_max_bytes() > 0 && !ring_dma : pos <= direct_max_bytes();
@@ -1092,7 +1134,10 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
     }
     pptk_rx_dev_batch b;
     memset(&b, 0, sizeof(b));
-    b.d_frames = ring && !ring_dma ? ring->dev : direct ? sl.hd_frames : sl.d_frames;
+    b.d_frames = ring && !ring_dma ? ring->dev
+                 : ring_dma           ? (const uint8_t *)((uintptr_t)sl.d_frames - lo)
+                 : direct             ? sl.hd_frames
+                                      : sl.d_frames;
     b.d_off = pcie ? sl.hd_off : sl.d_off;
     b.d_len = pcie ? sl.hd_len : sl.d_len;
     b.max_len = maxlen;

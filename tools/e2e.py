@@ -39,9 +39,11 @@ def main():
             out["slot"] = slot
         ref = torch.empty((n, 64), dtype=torch.uint8, device=dev)
         gt = int(os.environ.get("E2E_GATHER_THREADS", "8"))
+        lib = os.environ.get("E2E_LIB")     # A/B: another build of the library
         ctx = RxContext(0, bytes(range(1, 17)), max_batch=chunk, max_frame=1518,
-                        gather_threads=gt)
+                        gather_threads=gt, lib_path=lib)
         out["gather_threads"] = gt
+        out["lib"] = lib
         ctx.batch_device(b["frames"], n, stride=stride, fixed_len=b["fixed_len"], recs=ref)
         want = ref.cpu().numpy()
         pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * max(stride, slot),
@@ -51,7 +53,7 @@ def main():
             if os.environ.get("E2E_FRESH") and res:    # one context per mode
                 ctx.close()
                 ctx = RxContext(0, bytes(range(1, 17)), max_batch=chunk, max_frame=1518,
-                                gather_threads=gt)
+                                gather_threads=gt, lib_path=lib)
             if mode == "ring":
                 ctx.register_ring(ring)
             got = ctx.batch_host(pkts)          # warm-up (allocations)
