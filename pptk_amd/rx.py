@@ -473,10 +473,16 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, "pptk_rx_unregister_ring failed")
 
-    def batch_host(self, pkts):
-        """pptk_rx_batch over a ctypes array of LdpPacket; returns records."""
+    def batch_host(self, pkts, out=None):
+        """pptk_rx_batch over a ctypes array of LdpPacket; returns records
+        (into `out`, a REC_DTYPE array of len(pkts), when given: an rx loop
+        reuses its record array, so its pages are not faulted in per call)."""
         n = len(pkts)
-        recs = np.zeros(n, dtype=REC_DTYPE)
+        if out is not None:
+            assert out.dtype == REC_DTYPE and out.shape == (n,) and out.flags["C_CONTIGUOUS"]
+            recs = out
+        else:
+            recs = np.zeros(n, dtype=REC_DTYPE)
         rc = self._L.pptk_rx_batch(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n,
                                  ctypes.c_void_p(recs.ctypes.data))
         if rc != 0:

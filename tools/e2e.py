@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     import torch
-    from pptk_amd.records import diff_records
+    from pptk_amd.records import REC_DTYPE, diff_records
     from pptk_amd.rx import RxContext, ldp_packets
     from tools.synth import make_batch
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
@@ -49,6 +49,12 @@ def main():
         pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * max(stride, slot),
                            np.full(n, b["fixed_len"], np.uint16))
         res = {}
+        # the records land in one array reused by every call, as in an rx
+        # loop (a fresh 64 MB array per call faulted its pages in inside the
+        # call's copy-out: E2E_FRESH_OUT=1 measures that way)
+        fresh_out = bool(os.environ.get("E2E_FRESH_OUT"))
+        outbuf = None if fresh_out else np.zeros(n, dtype=REC_DTYPE)
+        out["fresh_out"] = fresh_out
         for mode in os.environ.get("E2E_MODES", "staged,ring").split(","):
             if os.environ.get("E2E_FRESH") and res:    # one context per mode
                 ctx.close()
@@ -56,11 +62,11 @@ def main():
                                 gather_threads=gt, lib_path=lib)
             if mode == "ring":
                 ctx.register_ring(ring)
-            got = ctx.batch_host(pkts)          # warm-up (allocations)
+            got = ctx.batch_host(pkts, out=outbuf)          # warm-up (allocations)
             assert not diff_records(got, want), f"{cfg} {mode} parity"
             reps, t0 = 0, time.perf_counter()
             while time.perf_counter() - t0 < 3.0:
-                ctx.batch_host(pkts)
+                ctx.batch_host(pkts, out=outbuf)
                 reps += 1
             el = (time.perf_counter() - t0) / reps
             res[mode] = {"mpkts": round(n / el / 1e6, 2),
