@@ -155,8 +155,11 @@ int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
  * frames fill >= 80 % of the ring span they cover (and that span > 8 MiB)
  * is copied down by DMA as one span, any other chunk is read by the GPU in
  * place over PCIe (PPTK_RX_RING_DMA_PCT sets the fraction).  Every frame's
- * end rounded up to 16 bytes must lie inside the region.  Unregister
- * before freeing the memory. */
+ * end rounded up to 16 bytes must lie inside the region.  A registered
+ * region that holds a call's whole record array (recs[0, num)) receives the
+ * records in place: the kernel writes them there over PCIe and the host
+ * copies nothing back -- register the rx loop's record array once.
+ * Unregister before freeing the memory. */
 int pptk_rx_register_ring(struct pptk_rx_ctx *ctx, void *base, size_t bytes);
 int pptk_rx_unregister_ring(struct pptk_rx_ctx *ctx, void *base);
 

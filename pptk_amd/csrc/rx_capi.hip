@@ -960,7 +960,7 @@ static int retire(RxSlot &sl, WorkerPool *pool) {
   // (HIP spins before it blocks: polling hipEventQuery instead measured
   // equal on 32-frame chunks)
   if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
-  copy_out(pool, sl.out, sl.h_recs, sl.count * 64);
+  if (sl.out) copy_out(pool, sl.out, sl.h_recs, sl.count * 64);
   return 0;
 }
 
@@ -980,6 +980,16 @@ static const RxRing *ring_of(const pptk_rx_ctx *c, const struct ldp_packet *pkts
     }
     return &r;
   }
+  return nullptr;
+}
+
+// The registered region holding the caller's whole record array, so that
+// the kernel writes the records there in place over PCIe (no record copy
+// from the staging); NULL otherwise.
+static const RxRing *records_region(const pptk_rx_ctx *c, const void *recs, size_t bytes) {
+  const uint8_t *p = (const uint8_t *)recs;
+  for (const RxRing &r : c->rings)
+    if (p >= r.host && bytes <= r.bytes && (size_t)(p - r.host) <= r.bytes - bytes) return &r;
   return nullptr;
 }
 
@@ -1021,6 +1031,7 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   if (!dg.ok) return -EIO;
   const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
   const RxRing *ring = ring_of(c, pkts, num);
+  const RxRing *rreg = records_region(c, recs, (size_t)num * sizeof(pptk_rx_rec));
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
   const size_t chunk_bytes = chunk * ((maxf + 15) & ~15u);
   WorkerPool *pool = pool_of(c);
@@ -1142,15 +1153,19 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
     b.d_len = pcie ? sl.hd_len : sl.d_len;
     b.max_len = maxlen;
     b.n = cnt;
-    b.d_recs = pcie ? sl.hd_recs : sl.d_recs;
+    // records: into the caller's array itself when it is registered
+    b.d_recs = rreg ? (pptk_rx_rec *)(rreg->dev + ((const uint8_t *)(recs + first) - rreg->host))
+               : pcie ? sl.hd_recs
+                      : sl.d_recs;
     if ((rc = pptk_rx_batch_device(c, &b, s)) != 0) break;
-    if ((!pcie && hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
-                      hipSuccess) ||
+    if ((!pcie && !rreg &&
+         hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
+             hipSuccess) ||
         hipEventRecord(sl.done, s) != hipSuccess) {
       rc = -EIO;
       break;
     }
-    sl.out = recs + first;
+    sl.out = rreg ? nullptr : recs + first;   // (retire copies only staged records)
     sl.count = cnt;
     sl.busy = true;
   }

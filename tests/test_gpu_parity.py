@@ -331,6 +331,63 @@ def test_host_batch_chunked_and_ring(name, max_batch, threads, dev):
     assert not d, "after unregister: " + d
 
 
+def _pages(nbytes):
+    """A zeroed uint8 buffer starting on a page boundary, whole pages long
+    (nbytes rounded up), with a free page after it."""
+    pg = 4096
+    size = (nbytes + pg - 1) // pg * pg
+    raw = np.zeros(size + 2 * pg, dtype=np.uint8)
+    a = (-raw.ctypes.data) % pg
+    return raw[a:a + size]
+
+
+@pytest.mark.parametrize("max_batch,threads", [(97, 1), (1500, 6), (65536, 8)])
+@pytest.mark.parametrize("name", ["fuzz", "cmix"])
+def test_host_batch_registered_records(name, max_batch, threads, dev):
+    """A registered record array receives the records in place (the kernel
+    writes them over PCIe, nothing is copied back), with staged frames and
+    with frames from a registered ring; an unregistered array and a record
+    array only partly inside a registered region take the copy path; every
+    record against the golden set, and the bytes around the array untouched."""
+    from pptk_amd.records import REC_DTYPE
+    from pptk_amd.rx import RxContext, ldp_packets
+    z = load_golden(name)
+    n = len(z["off"])
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_batch=max_batch, max_frame=65535,
+                    gather_threads=threads)
+    # page-aligned buffers of whole pages: no two registrations share a page
+    ring = _pages(z["buf"].size + 4096)
+    ring[:z["buf"].size] = z["buf"]
+    pkts = ldp_packets(ring, z["off"], z["len"])
+    # the record array inside a larger registered region, 8 records in
+    region = _pages((n + 16) * 64)
+    region[:] = 0x5A
+    region = region[:(n + 16) * 64]
+    out = region[8 * 64:(8 + n) * 64].view(REC_DTYPE)
+    ctx.register_ring(region)
+    for ring_too in (False, True):
+        if ring_too:
+            ctx.register_ring(ring)
+        for _ in range(2):
+            out[:] = np.zeros(1, dtype=REC_DTYPE)
+            got = ctx.batch_host(pkts, out=out)
+            d = diff_records(got, z["recs"])
+            assert not d, f"ring={ring_too}: " + d
+            assert (region[:8 * 64] == 0x5A).all() and (region[(8 + n) * 64:] == 0x5A).all()
+    ctx.unregister_ring(ring)
+    # straddling the region's end: the copy path
+    tail = _pages((n + 4) * 64)
+    ctx.register_ring(tail[: (n // 2) * 64])
+    d = diff_records(ctx.batch_host(pkts, out=tail[64:(n + 1) * 64].view(REC_DTYPE)),
+                     z["recs"])
+    assert not d, "straddling: " + d
+    ctx.unregister_ring(tail[: (n // 2) * 64])
+    ctx.unregister_ring(region)
+    d = diff_records(ctx.batch_host(pkts, out=out), z["recs"])
+    assert not d, "after unregister: " + d
+
+
 def test_ring_edge_falls_back(dev):
     """A frame whose 16-byte-rounded end leaves the registered region makes
     the batch use staging; results stay exact."""

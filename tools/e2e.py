@@ -55,11 +55,19 @@ def main():
         fresh_out = bool(os.environ.get("E2E_FRESH_OUT"))
         outbuf = None if fresh_out else np.zeros(n, dtype=REC_DTYPE)
         out["fresh_out"] = fresh_out
+        # E2E_REG_OUT=1: the record array registered with the context, so the
+        # kernel writes the records into it in place (no copy back)
+        reg_out = bool(os.environ.get("E2E_REG_OUT")) and outbuf is not None
+        out["registered_out"] = reg_out
+        if reg_out:
+            ctx.register_ring(outbuf)
         for mode in os.environ.get("E2E_MODES", "staged,ring").split(","):
             if os.environ.get("E2E_FRESH") and res:    # one context per mode
                 ctx.close()
                 ctx = RxContext(0, bytes(range(1, 17)), max_batch=chunk, max_frame=1518,
                                 gather_threads=gt, lib_path=lib)
+                if reg_out:
+                    ctx.register_ring(outbuf)
             if mode == "ring":
                 ctx.register_ring(ring)
             got = ctx.batch_host(pkts, out=outbuf)          # warm-up (allocations)
@@ -75,6 +83,8 @@ def main():
             if mode == "ring":
                 ctx.unregister_ring(ring)
         out[cfg] = res
+        if reg_out:
+            ctx.unregister_ring(outbuf)
         ctx.close()
         del b, ref
         torch.cuda.empty_cache()
