@@ -171,3 +171,47 @@ def test_bench_one_rank_rccl_path(tmp_path, frames, scaling):
     p = line["parity"]
     assert p["oracle_sample"]["mismatches"] == 0 and all(
         v for k, v in p["full_batch"].items() if k != "corrupted")
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("name", ["fuzz", "cmix"])
+def test_sharded_layout_n_ranks_one_gpu(dev, name, world):
+    """The N-rank data path without the collective: `world` contexts on the
+    one GPU each run their shard (pptk_rx_shard_range: equal shards, the
+    last padded) with the kernel writing the flow hashes into their slice of
+    ONE shared gather buffer -- the array an N-rank in-place all-gather
+    leaves on every rank.  It must hold global frame i's hash at index i, the
+    padding untouched, and every shard's records must equal the golden
+    records of its frames."""
+    from pptk_amd.shard import GatherBuffer
+    z = load_golden(name)
+    n = len(z["off"])
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    want = as_records(z["recs"])
+    shared = None
+    covered = 0
+    for rank in range(world):
+        ctx = _ctx(z)
+        gb = GatherBuffer(n, world, rank, dev, out=shared)
+        if shared is None:
+            shared = gb.out
+            shared.fill_(-1)
+        f, c = gb.first, gb.count
+        assert f == covered and gb.per * world >= n
+        covered += c
+        if c:
+            recs = ctx.batch_device(frames, c, off=off[f:f + c], lens=lens[f:f + c],
+                                    max_len=int(z["len"].max()), hash_out=gb.local[:c])
+            torch.cuda.synchronize()
+            got = recs.cpu().numpy().reshape(-1).view(want.dtype)
+            assert np.array_equal(got, want[f:f + c])
+        ctx.close()
+    assert covered == n
+    h = shared.cpu().numpy().view(np.uint64)
+    assert np.array_equal(h[:n], want["flow_hash"])
+    per = -(-n // world)
+    pad = np.concatenate([h[r * per + max(0, min(per, n - r * per)):(r + 1) * per]
+                          for r in range(world)])
+    assert (pad == np.uint64(0xFFFFFFFFFFFFFFFF)).all()
