@@ -13,7 +13,9 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
+#include <memory>
 #include <functional>
 #include <mutex>
 #include <new>
@@ -54,6 +56,8 @@ struct RxSlot {
   size_t count = 0;
   bool busy = false;
   std::vector<PartDesc> parts;  // pptk_rx_batch's per-part descriptor sums
+  std::unique_ptr<std::atomic<size_t>[]> run;   // the parts' running staging totals
+  size_t run_cap = 0;
 };
 
 // The context's host worker threads (opts.gather_threads - 1 of them, started
@@ -934,6 +938,8 @@ static WorkerPool *pool_of(pptk_rx_ctx *c) {
   return c->pool;
 }
 
+static size_t pool_size(const WorkerPool *pool) { return pool ? pool->size() : 1; }
+
 // Copy n bytes, split over the pool when it pays (a few MB and up; 256 KB
 // pieces measured slower than 1 MB ones on C64 chunks: the pool's per-item
 // cost).
@@ -1088,29 +1094,49 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
       // this thread's streaming stores, before the copy is queued
       if (gather && nt) _mm_sfence();
     };
-    const size_t nparts = pool && cnt >= 4096 ? std::min<size_t>((cnt + 1023) / 1024, 64 * pool->size())
-                                              : 1;
+    // The pool only for big chunks: waking it costs ~20-40 µs, more than a
+    // 256-frame or even a 1.5 MB gather saves (DESIGN.md "End-to-end").
+    // Staged chunks: parts of ~1024 frames or ~256 KB of frame bytes
+    // (estimated from the first frame), at most 8 per thread, in ONE pass
+    // over the pool -- each
+    // part sums its staging bytes, takes its base from the previous part's
+    // published running total (parts are claimed in order, so that one is
+    // done or in progress), publishes its own, then writes its offsets and
+    // gathers.  Ring chunks (no gather): parts of ~2048 frames.
+    const size_t est = cnt * (size_t)std::min<uint32_t>(cp[0].sz, maxf);
+    const bool staged = !ring;
+    size_t nparts = 1;
+    if (pool && staged && (cnt >= 8192 || est >= (4u << 20)))
+      nparts = std::max(cnt / 1024, est >> 18);
+    else if (pool && !staged && cnt >= 16384)
+      nparts = cnt / 2048;
+    nparts = std::max<size_t>(1, std::min<size_t>(nparts, std::min<size_t>(8 * pool_size(pool), cnt)));
     std::vector<PartDesc> &parts = sl.parts;
     parts.assign(nparts, PartDesc{});
-    const bool staged = !ring;
     if (nparts == 1) {
       describe(0, cnt, 0, staged, parts[0]);
-    } else {
+    } else if (!staged) {
       pool->parallel_for(nparts, [&](size_t t) {
         describe(cnt * t / nparts, cnt * (t + 1) / nparts, 0, false, parts[t]);
       });
-      if (staged) {
-        size_t run = 0;
-        for (PartDesc &d : parts) {
-          const size_t b = d.bytes;
-          d.base = run;
-          run += b;
-        }
-        pool->parallel_for(nparts, [&](size_t t) {
-          PartDesc d2{};
-          describe(cnt * t / nparts, cnt * (t + 1) / nparts, parts[t].base, true, d2);
-        });
+    } else {
+      if (sl.run_cap < nparts) {
+        sl.run.reset(new std::atomic<size_t>[nparts]);
+        sl.run_cap = nparts;
       }
+      std::atomic<size_t> *run = sl.run.get();
+      for (size_t t = 0; t < nparts; ++t) run[t].store(SIZE_MAX, std::memory_order_relaxed);
+      pool->parallel_for(nparts, [&](size_t t) {
+        const size_t i0 = cnt * t / nparts, i1 = cnt * (t + 1) / nparts;
+        PartDesc &d = parts[t];
+        describe(i0, i1, 0, false, d);            // lengths, this part's bytes
+        size_t base = 0;
+        if (t > 0)
+          while ((base = run[t - 1].load(std::memory_order_acquire)) == SIZE_MAX) _mm_pause();
+        run[t].store(base + d.bytes, std::memory_order_release);
+        PartDesc d2{};
+        describe(i0, i1, base, true, d2);         // offsets + gather
+      });
     }
     size_t pos = 0, lo = SIZE_MAX, hi = 0, fbytes = 0;
     uint32_t maxlen = 0;

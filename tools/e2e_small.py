@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     import torch
-    from pptk_amd.records import diff_records
+    from pptk_amd.records import REC_DTYPE, diff_records
     from pptk_amd.rx import RxContext, ldp_packets
     from tools.synth import make_batch
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c64"
@@ -29,26 +29,38 @@ def main():
     ring = b["frames"][: nmax * stride + 64].cpu().numpy()
     want = RxContext(0, bytes(range(1, 17))).batch_device(
         b["frames"], nmax, stride=stride, fixed_len=b["fixed_len"]).cpu().numpy()
-    out = {"cfg": cfg}
+    # E2E_OUT=fresh: a new record array per call (the earlier measurement);
+    # reuse (default): one array reused; reg: reused and registered, so the
+    # records land in it directly
+    out_mode = os.environ.get("E2E_OUT", "reuse")
+    out = {"cfg": cfg, "out": out_mode,
+           "gather_threads": int(os.environ.get("E2E_GATHER_THREADS", "1"))}
+    outbuf = np.zeros(nmax, dtype=REC_DTYPE)
     for mode in ("staged", "ring"):
         ctx = RxContext(0, bytes(range(1, 17)), max_batch=nmax, max_frame=1518,
-                        gather_threads=int(os.environ.get("E2E_GATHER_THREADS", "1")))
+                        gather_threads=int(os.environ.get("E2E_GATHER_THREADS", "1")),
+                        lib_path=os.environ.get("E2E_LIB"))    # A/B: another build
         if mode == "ring":
             ctx.register_ring(ring)
+        if out_mode == "reg":
+            ctx.register_ring(outbuf)
         for n in sizes:
             pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
                                np.full(n, b["fixed_len"], np.uint16))
-            got = ctx.batch_host(pkts)
+            o = None if out_mode == "fresh" else outbuf[:n]
+            got = ctx.batch_host(pkts, out=o)
             assert not diff_records(got, want[:n]), (mode, n)
             ts = []
             for _ in range(300 if n <= 4096 else 60):
                 t0 = time.perf_counter()
-                ctx.batch_host(pkts)
+                ctx.batch_host(pkts, out=o)
                 ts.append(time.perf_counter() - t0)
             us = float(np.median(ts)) * 1e6
             out[f"{mode}_{n}"] = {"us_per_call": round(us, 1), "mpkts": round(n / us, 2)}
         if mode == "ring":
             ctx.unregister_ring(ring)
+        if out_mode == "reg":
+            ctx.unregister_ring(outbuf)
         ctx.close()
     print(json.dumps(out))
 
