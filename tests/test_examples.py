@@ -5,7 +5,9 @@ over the golden sets (examples/rxq_file.h frame-set files written here):
                           (reference ldp/ldprecvmt.c:16-67), pptk_rx_batch;
   examples/rx_multigpu.c  one thread per GPU, one RCCL communicator over all
                           of them (pptk_rx_comm_create_all), sharded device
-                          batches and the in-place flow-hash all-gather.
+                          batches and the in-place flow-hash all-gather;
+  examples/rx_perf.c      device-resident throughput from C (ipcksumperf's
+                          GPU counterpart), checked against the host APIs.
 
 Both compare every record (and the gathered hash array) with the
 reference-made golden records, so a passing run is bit-exact parity."""
@@ -62,6 +64,8 @@ def build(tmp_path, name, hip=False):
 def test_examples_build(tmp_path):
     build(tmp_path, "rx_mt")
     build(tmp_path, "rx_multigpu", hip=True)
+    build(tmp_path, "rx_perf", hip=True)
+    build(tmp_path, "rx_loop")
 
 
 def test_rxq_file_layout(tmp_path):
@@ -96,3 +100,17 @@ def test_rx_multigpu_allgather_bit_exact(tmp_path):
                          text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert f"{n} frames, 0 mismatches" in out.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbytes", [1500, 64])
+def test_rx_perf_device_resident_from_c(tmp_path, nbytes):
+    """examples/rx_perf.c: the device-resident throughput timed from a plain
+    C host (the GPU counterpart of iphdr/ipcksumperf.c), its records checked
+    against the kept per-packet C APIs (checksums, getters, siphash_buf)."""
+    exe = build(tmp_path, "rx_perf", hip=True)
+    out = subprocess.run([exe, str(1 << 20), str(nbytes), "5"], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "8192 records checked against the host APIs, 0 mismatches" in out.stdout, out.stdout
+    print(out.stdout)
