@@ -7,9 +7,13 @@
  * ldp/ldpsend.c:141-168), each batch goes through pptk_rx_batch() between
  * "nextpkts" and "deallocate_some", and the loop reports MPPS and the
  * checksum verdicts.  The ring is registered once for zero-copy reads.
+ * With "pipe", batch k+1 is fetched and submitted (pptk_rx_batch_submit)
+ * before batch k is completed and released (pptk_rx_batch_complete, then
+ * deallocate_some), so each batch's GPU round trip overlaps the next one's
+ * host work.
  *
  *   gcc -O2 -Iinclude examples/rx_loop.c -Lpptk_amd -lpptkrx -o rx_loop
- *   ./rx_loop [batches]
+ *   ./rx_loop [batches] [pipe]
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -53,6 +57,32 @@ static void construct_packet(unsigned char *f, uint32_t src, uint32_t dst, uint1
   hdr_set16n(udp + 6, udp_cksum_calc(ip, 20, udp, 8 + PAYLOAD));
 }
 
+static unsigned long ok, bad;
+
+static void tally(const struct pptk_rx_rec *recs, int num)
+{
+  int i;
+  for (i = 0; i < num; i++) {
+    if ((recs[i].flags & (PPTK_RX_F_IP_OK | PPTK_RX_F_L4_OK)) ==
+        (PPTK_RX_F_IP_OK | PPTK_RX_F_L4_OK))
+      ok++;
+    else
+      bad++;
+  }
+}
+
+/* num = ldp_in_nextpkts(inq, pkt_tbl, BATCH): the next BATCH ring slots */
+static void nextpkts(struct ldp_packet *pkt_tbl, unsigned char *ring, unsigned head)
+{
+  int i;
+  for (i = 0; i < BATCH; i++) {
+    unsigned slot = (head + (unsigned)i) % RING_SLOTS;
+    pkt_tbl[i].data = ring + (size_t)slot * SLOT_BYTES;
+    pkt_tbl[i].sz = 14 + 20 + 8 + PAYLOAD;
+    pkt_tbl[i].ancillary = slot;                   /* netmap buf_idx stand-in */
+  }
+}
+
 static double now(void)
 {
   struct timeval tv;
@@ -63,13 +93,16 @@ static double now(void)
 int main(int argc, char **argv)
 {
   int batches = argc > 1 ? atoi(argv[1]) : 2000;
+  int pipe = argc > 2 && strcmp(argv[2], "pipe") == 0;
   unsigned char *ring = aligned_alloc(4096, (size_t)RING_SLOTS * SLOT_BYTES);
-  static struct ldp_packet pkt_tbl[BATCH];
-  static struct pptk_rx_rec recs[BATCH];
+  /* two packet tables and record arrays: batch k+1 is in hand while batch k
+     is still with the GPU (pipelined mode) */
+  static struct ldp_packet pkt_tbl[2][BATCH];
+  static struct pptk_rx_rec recs[2][BATCH];
   struct pptk_rx_opts o;
   struct pptk_rx_ctx *ctx;
   unsigned head = 0;
-  unsigned long pkts = 0, ok = 0, bad = 0;
+  unsigned long pkts = 0;
   double t0;
   int b, i, rc;
 
@@ -95,27 +128,39 @@ int main(int argc, char **argv)
 
   t0 = now();
   for (b = 0; b < batches; b++) {
-    /* num = ldp_in_nextpkts(inq, pkt_tbl, BATCH); */
-    for (i = 0; i < BATCH; i++) {
-      unsigned slot = (head + (unsigned)i) % RING_SLOTS;
-      pkt_tbl[i].data = ring + (size_t)slot * SLOT_BYTES;
-      pkt_tbl[i].sz = 14 + 20 + 8 + PAYLOAD;
-      pkt_tbl[i].ancillary = slot;                   /* netmap buf_idx stand-in */
+    const int k = pipe ? b & 1 : 0;
+    nextpkts(pkt_tbl[k], ring, head);
+    head = (head + BATCH) % RING_SLOTS;
+    pkts += BATCH;
+    if (!pipe) {
+      if ((rc = pptk_rx_batch(ctx, pkt_tbl[0], BATCH, recs[0])) != 0) {
+        fprintf(stderr, "pptk_rx_batch: %d\n", rc);
+        return 1;
+      }
+      tally(recs[0], BATCH);
+      /* ldp_in_deallocate_some(inq, pkt_tbl, num); */
+      continue;
     }
-    if ((rc = pptk_rx_batch(ctx, pkt_tbl, BATCH, recs)) != 0) {
-      fprintf(stderr, "pptk_rx_batch: %d\n", rc);
+    /* pipelined: batch b goes to the GPU, then batch b-1 comes back */
+    if ((rc = pptk_rx_batch_submit(ctx, pkt_tbl[k], BATCH, recs[k])) != 0) {
+      fprintf(stderr, "pptk_rx_batch_submit: %d\n", rc);
       return 1;
     }
-    for (i = 0; i < BATCH; i++) {
-      if ((recs[i].flags & (PPTK_RX_F_IP_OK | PPTK_RX_F_L4_OK)) ==
-          (PPTK_RX_F_IP_OK | PPTK_RX_F_L4_OK))
-        ok++;
-      else
-        bad++;
+    if (pptk_rx_batch_pending(ctx) == PPTK_RX_MAX_INFLIGHT) {
+      if ((rc = pptk_rx_batch_complete(ctx)) != BATCH) {
+        fprintf(stderr, "pptk_rx_batch_complete: %d\n", rc);
+        return 1;
+      }
+      tally(recs[k ^ 1], BATCH);
+      /* ldp_in_deallocate_some(inq, pkt_tbl[k ^ 1], num); */
     }
-    pkts += BATCH;
-    /* ldp_in_deallocate_some(inq, pkt_tbl, num); */
-    head = (head + BATCH) % RING_SLOTS;
+  }
+  for (; pptk_rx_batch_pending(ctx) > 0; b++) {     /* drain: the last batch */
+    if ((rc = pptk_rx_batch_complete(ctx)) != BATCH) {
+      fprintf(stderr, "pptk_rx_batch_complete: %d\n", rc);
+      return 1;
+    }
+    tally(recs[(b - 1) & 1], BATCH);
   }
   printf("%lu frames, %.3f MPPS, %lu verified, %lu failed\n", pkts, pkts / (now() - t0) / 1e6,
          ok, bad);

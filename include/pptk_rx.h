@@ -149,6 +149,35 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *ctx);
 int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
                   int num, struct pptk_rx_rec *recs);
 
+/* pptk_rx_batch split in two, so that an rx loop overlaps one batch's GPU
+ * round trip with fetching and submitting the next (the synchronous call
+ * leaves the host idle for the whole launch-to-completion latency, which
+ * dominates LDP-sized batches; DESIGN.md "Pipelined host batches"):
+ *
+ *   ldp_in_nextpkts(q, pkts[k], ...);  pptk_rx_batch_submit(ctx, pkts[k], n, recs[k]);
+ *   if (pptk_rx_batch_pending(ctx) == PPTK_RX_MAX_INFLIGHT) {
+ *     pptk_rx_batch_complete(ctx);      -- batch k-1: recs final, frames free
+ *     ... use recs[k-1] ...;  ldp_in_deallocate_some(q, pkts[k-1], ...);
+ *   }
+ *
+ * submit gathers and enqueues one batch of 1..opts.max_batch frames (one
+ * chunk) and returns without waiting; the frames and recs[0, num) must stay
+ * valid and untouched until the batch is completed.  complete waits for the
+ * OLDEST outstanding submission (FIFO) and returns its frame count (> 0):
+ * after it its records are final and none of its pointers is retained.
+ * Results are those of pptk_rx_batch.  At most PPTK_RX_MAX_INFLIGHT
+ * submissions are outstanding per context (submit returns -EBUSY beyond);
+ * pptk_rx_batch returns -EBUSY while any is; num == 0 submits nothing and
+ * returns 0; num > opts.max_batch is -EINVAL (use pptk_rx_batch);
+ * complete with nothing outstanding returns -ENOENT.  A failed submit
+ * leaves nothing outstanding.  pptk_rx_ctx_destroy waits for (and drops)
+ * outstanding submissions. */
+#define PPTK_RX_MAX_INFLIGHT 2
+int pptk_rx_batch_submit(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts, int num,
+                         struct pptk_rx_rec *recs);
+int pptk_rx_batch_complete(struct pptk_rx_ctx *ctx);
+int pptk_rx_batch_pending(const struct pptk_rx_ctx *ctx);
+
 /* Zero-copy rx rings: register a host region (e.g. a netmap ring's buffer
  * area or a socket ring) once; pptk_rx_batch() calls whose frames all lie in
  * one registered ring skip the host gather into staging: a chunk whose

@@ -166,7 +166,9 @@ struct pptk_rx_ctx {
   // pptk_rx_autotune's choice per automatic variant, for fixed-stride [0]
   // and offset-described [1] batches (-1: the automatic variant itself)
   int tuned[2][RX_NVARIANTS];
-  RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch)
+  RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch, pptk_rx_batch_submit)
+  int async_head = 0;  // slot of the oldest outstanding submission
+  int async_n = 0;     // outstanding submissions (0..PPTK_RX_MAX_INFLIGHT)
   std::vector<RxRing> rings;
   WorkerPool *pool = nullptr;   // started by the first host batch
   void *comm = nullptr;         // RCCL communicator (rx_comm.hip), or null
@@ -1029,171 +1031,197 @@ int pptk_rx_unregister_ring(struct pptk_rx_ctx *c, void *base) {
   return -EINVAL;
 }
 
+// A chunk that failed part-way: nothing it queued may still run (it may
+// read the caller's frames or write the slot) when the error is returned.
+static int chunk_failed(RxSlot &sl, int rc) {
+  (void)hipStreamSynchronize(sl.stream);
+  sl.busy = false;
+  return rc;
+}
+
+// One chunk of a host batch (cnt <= opts.max_batch frames) into slot `sl`,
+// idle and sized by ensure_slot: its descriptors and frames, then its
+// copies, the launch and the record copy-back queued on the slot's stream,
+// nothing waited for.  retire() waits for it and hands the records to `out`.
+// In a registered ring the kernel reads the frames in place over PCIe (or
+// the span goes down by DMA) and only the 10-byte descriptors are written.
+static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp, size_t cnt,
+                         pptk_rx_rec *out, const RxRing *ring, const RxRing *rreg,
+                         WorkerPool *pool) {
+  const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
+  // Descriptors, then the frame bytes.  On one thread (no pool, or a
+  // small chunk) both in one pass.  With the pool, both in parallel over
+  // parts of the chunk: a first pass writes the lengths (and a ring's
+  // offsets) and sums each part's staging bytes, a serial prefix over the
+  // parts gives each part its staging base, and a second pass writes the
+  // staging offsets while it gathers the frames (a serial descriptor pass
+  // had cost a 65 536-frame C64 chunk as much as the whole parallel
+  // gather, DESIGN.md "End-to-end").
+  const bool nt = nt_gather();
+  auto stage = [&sl, cp, nt](size_t i) {
+    if (nt) stage_frame(sl.h_frames + sl.h_off[i], (const uint8_t *)cp[i].data, sl.h_len[i]);
+    else memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
+  };
+  // one part: lengths (+ ring offsets / span) and, for staged chunks, the
+  // staging bytes it needs; with `base` given, also the staging offsets
+  // and the gather
+  auto describe = [&sl, cp, ring, maxf, nt, &stage](size_t i0, size_t i1, size_t base,
+                                                    bool gather, PartDesc &d) {
+    size_t pos = base;
+    for (size_t i = i0; i < i1; ++i) {
+      const struct ldp_packet &pk = cp[i];
+      const bool ok = pk.data && pk.sz <= maxf;
+      const uint32_t sz = ok ? pk.sz : 0u;
+      sl.h_len[i] = (uint16_t)sz;
+      if (ring) {
+        const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
+        sl.h_off[i] = o;
+        d.lo = std::min<size_t>(d.lo, o);
+        d.hi = std::max<size_t>(d.hi, o + ((sz + 15) & ~(size_t)15));
+        d.fbytes += sz;
+      } else if (gather) {
+        sl.h_off[i] = pos;
+        if (sz) stage(i);
+      }
+      pos += (sz + 15) & ~(size_t)15;
+      d.maxlen = std::max(d.maxlen, sz);
+    }
+    d.bytes = pos - base;
+    // this thread's streaming stores, before the copy is queued
+    if (gather && nt) _mm_sfence();
+  };
+  // The pool only for big chunks: waking it costs ~20-40 µs, more than a
+  // 256-frame or even a 1.5 MB gather saves (DESIGN.md "End-to-end").
+  // Staged chunks: parts of ~1024 frames or ~256 KB of frame bytes
+  // (estimated from the first frame), at most 8 per thread, in ONE pass
+  // over the pool -- each
+  // part sums its staging bytes, takes its base from the previous part's
+  // published running total (parts are claimed in order, so that one is
+  // done or in progress), publishes its own, then writes its offsets and
+  // gathers.  Ring chunks (no gather): parts of ~2048 frames.
+  const size_t est = cnt * (size_t)std::min<uint32_t>(cp[0].sz, maxf);
+  const bool staged = !ring;
+  size_t nparts = 1;
+  if (pool && staged && (cnt >= 8192 || est >= (4u << 20)))
+    nparts = std::max(cnt / 1024, est >> 18);
+  else if (pool && !staged && cnt >= 16384)
+    nparts = cnt / 2048;
+  nparts = std::max<size_t>(1, std::min<size_t>(nparts, std::min<size_t>(8 * pool_size(pool), cnt)));
+  std::vector<PartDesc> &parts = sl.parts;
+  parts.assign(nparts, PartDesc{});
+  if (nparts == 1) {
+    describe(0, cnt, 0, staged, parts[0]);
+  } else if (!staged) {
+    pool->parallel_for(nparts, [&](size_t t) {
+      describe(cnt * t / nparts, cnt * (t + 1) / nparts, 0, false, parts[t]);
+    });
+  } else {
+    if (sl.run_cap < nparts) {
+      sl.run.reset(new std::atomic<size_t>[nparts]);
+      sl.run_cap = nparts;
+    }
+    std::atomic<size_t> *run = sl.run.get();
+    for (size_t t = 0; t < nparts; ++t) run[t].store(SIZE_MAX, std::memory_order_relaxed);
+    pool->parallel_for(nparts, [&](size_t t) {
+      const size_t i0 = cnt * t / nparts, i1 = cnt * (t + 1) / nparts;
+      PartDesc &d = parts[t];
+      describe(i0, i1, 0, false, d);            // lengths, this part's bytes
+      size_t base = 0;
+      if (t > 0)
+        while ((base = run[t - 1].load(std::memory_order_acquire)) == SIZE_MAX) _mm_pause();
+      run[t].store(base + d.bytes, std::memory_order_release);
+      PartDesc d2{};
+      describe(i0, i1, base, true, d2);         // offsets + gather
+    });
+  }
+  size_t pos = 0, lo = SIZE_MAX, hi = 0, fbytes = 0;
+  uint32_t maxlen = 0;
+  for (const PartDesc &d : parts) {
+    pos += d.bytes;
+    lo = std::min(lo, d.lo);
+    hi = std::max(hi, d.hi);
+    fbytes += d.fbytes;
+    maxlen = std::max(maxlen, d.maxlen);
+  }
+  // a dense ring chunk goes down as one span; the kernel sees the span's
+  // buffer shifted down by `lo`, so the ring offsets stay as they are
+  const bool ring_dma = ring && hi > lo && hi - lo > direct_max_bytes() &&
+                        (double)fbytes >= ring_dma_density() * (double)(hi - lo) &&
+                        fit_span(sl, hi - lo + 16);
+  hipStream_t s = sl.stream;
+  const bool direct =
+      ring ? direct_max_bytes() > 0 && !ring_dma : pos <= direct_max_bytes();
+  // descriptors and records over PCIe, frames by DMA
+  const bool split = !direct && (ring_dma || !ring) && split_chunks();
+  const bool pcie = direct || split;
+  if ((!direct && !ring &&
+       hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
+                      hipMemcpyHostToDevice, s) != hipSuccess) ||
+      (ring_dma && hipMemcpyAsync(sl.d_frames, ring->host + lo, hi - lo,
+                                  hipMemcpyHostToDevice, s) != hipSuccess) ||
+      (!pcie &&
+       (hipMemcpyAsync(sl.d_off, sl.h_off, cnt * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(sl.d_len, sl.h_len, cnt * 2, hipMemcpyHostToDevice, s) != hipSuccess)))
+    return chunk_failed(sl, -EIO);
+  pptk_rx_dev_batch b;
+  memset(&b, 0, sizeof(b));
+  b.d_frames = ring && !ring_dma ? ring->dev
+               : ring_dma           ? (const uint8_t *)((uintptr_t)sl.d_frames - lo)
+               : direct             ? sl.hd_frames
+                                    : sl.d_frames;
+  b.d_off = pcie ? sl.hd_off : sl.d_off;
+  b.d_len = pcie ? sl.hd_len : sl.d_len;
+  b.max_len = maxlen;
+  b.n = cnt;
+  // records: into the caller's array itself when it is registered
+  b.d_recs = rreg ? (pptk_rx_rec *)(rreg->dev + ((const uint8_t *)out - rreg->host))
+             : pcie ? sl.hd_recs
+                    : sl.d_recs;
+  const int rc = pptk_rx_batch_device(c, &b, s);
+  if (rc != 0) return chunk_failed(sl, rc);
+  if ((!pcie && !rreg &&
+       hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
+           hipSuccess) ||
+      hipEventRecord(sl.done, s) != hipSuccess)
+    return chunk_failed(sl, -EIO);
+  sl.out = rreg ? nullptr : out;   // (retire copies only staged records)
+  sl.count = cnt;
+  sl.busy = true;
+  return 0;
+}
+
+// Staging bytes a slot needs for one chunk of this context's batches.
+static size_t chunk_bytes(const pptk_rx_ctx *c) {
+  const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
+  return std::max<size_t>(c->opts.max_batch, 1) * ((maxf + 15) & ~15u);
+}
+
+static bool host_args_ok(const pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
+                         const struct pptk_rx_rec *recs) {
+  return c && num >= 0 && (num == 0 || (pkts && recs));
+}
+
 int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
                   struct pptk_rx_rec *recs) {
-  if (!c || num < 0 || (num > 0 && (!pkts || !recs))) return -EINVAL;
+  if (!host_args_ok(c, pkts, num, recs)) return -EINVAL;
   if (num == 0) return 0;
+  if (c->async_n) return -EBUSY;   // the submissions own the slots
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
-  const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
   const RxRing *ring = ring_of(c, pkts, num);
   const RxRing *rreg = records_region(c, recs, (size_t)num * sizeof(pptk_rx_rec));
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
-  const size_t chunk_bytes = chunk * ((maxf + 15) & ~15u);
   WorkerPool *pool = pool_of(c);
   int rc = 0;
   // Double-buffered: while chunk k runs on one slot's stream (H2D, kernel,
-  // D2H), the host gathers chunk k+1 into the other slot.  In a registered
-  // ring the kernel reads the frames in place over PCIe and only the 10-byte
-  // descriptors go down.
+  // D2H), the host gathers chunk k+1 into the other slot.
   size_t k = 0, cnt = 0;
   for (size_t first = 0; first < (size_t)num && rc == 0; first += cnt, ++k) {
     RxSlot &sl = c->slot[k & 1];
     if ((rc = retire(sl, pool)) != 0) break;
     cnt = std::min(chunk, (size_t)num - first);
-    if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes)) != 0) break;
-    // Descriptors, then the frame bytes.  On one thread (no pool, or a
-    // small chunk) both in one pass.  With the pool, both in parallel over
-    // parts of the chunk: a first pass writes the lengths (and a ring's
-    // offsets) and sums each part's staging bytes, a serial prefix over the
-    // parts gives each part its staging base, and a second pass writes the
-    // staging offsets while it gathers the frames (a serial descriptor pass
-    // had cost a 65 536-frame C64 chunk as much as the whole parallel
-    // gather, DESIGN.md "End-to-end").
-    const struct ldp_packet *cp = pkts + first;
-    const bool nt = nt_gather();
-    auto stage = [&sl, cp, nt](size_t i) {
-      if (nt) stage_frame(sl.h_frames + sl.h_off[i], (const uint8_t *)cp[i].data, sl.h_len[i]);
-      else memcpy(sl.h_frames + sl.h_off[i], cp[i].data, sl.h_len[i]);
-    };
-    // one part: lengths (+ ring offsets / span) and, for staged chunks, the
-    // staging bytes it needs; with `base` given, also the staging offsets
-    // and the gather
-    auto describe = [&sl, cp, ring, maxf, nt, &stage](size_t i0, size_t i1, size_t base,
-                                                      bool gather, PartDesc &d) {
-      size_t pos = base;
-      for (size_t i = i0; i < i1; ++i) {
-        const struct ldp_packet &pk = cp[i];
-        const bool ok = pk.data && pk.sz <= maxf;
-        const uint32_t sz = ok ? pk.sz : 0u;
-        sl.h_len[i] = (uint16_t)sz;
-        if (ring) {
-          const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
-          sl.h_off[i] = o;
-          d.lo = std::min<size_t>(d.lo, o);
-          d.hi = std::max<size_t>(d.hi, o + ((sz + 15) & ~(size_t)15));
-          d.fbytes += sz;
-        } else if (gather) {
-          sl.h_off[i] = pos;
-          if (sz) stage(i);
-        }
-        pos += (sz + 15) & ~(size_t)15;
-        d.maxlen = std::max(d.maxlen, sz);
-      }
-      d.bytes = pos - base;
-      // this thread's streaming stores, before the copy is queued
-      if (gather && nt) _mm_sfence();
-    };
-    // The pool only for big chunks: waking it costs ~20-40 µs, more than a
-    // 256-frame or even a 1.5 MB gather saves (DESIGN.md "End-to-end").
-    // Staged chunks: parts of ~1024 frames or ~256 KB of frame bytes
-    // (estimated from the first frame), at most 8 per thread, in ONE pass
-    // over the pool -- each
-    // part sums its staging bytes, takes its base from the previous part's
-    // published running total (parts are claimed in order, so that one is
-    // done or in progress), publishes its own, then writes its offsets and
-    // gathers.  Ring chunks (no gather): parts of ~2048 frames.
-    const size_t est = cnt * (size_t)std::min<uint32_t>(cp[0].sz, maxf);
-    const bool staged = !ring;
-    size_t nparts = 1;
-    if (pool && staged && (cnt >= 8192 || est >= (4u << 20)))
-      nparts = std::max(cnt / 1024, est >> 18);
-    else if (pool && !staged && cnt >= 16384)
-      nparts = cnt / 2048;
-    nparts = std::max<size_t>(1, std::min<size_t>(nparts, std::min<size_t>(8 * pool_size(pool), cnt)));
-    std::vector<PartDesc> &parts = sl.parts;
-    parts.assign(nparts, PartDesc{});
-    if (nparts == 1) {
-      describe(0, cnt, 0, staged, parts[0]);
-    } else if (!staged) {
-      pool->parallel_for(nparts, [&](size_t t) {
-        describe(cnt * t / nparts, cnt * (t + 1) / nparts, 0, false, parts[t]);
-      });
-    } else {
-      if (sl.run_cap < nparts) {
-        sl.run.reset(new std::atomic<size_t>[nparts]);
-        sl.run_cap = nparts;
-      }
-      std::atomic<size_t> *run = sl.run.get();
-      for (size_t t = 0; t < nparts; ++t) run[t].store(SIZE_MAX, std::memory_order_relaxed);
-      pool->parallel_for(nparts, [&](size_t t) {
-        const size_t i0 = cnt * t / nparts, i1 = cnt * (t + 1) / nparts;
-        PartDesc &d = parts[t];
-        describe(i0, i1, 0, false, d);            // lengths, this part's bytes
-        size_t base = 0;
-        if (t > 0)
-          while ((base = run[t - 1].load(std::memory_order_acquire)) == SIZE_MAX) _mm_pause();
-        run[t].store(base + d.bytes, std::memory_order_release);
-        PartDesc d2{};
-        describe(i0, i1, base, true, d2);         // offsets + gather
-      });
-    }
-    size_t pos = 0, lo = SIZE_MAX, hi = 0, fbytes = 0;
-    uint32_t maxlen = 0;
-    for (const PartDesc &d : parts) {
-      pos += d.bytes;
-      lo = std::min(lo, d.lo);
-      hi = std::max(hi, d.hi);
-      fbytes += d.fbytes;
-      maxlen = std::max(maxlen, d.maxlen);
-    }
-    // a dense ring chunk goes down as one span; the kernel sees the span's
-    // buffer shifted down by `lo`, so the ring offsets stay as they are
-    const bool ring_dma = ring && hi > lo && hi - lo > direct_max_bytes() &&
-                          (double)fbytes >= ring_dma_density() * (double)(hi - lo) &&
-                          fit_span(sl, hi - lo + 16);
-    hipStream_t s = sl.stream;
-    const bool direct =
-        ring ? direct_max_bytes() > 0 && !ring_dma : pos <= direct_max_bytes();
-    // descriptors and records over PCIe, frames by DMA
-    const bool split = !direct && (ring_dma || !ring) && split_chunks();
-    const bool pcie = direct || split;
-    if ((!direct && !ring &&
-         hipMemcpyAsync(sl.d_frames, sl.h_frames, std::max<size_t>(pos, 16),
-                        hipMemcpyHostToDevice, s) != hipSuccess) ||
-        (ring_dma && hipMemcpyAsync(sl.d_frames, ring->host + lo, hi - lo,
-                                    hipMemcpyHostToDevice, s) != hipSuccess) ||
-        (!pcie &&
-         (hipMemcpyAsync(sl.d_off, sl.h_off, cnt * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-          hipMemcpyAsync(sl.d_len, sl.h_len, cnt * 2, hipMemcpyHostToDevice, s) != hipSuccess))) {
-      rc = -EIO;
-      break;
-    }
-    pptk_rx_dev_batch b;
-    memset(&b, 0, sizeof(b));
-    b.d_frames = ring && !ring_dma ? ring->dev
-                 : ring_dma           ? (const uint8_t *)((uintptr_t)sl.d_frames - lo)
-                 : direct             ? sl.hd_frames
-                                      : sl.d_frames;
-    b.d_off = pcie ? sl.hd_off : sl.d_off;
-    b.d_len = pcie ? sl.hd_len : sl.d_len;
-    b.max_len = maxlen;
-    b.n = cnt;
-    // records: into the caller's array itself when it is registered
-    b.d_recs = rreg ? (pptk_rx_rec *)(rreg->dev + ((const uint8_t *)(recs + first) - rreg->host))
-               : pcie ? sl.hd_recs
-                      : sl.d_recs;
-    if ((rc = pptk_rx_batch_device(c, &b, s)) != 0) break;
-    if ((!pcie && !rreg &&
-         hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
-             hipSuccess) ||
-        hipEventRecord(sl.done, s) != hipSuccess) {
-      rc = -EIO;
-      break;
-    }
-    sl.out = rreg ? nullptr : recs + first;   // (retire copies only staged records)
-    sl.count = cnt;
-    sl.busy = true;
+    if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes(c))) != 0) break;
+    rc = enqueue_chunk(c, sl, pkts + first, cnt, recs + first, ring, rreg, pool);
   }
   // drain (also on error: nothing may still read the caller's buffers)
   for (RxSlot &sl : c->slot) {
@@ -1202,5 +1230,41 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   }
   return rc;
 }
+
+int pptk_rx_batch_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
+                         struct pptk_rx_rec *recs) {
+  if (!host_args_ok(c, pkts, num, recs)) return -EINVAL;
+  if (num == 0) return 0;
+  if ((size_t)num > std::max<size_t>(c->opts.max_batch, 1)) return -EINVAL;
+  if (c->async_n >= PPTK_RX_MAX_INFLIGHT) return -EBUSY;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
+  const RxRing *ring = ring_of(c, pkts, num);
+  const RxRing *rreg = records_region(c, recs, (size_t)num * sizeof(pptk_rx_rec));
+  // the slots alternate in submission order (FIFO), so consecutive
+  // submissions run on different streams and may overlap on the GPU
+  RxSlot &sl = c->slot[(c->async_head + c->async_n) & 1];
+  int rc = ensure_slot(c, sl, std::max<size_t>(c->opts.max_batch, 1), ring ? 64 : chunk_bytes(c));
+  if (rc == 0) rc = enqueue_chunk(c, sl, pkts, (size_t)num, recs, ring, rreg, pool_of(c));
+  if (rc != 0) return rc;
+  ++c->async_n;
+  return 0;
+}
+
+int pptk_rx_batch_complete(struct pptk_rx_ctx *c) {
+  if (!c) return -EINVAL;
+  if (c->async_n == 0) return -ENOENT;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
+  RxSlot &sl = c->slot[c->async_head];
+  const int cnt = (int)sl.count;
+  const int rc = retire(sl, c->pool);
+  // (dropped from the queue even on an error: its slot is idle again)
+  c->async_head ^= 1;
+  --c->async_n;
+  return rc ? rc : cnt;
+}
+
+int pptk_rx_batch_pending(const struct pptk_rx_ctx *c) { return c ? c->async_n : -EINVAL; }
 
 }  // extern "C"

@@ -41,7 +41,8 @@ assert ctypes.sizeof(LdpPacket) == 24
 assert ctypes.sizeof(RxOpts) == 36
 
 EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
-           "pptk_rx_batch", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
+           "pptk_rx_batch", "pptk_rx_batch_submit", "pptk_rx_batch_complete",
+           "pptk_rx_batch_pending", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
@@ -160,6 +161,13 @@ def lib(path=None):
         if hasattr(L, "pptk_rx_last_variant"):   # (absent from older A/B builds)
             L.pptk_rx_last_variant.argtypes = [vp]
             L.pptk_rx_last_variant.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_batch_submit"):   # (absent from older A/B builds)
+            L.pptk_rx_batch_submit.argtypes = [vp, vp, ctypes.c_int, vp]
+            L.pptk_rx_batch_submit.restype = ctypes.c_int
+            L.pptk_rx_batch_complete.argtypes = [vp]
+            L.pptk_rx_batch_complete.restype = ctypes.c_int
+            L.pptk_rx_batch_pending.argtypes = [vp]
+            L.pptk_rx_batch_pending.restype = ctypes.c_int
         L.pptk_rx_register_ring.argtypes = [vp, vp, ctypes.c_size_t]
         L.pptk_rx_register_ring.restype = ctypes.c_int
         L.pptk_rx_unregister_ring.argtypes = [vp, vp]
@@ -488,6 +496,30 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch failed ({rc})")
         return recs
+
+    def submit_host(self, pkts, out):
+        """pptk_rx_batch_submit: enqueue one batch (len(pkts) <= max_batch);
+        `pkts`, the frames they point at and `out` (a REC_DTYPE array of
+        len(pkts)) must stay alive and untouched until complete_host() has
+        returned this batch.  Raises OSError(EBUSY) with
+        PPTK_RX_MAX_INFLIGHT batches outstanding."""
+        n = len(pkts)
+        assert out.dtype == REC_DTYPE and out.shape == (n,) and out.flags["C_CONTIGUOUS"]
+        rc = self._L.pptk_rx_batch_submit(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n,
+                                          ctypes.c_void_p(out.ctypes.data))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_batch_submit failed ({rc})")
+
+    def complete_host(self):
+        """pptk_rx_batch_complete: wait for the oldest outstanding batch;
+        returns its frame count."""
+        rc = self._L.pptk_rx_batch_complete(self._ctx)
+        if rc < 0:
+            raise OSError(-rc, f"pptk_rx_batch_complete failed ({rc})")
+        return rc
+
+    def pending_host(self):
+        return self._L.pptk_rx_batch_pending(self._ctx)
 
 
 def comm_uid(lib_path=None):

@@ -169,9 +169,11 @@ def test_example_rx_loop_builds(tmp_path):
 
 
 @pytest.mark.gpu
-def test_example_rx_loop_runs(tmp_path):
-    """The LDP-style rx loop verifies every frame but the one it corrupted."""
-    out = subprocess.run([_build_rx_loop(tmp_path), "20"], capture_output=True, text=True,
+@pytest.mark.parametrize("mode", [[], ["pipe"]])
+def test_example_rx_loop_runs(tmp_path, mode):
+    """The LDP-style rx loop verifies every frame but the one it corrupted,
+    synchronous and pipelined (pptk_rx_batch_submit / _complete)."""
+    out = subprocess.run([_build_rx_loop(tmp_path), "20"] + mode, capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "20000 frames" in out.stdout and "19995 verified, 5 failed" in out.stdout
@@ -499,6 +501,9 @@ def test_entry_points_reject_bad_arguments(lib):
     bad.iphash_bits4, bad.iphash_size = 24, 1000          # not a power of two
     assert lib.pptk_rx_ctx_create(ctypes.byref(out), ctypes.byref(bad)) == EINVAL
     assert lib.pptk_rx_batch(None, None, 1, None) == EINVAL
+    assert lib.pptk_rx_batch_submit(None, None, 1, None) == EINVAL
+    assert lib.pptk_rx_batch_complete(None) == EINVAL
+    assert lib.pptk_rx_batch_pending(None) == EINVAL
     b = RxDevBatch()
     assert lib.pptk_rx_batch_device(None, ctypes.byref(b), None) == EINVAL
     assert lib.pptk_rx_batch_device_mixed(None, ctypes.byref(b), None, None, None) == EINVAL

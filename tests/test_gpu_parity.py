@@ -388,6 +388,88 @@ def test_host_batch_registered_records(name, max_batch, threads, dev):
     assert not d, "after unregister: " + d
 
 
+def _packet_slice(pkts, lo, hi):
+    """pkts[lo:hi] as a ctypes LdpPacket array aliasing `pkts` (no copy)."""
+    import ctypes
+    from pptk_amd.rx import LdpPacket
+    s = (LdpPacket * (hi - lo)).from_address(ctypes.addressof(pkts) + lo * ctypes.sizeof(LdpPacket))
+    s._keep = pkts
+    return s
+
+
+@pytest.mark.parametrize("mode", ["staged", "ring", "ring_recs"])
+@pytest.mark.parametrize("name", ["fuzz", "cmix", "c64", "c1500"])
+def test_host_batch_pipelined(name, mode, dev):
+    """pptk_rx_batch_submit / _complete as an LDP rx loop uses them: ragged
+    batches of 1 .. max_batch frames submitted two deep (staged frames, frames
+    in a registered ring, and records into a registered array too), every
+    record against the golden set; and the queue contract: FIFO frame counts,
+    -EBUSY for a third submission and for pptk_rx_batch while any is
+    outstanding, -EINVAL above max_batch, -ENOENT on an empty queue, and a
+    context destroyed with submissions outstanding."""
+    import errno
+    from pptk_amd.records import REC_DTYPE
+    from pptk_amd.rx import RxContext, ldp_packets
+    z = load_golden(name)
+    n = len(z["off"])
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    max_batch = 1024
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_batch=max_batch, max_frame=65535,
+                    gather_threads=4)
+    ring = _pages(z["buf"].size + 4096)
+    ring[:z["buf"].size] = z["buf"]
+    pkts = ldp_packets(ring, z["off"], z["len"])
+    region = _pages(n * 64)
+    out = region[:n * 64].view(REC_DTYPE)
+    if mode != "staged":
+        ctx.register_ring(ring)
+    if mode == "ring_recs":
+        ctx.register_ring(region)
+    rng = np.random.default_rng(7)
+    sizes, pos = [], 0
+    while pos < n:
+        k = int(min(n - pos, rng.choice([1, 3, 64, 500, max_batch, int(rng.integers(1, max_batch))])))
+        sizes.append((pos, k))
+        pos += k
+    for lap in range(2):
+        out[:] = np.zeros(1, dtype=REC_DTYPE)
+        queue = []
+        for i, (lo, k) in enumerate(sizes):
+            ctx.submit_host(_packet_slice(pkts, lo, lo + k), out[lo:lo + k])
+            queue.append(k)
+            if ctx.pending_host() == 2:
+                if lap == 0 and i == 1:
+                    with pytest.raises(OSError) as e:
+                        ctx.submit_host(_packet_slice(pkts, 0, 1), out[:1])
+                    assert e.value.errno == errno.EBUSY
+                    with pytest.raises(OSError) as e:
+                        ctx.batch_host(_packet_slice(pkts, 0, 1), out=np.zeros(1, REC_DTYPE))
+                    assert e.value.errno == errno.EBUSY
+                assert ctx.complete_host() == queue.pop(0)
+        while queue:
+            assert ctx.complete_host() == queue.pop(0)
+        assert ctx.pending_host() == 0
+        d = diff_records(out.copy(), z["recs"])
+        assert not d, f"{mode} lap {lap}: " + d
+    with pytest.raises(OSError) as e:
+        ctx.complete_host()
+    assert e.value.errno == errno.ENOENT
+    if n > max_batch:
+        with pytest.raises(OSError) as e:
+            ctx.submit_host(_packet_slice(pkts, 0, max_batch + 1), out[:max_batch + 1])
+        assert e.value.errno == errno.EINVAL
+    # the synchronous call works again on the same slots
+    d = diff_records(ctx.batch_host(pkts), z["recs"])
+    assert not d, f"{mode} sync after async: " + d
+    # destroyed with two submissions outstanding: waits for them, no fault
+    k = min(n, max_batch)
+    spare = np.zeros(k, REC_DTYPE)
+    ctx.submit_host(_packet_slice(pkts, 0, k), out[:k])
+    ctx.submit_host(_packet_slice(pkts, 0, k), spare)
+    assert ctx.pending_host() == 2
+    ctx.close()
+
+
 def test_ring_edge_falls_back(dev):
     """A frame whose 16-byte-rounded end leaves the registered region makes
     the batch use staging; results stay exact."""
