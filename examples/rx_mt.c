@@ -9,10 +9,12 @@
  * pinned staging; contexts spread over the visible GPUs), and the
  * per-packet work is one pptk_rx_batch() per burst of up to BURST frames.
  * Every record is compared with the expected one from the set file, on
- * every lap.
+ * every lap.  With "pipe", each thread keeps two bursts in flight
+ * (pptk_rx_batch_submit, then pptk_rx_batch_complete of the previous burst
+ * before its deallocate_some).
  *
  *   gcc -O2 -pthread -Iinclude examples/rx_mt.c -Lpptk_amd -lpptkrx -o rx_mt
- *   ./rx_mt frames.rxq [threads [laps]]
+ *   ./rx_mt frames.rxq [threads [laps [pipe]]]
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -26,7 +28,7 @@
 #define BURST 1000 /* ldp/ldprecvmt.c:23: struct ldp_packet pkt_tbl[1000] */
 
 struct rxq_thread {
-  int id, device, laps;
+  int id, device, laps, pipe;
   const struct rxq_set *set;
   uint32_t first, count;   /* this thread's queue */
   unsigned long pkts, mismatches;
@@ -40,12 +42,24 @@ static double now(void)
   return tv.tv_sec + tv.tv_usec * 1e-6;
 }
 
+/* records of the burst starting at queue position `head` against the set */
+static void check(struct rxq_thread *t, const struct pptk_rx_rec *recs, uint32_t head, int num)
+{
+  for (int i = 0; i < num; i++)
+    if (memcmp(&recs[i], &t->set->want[t->first + head + (uint32_t)i], sizeof(recs[i])) != 0)
+      t->mismatches++;
+  t->pkts += (unsigned long)num;
+}
+
 static void *thrfn(void *arg)
 {
   struct rxq_thread *t = arg;
   const struct rxq_set *s = t->set;
-  static __thread struct ldp_packet pkt_tbl[BURST];
-  static __thread struct pptk_rx_rec recs[BURST];
+  /* two bursts: one in hand while the other is with the GPU (pipe) */
+  static __thread struct ldp_packet pkt_tbl[2][BURST];
+  static __thread struct pptk_rx_rec recs[2][BURST];
+  uint32_t burst_head[2] = {0, 0};
+  int burst_num[2] = {0, 0};
   struct pptk_rx_opts o;
   struct pptk_rx_ctx *ctx;
   pptk_rx_opts_default(&o);
@@ -54,10 +68,11 @@ static void *thrfn(void *arg)
   o.iphash_bits4 = 24;           /* the golden sets' ip_hash parameters */
   o.iphash_bits6 = 48;
   o.iphash_size = 4096;
-  o.max_batch = 256;
+  o.max_batch = t->pipe ? BURST : 256;   /* a submission is one chunk */
   o.max_frame = 65535;
   if ((t->rc = pptk_rx_ctx_create(&ctx, &o)) != 0)
     return NULL;
+  int b = 0;   /* which of the two bursts is in hand */
   for (int lap = 0; lap < t->laps && t->rc == 0; lap++) {
     uint32_t head = 0;
     while (head < t->count) {
@@ -65,19 +80,42 @@ static void *thrfn(void *arg)
       int num = t->count - head < BURST ? (int)(t->count - head) : BURST;
       for (int i = 0; i < num; i++) {
         uint32_t k = t->first + head + (uint32_t)i;
-        pkt_tbl[i].data = s->buf + s->off[k];
-        pkt_tbl[i].sz = s->len[k];
-        pkt_tbl[i].ancillary = k;
+        pkt_tbl[b][i].data = s->buf + s->off[k];
+        pkt_tbl[b][i].sz = s->len[k];
+        pkt_tbl[b][i].ancillary = k;
       }
-      if ((t->rc = pptk_rx_batch(ctx, pkt_tbl, num, recs)) != 0)
-        break;
-      for (int i = 0; i < num; i++)
-        if (memcmp(&recs[i], &s->want[t->first + head + (uint32_t)i], sizeof(recs[i])) != 0)
-          t->mismatches++;
-      t->pkts += (unsigned long)num;
-      /* ldp_in_deallocate_some(intf->inq[id], pkt_tbl, num); */
+      if (!t->pipe) {
+        if ((t->rc = pptk_rx_batch(ctx, pkt_tbl[b], num, recs[b])) != 0)
+          break;
+        check(t, recs[b], head, num);
+        /* ldp_in_deallocate_some(intf->inq[id], pkt_tbl, num); */
+      } else {
+        if ((t->rc = pptk_rx_batch_submit(ctx, pkt_tbl[b], num, recs[b])) != 0)
+          break;
+        burst_head[b] = head;
+        burst_num[b] = num;
+        if (pptk_rx_batch_pending(ctx) == PPTK_RX_MAX_INFLIGHT) {
+          int rc = pptk_rx_batch_complete(ctx);           /* the other burst */
+          if (rc != burst_num[b ^ 1]) {
+            t->rc = rc < 0 ? rc : -1;
+            break;
+          }
+          check(t, recs[b ^ 1], burst_head[b ^ 1], burst_num[b ^ 1]);
+          /* ldp_in_deallocate_some(intf->inq[id], pkt_tbl[b ^ 1], num); */
+        }
+        b ^= 1;
+      }
       head += (uint32_t)num;
     }
+  }
+  while (t->rc == 0 && pptk_rx_batch_pending(ctx) > 0) {   /* the last burst */
+    int rc = pptk_rx_batch_complete(ctx);
+    if (rc != burst_num[b ^ 1]) {
+      t->rc = rc < 0 ? rc : -1;
+      break;
+    }
+    check(t, recs[b ^ 1], burst_head[b ^ 1], burst_num[b ^ 1]);
+    b ^= 1;
   }
   pptk_rx_ctx_destroy(ctx);
   return NULL;
@@ -87,6 +125,7 @@ int main(int argc, char **argv)
 {
   struct rxq_set set;
   int nthr = argc > 2 ? atoi(argv[2]) : 4, laps = argc > 3 ? atoi(argv[3]) : 3;
+  int pipe = argc > 4 && strcmp(argv[4], "pipe") == 0;
   int ndev = pptk_rx_device_count();
   unsigned long pkts = 0, bad = 0;
   pthread_t pth[64];
@@ -95,7 +134,7 @@ int main(int argc, char **argv)
   int i, failed = 0;
 
   if (argc < 2 || rxq_load(argv[1], &set) != 0) {
-    fprintf(stderr, "usage: rx_mt frames.rxq [threads [laps]]\n");
+    fprintf(stderr, "usage: rx_mt frames.rxq [threads [laps [pipe]]]\n");
     return 1;
   }
   if (nthr < 1 || nthr > 64 || ndev < 1) {
@@ -104,7 +143,8 @@ int main(int argc, char **argv)
   }
   t0 = now();
   for (i = 0; i < nthr; i++) {
-    thr[i] = (struct rxq_thread){.id = i, .device = i % ndev, .laps = laps, .set = &set};
+    thr[i] = (struct rxq_thread){.id = i, .device = i % ndev, .laps = laps, .pipe = pipe,
+                                  .set = &set};
     thr[i].first = (uint32_t)((uint64_t)set.h.n * (uint64_t)i / (uint64_t)nthr);
     thr[i].count = (uint32_t)((uint64_t)set.h.n * (uint64_t)(i + 1) / (uint64_t)nthr) - thr[i].first;
     pthread_create(&pth[i], NULL, thrfn, &thr[i]);
@@ -120,8 +160,8 @@ int main(int argc, char **argv)
     pkts += thr[i].pkts;
     bad += thr[i].mismatches;
   }
-  printf("rx_mt: %d threads, %lu frames, %.3f MPPS, %lu mismatches\n", nthr, pkts,
-         pkts / (now() - t0) / 1e6, bad);
+  printf("rx_mt: %d threads%s, %lu frames, %.3f MPPS, %lu mismatches\n", nthr,
+         pipe ? " (pipelined)" : "", pkts, pkts / (now() - t0) / 1e6, bad);
   rxq_free(&set);
   return failed ? 1 : bad ? 2 : 0;
 }

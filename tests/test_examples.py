@@ -78,16 +78,19 @@ def test_rxq_file_layout(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pipe", [False, True])
 @pytest.mark.parametrize("threads", [1, 4, 8])
-def test_rx_mt_threads_bit_exact(tmp_path, threads):
-    """N rx threads, each with its own context and queue, 2 laps: every
-    record equals the golden record."""
+def test_rx_mt_threads_bit_exact(tmp_path, threads, pipe):
+    """N rx threads, each with its own context and queue, 2 laps, bursts
+    synchronous or two in flight per thread: every record equals the golden
+    record."""
     p = str(tmp_path / "s.rxq")
     n = write_rxq(p)
-    out = subprocess.run([build(tmp_path, "rx_mt"), p, str(threads), "2"], capture_output=True,
-                         text=True, timeout=300)
+    out = subprocess.run([build(tmp_path, "rx_mt"), p, str(threads), "2"] + (["pipe"] if pipe else []),
+                         capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    assert f"{threads} threads, {2 * n} frames" in out.stdout and "0 mismatches" in out.stdout
+    mode = " (pipelined)" if pipe else ""
+    assert f"{threads} threads{mode}, {2 * n} frames" in out.stdout and "0 mismatches" in out.stdout
 
 
 @pytest.mark.gpu
