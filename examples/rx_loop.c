@@ -7,10 +7,10 @@
  * ldp/ldpsend.c:141-168), each batch goes through pptk_rx_batch() between
  * "nextpkts" and "deallocate_some", and the loop reports MPPS and the
  * checksum verdicts.  The ring is registered once for zero-copy reads.
- * With "pipe", batch k+1 is fetched and submitted (pptk_rx_batch_submit)
- * before batch k is completed and released (pptk_rx_batch_complete, then
- * deallocate_some), so each batch's GPU round trip overlaps the next one's
- * host work.
+ * With "pipe", DEPTH batches are in flight: batch k is fetched and
+ * submitted (pptk_rx_batch_submit) before batch k-DEPTH+1 is completed and
+ * released (pptk_rx_batch_complete, then deallocate_some), so the batches'
+ * GPU round trips overlap the host work of the ones after them.
  *
  *   gcc -O2 -Iinclude examples/rx_loop.c -Lpptk_amd -lpptkrx -o rx_loop
  *   ./rx_loop [batches] [pipe]
@@ -29,6 +29,7 @@
 #define SLOT_BYTES 2048       /* netmap-style fixed buffers */
 #define BATCH 1000            /* ldp/ldprecv.c:14 uses 1000 */
 #define PAYLOAD 1458          /* 14 + 20 + 8 + 1458 = 1500-byte frames */
+#define DEPTH 4               /* pipelined: batches in flight (<= PPTK_RX_MAX_INFLIGHT) */
 
 static void put16(unsigned char *p, uint16_t v) { p[0] = (unsigned char)(v >> 8); p[1] = (unsigned char)v; }
 
@@ -95,10 +96,9 @@ int main(int argc, char **argv)
   int batches = argc > 1 ? atoi(argv[1]) : 2000;
   int pipe = argc > 2 && strcmp(argv[2], "pipe") == 0;
   unsigned char *ring = aligned_alloc(4096, (size_t)RING_SLOTS * SLOT_BYTES);
-  /* two packet tables and record arrays: batch k+1 is in hand while batch k
-     is still with the GPU (pipelined mode) */
-  static struct ldp_packet pkt_tbl[2][BATCH];
-  static struct pptk_rx_rec recs[2][BATCH];
+  /* a packet table and record array per batch in flight (pipelined mode) */
+  static struct ldp_packet pkt_tbl[DEPTH][BATCH];
+  static struct pptk_rx_rec recs[DEPTH][BATCH];
   struct pptk_rx_opts o;
   struct pptk_rx_ctx *ctx;
   unsigned head = 0;
@@ -128,7 +128,7 @@ int main(int argc, char **argv)
 
   t0 = now();
   for (b = 0; b < batches; b++) {
-    const int k = pipe ? b & 1 : 0;
+    const int k = pipe ? b % DEPTH : 0;
     nextpkts(pkt_tbl[k], ring, head);
     head = (head + BATCH) % RING_SLOTS;
     pkts += BATCH;
@@ -141,26 +141,26 @@ int main(int argc, char **argv)
       /* ldp_in_deallocate_some(inq, pkt_tbl, num); */
       continue;
     }
-    /* pipelined: batch b goes to the GPU, then batch b-1 comes back */
+    /* pipelined: batch b goes to the GPU, then batch b-DEPTH+1 comes back */
     if ((rc = pptk_rx_batch_submit(ctx, pkt_tbl[k], BATCH, recs[k])) != 0) {
       fprintf(stderr, "pptk_rx_batch_submit: %d\n", rc);
       return 1;
     }
-    if (pptk_rx_batch_pending(ctx) == PPTK_RX_MAX_INFLIGHT) {
+    if (pptk_rx_batch_pending(ctx) == DEPTH) {
       if ((rc = pptk_rx_batch_complete(ctx)) != BATCH) {
         fprintf(stderr, "pptk_rx_batch_complete: %d\n", rc);
         return 1;
       }
-      tally(recs[k ^ 1], BATCH);
-      /* ldp_in_deallocate_some(inq, pkt_tbl[k ^ 1], num); */
+      tally(recs[(b + 1) % DEPTH], BATCH);       /* batch b-DEPTH+1 */
+      /* ldp_in_deallocate_some(inq, pkt_tbl[(b + 1) % DEPTH], num); */
     }
   }
-  for (; pptk_rx_batch_pending(ctx) > 0; b++) {     /* drain: the last batch */
+  for (b -= pptk_rx_batch_pending(ctx); b < batches; b++) {   /* drain, oldest first */
     if ((rc = pptk_rx_batch_complete(ctx)) != BATCH) {
       fprintf(stderr, "pptk_rx_batch_complete: %d\n", rc);
       return 1;
     }
-    tally(recs[(b - 1) & 1], BATCH);
+    tally(recs[b % DEPTH], BATCH);
   }
   printf("%lu frames, %.3f MPPS, %lu verified, %lu failed\n", pkts, pkts / (now() - t0) / 1e6,
          ok, bad);

@@ -94,7 +94,7 @@ static void *thrfn(void *arg)
           break;
         burst_head[b] = head;
         burst_num[b] = num;
-        if (pptk_rx_batch_pending(ctx) == PPTK_RX_MAX_INFLIGHT) {
+        if (pptk_rx_batch_pending(ctx) == 2) {        /* two bursts in flight */
           int rc = pptk_rx_batch_complete(ctx);           /* the other burst */
           if (rc != burst_num[b ^ 1]) {
             t->rc = rc < 0 ? rc : -1;

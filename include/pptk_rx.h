@@ -155,9 +155,9 @@ int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
  * dominates LDP-sized batches; DESIGN.md "Pipelined host batches"):
  *
  *   ldp_in_nextpkts(q, pkts[k], ...);  pptk_rx_batch_submit(ctx, pkts[k], n, recs[k]);
- *   if (pptk_rx_batch_pending(ctx) == PPTK_RX_MAX_INFLIGHT) {
- *     pptk_rx_batch_complete(ctx);      -- batch k-1: recs final, frames free
- *     ... use recs[k-1] ...;  ldp_in_deallocate_some(q, pkts[k-1], ...);
+ *   if (pptk_rx_batch_pending(ctx) == DEPTH) {   -- DEPTH <= PPTK_RX_MAX_INFLIGHT
+ *     pptk_rx_batch_complete(ctx);      -- batch k-DEPTH+1: recs final, frames free
+ *     ... use its recs ...;  ldp_in_deallocate_some(q, its pkts, ...);
  *   }
  *
  * submit gathers and enqueues one batch of 1..opts.max_batch frames (one
@@ -166,13 +166,14 @@ int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
  * OLDEST outstanding submission (FIFO) and returns its frame count (> 0):
  * after it its records are final and none of its pointers is retained.
  * Results are those of pptk_rx_batch.  At most PPTK_RX_MAX_INFLIGHT
- * submissions are outstanding per context (submit returns -EBUSY beyond);
+ * submissions are outstanding per context (submit returns -EBUSY beyond;
+ * each depth in use keeps its own staging buffers, allocated on first use);
  * pptk_rx_batch returns -EBUSY while any is; num == 0 submits nothing and
  * returns 0; num > opts.max_batch is -EINVAL (use pptk_rx_batch);
  * complete with nothing outstanding returns -ENOENT.  A failed submit
  * leaves nothing outstanding.  pptk_rx_ctx_destroy waits for (and drops)
  * outstanding submissions. */
-#define PPTK_RX_MAX_INFLIGHT 2
+#define PPTK_RX_MAX_INFLIGHT 4
 int pptk_rx_batch_submit(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts, int num,
                          struct pptk_rx_rec *recs);
 int pptk_rx_batch_complete(struct pptk_rx_ctx *ctx);

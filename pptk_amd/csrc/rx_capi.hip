@@ -166,7 +166,9 @@ struct pptk_rx_ctx {
   // pptk_rx_autotune's choice per automatic variant, for fixed-stride [0]
   // and offset-described [1] batches (-1: the automatic variant itself)
   int tuned[2][RX_NVARIANTS];
-  RxSlot slot[2];      // host-batch pipeline (pptk_rx_batch, pptk_rx_batch_submit)
+  // host-batch pipeline: pptk_rx_batch double-buffers over slots 0 and 1,
+  // pptk_rx_batch_submit rotates over all of them (allocated on first use)
+  RxSlot slot[PPTK_RX_MAX_INFLIGHT];
   int async_head = 0;  // slot of the oldest outstanding submission
   int async_n = 0;     // outstanding submissions (0..PPTK_RX_MAX_INFLIGHT)
   std::vector<RxRing> rings;
@@ -277,8 +279,7 @@ static void free_slot(RxSlot &sl) {
 }
 
 static void free_staging(pptk_rx_ctx *c) {
-  free_slot(c->slot[0]);
-  free_slot(c->slot[1]);
+  for (RxSlot &sl : c->slot) free_slot(sl);
 }
 
 void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
@@ -1241,9 +1242,9 @@ int pptk_rx_batch_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, i
   if (!dg.ok) return -EIO;
   const RxRing *ring = ring_of(c, pkts, num);
   const RxRing *rreg = records_region(c, recs, (size_t)num * sizeof(pptk_rx_rec));
-  // the slots alternate in submission order (FIFO), so consecutive
+  // the slots rotate in submission order (FIFO), so consecutive
   // submissions run on different streams and may overlap on the GPU
-  RxSlot &sl = c->slot[(c->async_head + c->async_n) & 1];
+  RxSlot &sl = c->slot[(c->async_head + c->async_n) % PPTK_RX_MAX_INFLIGHT];
   int rc = ensure_slot(c, sl, std::max<size_t>(c->opts.max_batch, 1), ring ? 64 : chunk_bytes(c));
   if (rc == 0) rc = enqueue_chunk(c, sl, pkts, (size_t)num, recs, ring, rreg, pool_of(c));
   if (rc != 0) return rc;
@@ -1260,7 +1261,7 @@ int pptk_rx_batch_complete(struct pptk_rx_ctx *c) {
   const int cnt = (int)sl.count;
   const int rc = retire(sl, c->pool);
   // (dropped from the queue even on an error: its slot is idle again)
-  c->async_head ^= 1;
+  c->async_head = (c->async_head + 1) % PPTK_RX_MAX_INFLIGHT;
   --c->async_n;
   return rc ? rc : cnt;
 }

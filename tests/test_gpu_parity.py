@@ -397,16 +397,20 @@ def _packet_slice(pkts, lo, hi):
     return s
 
 
-@pytest.mark.parametrize("mode", ["staged", "ring", "ring_recs"])
+MAX_INFLIGHT = 4   # include/pptk_rx.h PPTK_RX_MAX_INFLIGHT
+
+
+@pytest.mark.parametrize("mode,depth", [("staged", 2), ("ring", 2), ("ring_recs", 2),
+                                        ("staged", 4), ("ring_recs", 4)])
 @pytest.mark.parametrize("name", ["fuzz", "cmix", "c64", "c1500"])
-def test_host_batch_pipelined(name, mode, dev):
+def test_host_batch_pipelined(name, mode, depth, dev):
     """pptk_rx_batch_submit / _complete as an LDP rx loop uses them: ragged
-    batches of 1 .. max_batch frames submitted two deep (staged frames, frames
-    in a registered ring, and records into a registered array too), every
-    record against the golden set; and the queue contract: FIFO frame counts,
-    -EBUSY for a third submission and for pptk_rx_batch while any is
-    outstanding, -EINVAL above max_batch, -ENOENT on an empty queue, and a
-    context destroyed with submissions outstanding."""
+    batches of 1 .. max_batch frames submitted `depth` deep (staged frames,
+    frames in a registered ring, and records into a registered array too),
+    every record against the golden set; and the queue contract: FIFO frame
+    counts, -EBUSY for a submission beyond PPTK_RX_MAX_INFLIGHT and for
+    pptk_rx_batch while any is outstanding, -EINVAL above max_batch, -ENOENT
+    on an empty queue, and a context destroyed with submissions outstanding."""
     import errno
     from pptk_amd.records import REC_DTYPE
     from pptk_amd.rx import RxContext, ldp_packets
@@ -437,20 +441,17 @@ def test_host_batch_pipelined(name, mode, dev):
         for i, (lo, k) in enumerate(sizes):
             ctx.submit_host(_packet_slice(pkts, lo, lo + k), out[lo:lo + k])
             queue.append(k)
-            if ctx.pending_host() == 2:
-                if lap == 0 and i == 1:
-                    with pytest.raises(OSError) as e:
-                        ctx.submit_host(_packet_slice(pkts, 0, 1), out[:1])
-                    assert e.value.errno == errno.EBUSY
-                    with pytest.raises(OSError) as e:
-                        ctx.batch_host(_packet_slice(pkts, 0, 1), out=np.zeros(1, REC_DTYPE))
-                    assert e.value.errno == errno.EBUSY
+            if lap == 0 and i == 1:
+                with pytest.raises(OSError) as e:
+                    ctx.batch_host(_packet_slice(pkts, 0, 1), out=np.zeros(1, REC_DTYPE))
+                assert e.value.errno == errno.EBUSY
+            if ctx.pending_host() == depth:
                 assert ctx.complete_host() == queue.pop(0)
         while queue:
             assert ctx.complete_host() == queue.pop(0)
         assert ctx.pending_host() == 0
         d = diff_records(out.copy(), z["recs"])
-        assert not d, f"{mode} lap {lap}: " + d
+        assert not d, f"{mode} depth {depth} lap {lap}: " + d
     with pytest.raises(OSError) as e:
         ctx.complete_host()
     assert e.value.errno == errno.ENOENT
@@ -461,12 +462,16 @@ def test_host_batch_pipelined(name, mode, dev):
     # the synchronous call works again on the same slots
     d = diff_records(ctx.batch_host(pkts), z["recs"])
     assert not d, f"{mode} sync after async: " + d
-    # destroyed with two submissions outstanding: waits for them, no fault
+    # the queue is full at PPTK_RX_MAX_INFLIGHT; the context is destroyed
+    # with every submission outstanding: it waits for them, no fault
     k = min(n, max_batch)
-    spare = np.zeros(k, REC_DTYPE)
-    ctx.submit_host(_packet_slice(pkts, 0, k), out[:k])
-    ctx.submit_host(_packet_slice(pkts, 0, k), spare)
-    assert ctx.pending_host() == 2
+    spare = [np.zeros(k, REC_DTYPE) for _ in range(MAX_INFLIGHT)]
+    for j in range(MAX_INFLIGHT):
+        ctx.submit_host(_packet_slice(pkts, 0, k), spare[j])
+    with pytest.raises(OSError) as e:
+        ctx.submit_host(_packet_slice(pkts, 0, k), out[:k])
+    assert e.value.errno == errno.EBUSY
+    assert ctx.pending_host() == MAX_INFLIGHT
     ctx.close()
 
 

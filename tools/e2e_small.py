@@ -1,9 +1,9 @@
 """BENCH TOOLING: latency of pptk_rx_batch for small LDP-sized batches (the
 rx loop hands out 32 - 4096 frames per ldp_in_nextpkts call): median
 microseconds per call and the frame rate, staged and zero-copy ring; and
-the same batches through pptk_rx_batch_submit / _complete two deep
-(`pipe_*`: microseconds per batch in a steady loop of back-to-back
-submissions, what an rx loop that overlaps batches gets).
+the same batches through pptk_rx_batch_submit / _complete E2E_DEPTH deep
+(default 2; `pipe_*`: microseconds per batch in a steady loop of
+back-to-back submissions, what an rx loop that overlaps batches gets).
 
     python tools/e2e_small.py [cfg]
 """
@@ -38,8 +38,10 @@ def main():
     out_mode = os.environ.get("E2E_OUT", "reuse")
     out = {"cfg": cfg, "out": out_mode,
            "gather_threads": int(os.environ.get("E2E_GATHER_THREADS", "1"))}
-    both = np.zeros(2 * nmax, dtype=REC_DTYPE)     # two record arrays (pipelined)
-    outbuf, outbuf2 = both[:nmax], both[nmax:]
+    depth = int(os.environ.get("E2E_DEPTH", "2"))
+    out["depth"] = depth
+    both = np.zeros(depth * nmax, dtype=REC_DTYPE)     # a record array per batch in flight
+    outbuf = both[:nmax]
     for mode in ("staged", "ring"):
         ctx = RxContext(0, bytes(range(1, 17)), max_batch=nmax, max_frame=1518,
                         gather_threads=int(os.environ.get("E2E_GATHER_THREADS", "1")),
@@ -62,20 +64,20 @@ def main():
             us = float(np.median(ts)) * 1e6
             out[f"{mode}_{n}"] = {"us_per_call": round(us, 1), "mpkts": round(n / us, 2)}
             if hasattr(ctx._L, "pptk_rx_batch_submit"):
-                outs = [outbuf[:n], outbuf2[:n]]
+                outs = [both[j * nmax:j * nmax + n] for j in range(depth)]
                 reps = 300 if n <= 4096 else 60
                 runs = []
                 for _ in range(3):
                     t0 = time.perf_counter()
                     for k in range(reps):
-                        if ctx.pending_host() == 2:
+                        if ctx.pending_host() == depth:
                             ctx.complete_host()
-                        ctx.submit_host(pkts, outs[k & 1])
+                        ctx.submit_host(pkts, outs[k % depth])
                     while ctx.pending_host():
                         ctx.complete_host()
                     runs.append((time.perf_counter() - t0) / reps)
-                assert not diff_records(outs[0].copy(), want[:n]), ("pipe", mode, n)
-                assert not diff_records(outs[1].copy(), want[:n]), ("pipe", mode, n)
+                for o_ in outs:
+                    assert not diff_records(o_.copy(), want[:n]), ("pipe", mode, n)
                 us = float(np.median(runs)) * 1e6
                 out[f"pipe_{mode}_{n}"] = {"us_per_batch": round(us, 1),
                                            "mpkts": round(n / us, 2)}
