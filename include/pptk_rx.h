@@ -142,7 +142,9 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *ctx);
 /* Host in -> host out.  Gathers the borrowed ldp_packet frames into pinned
  * staging (or reads them in place from a registered ring, see below), copies
  * them to HBM, runs the transform and copies the records back, in chunks of
- * opts.max_batch frames double-buffered over two streams; synchronous: on
+ * opts.max_batch frames, up to four in flight on their own streams (each
+ * with its own staging, allocated when a call first has that many chunks);
+ * synchronous: on
  * return recs[0..num) are final and no pointer in pkts is retained.
  * ancillary fields are neither read nor written.  Frames longer than
  * opts.max_frame get PPTK_RX_F_MALFORMED only. */

@@ -1191,6 +1191,16 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
   return 0;
 }
 
+// Slots a synchronous pptk_rx_batch rotates over (chunks in flight; a slot
+// is allocated when a call first has that many chunks): four measured
+// +17-24 % on 1 M-frame C64 calls against two, C1500 +1-2 % (at the PCIe
+// ceiling either way; DESIGN.md "End-to-end").  PPTK_RX_SYNC_SLOTS (2 ..
+// PPTK_RX_MAX_INFLIGHT) overrides.
+static size_t sync_slots() {
+  static const long v = env_long("PPTK_RX_SYNC_SLOTS", PPTK_RX_MAX_INFLIGHT);
+  return (size_t)std::min<long>(std::max<long>(v, 2), PPTK_RX_MAX_INFLIGHT);
+}
+
 // Staging bytes a slot needs for one chunk of this context's batches.
 static size_t chunk_bytes(const pptk_rx_ctx *c) {
   const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
@@ -1214,11 +1224,12 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
   WorkerPool *pool = pool_of(c);
   int rc = 0;
-  // Double-buffered: while chunk k runs on one slot's stream (H2D, kernel,
-  // D2H), the host gathers chunk k+1 into the other slot.
+  // Multi-buffered: while chunk k runs on one slot's stream (H2D, kernel,
+  // D2H), the host gathers the next chunks into the other slots.
+  const size_t nslots = sync_slots();
   size_t k = 0, cnt = 0;
   for (size_t first = 0; first < (size_t)num && rc == 0; first += cnt, ++k) {
-    RxSlot &sl = c->slot[k & 1];
+    RxSlot &sl = c->slot[k % nslots];
     if ((rc = retire(sl, pool)) != 0) break;
     cnt = std::min(chunk, (size_t)num - first);
     if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes(c))) != 0) break;
