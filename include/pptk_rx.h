@@ -236,9 +236,11 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *ctx, const uint16_t *d_len,
                        void *stream);
 
 /* Mixed-size batch in one call: pptk_rx_bin_device() into d_perm/d_scratch,
- * then one launch per length group (64..113, ..241, ..497, ..1009, ..1521
- * bytes, longer), each streamed by the kernel shape sized for that group
- * instead of every frame by the shape of the longest.  Requires d_len;
+ * then one launch per length group (..113, ..1521 bytes, longer), each
+ * streamed by the kernel shape sized for that group instead of every frame
+ * by the shape of the longest.  (On MI355X the batch-order call,
+ * pptk_rx_batch_device with d_off/d_len, is faster on mixed traffic: every
+ * finer grouping measured slower, DESIGN.md "Binned CMIX".)  Requires d_len;
  * b->d_perm is ignored (d_perm receives the processing order).  b->max_len
  * (when nonzero) is a hint: the groups above it are folded into the group
  * that holds it (one launch fewer each; a wrong hint changes speed only).

@@ -19,22 +19,23 @@ constexpr int NB = kGroups;   // length groups
 constexpr int BT = 256;       // threads per block
 constexpr int NWARP = BT / 64;
 
-__device__ __forceinline__ int bin_of(uint32_t len) {
+__device__ __forceinline__ int bin_of(uint32_t len, const BinBounds &bb) {
   int b = 0;
 #pragma unroll
-  for (int k = 0; k < NB - 1; ++k) b += len > kGroupMaxLen[k];
+  for (int k = 0; k < NB - 1; ++k) b += len > bb.b[k];
   return b;
 }
 
 __global__ __launch_bounds__(BT) void bin_count(const uint16_t *len, uint64_t n,
-                                                uint64_t per_block, uint32_t *counts) {
+                                                uint64_t per_block, uint32_t *counts,
+                                                BinBounds bb) {
   __shared__ uint32_t h[NB];
   if (threadIdx.x < NB) h[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t lo = blockIdx.x * per_block;
   const uint64_t hi = min(lo + per_block, n);
   for (uint64_t i = lo + threadIdx.x; i < hi; i += BT)
-    atomicAdd(&h[bin_of(len[i])], 1u);
+    atomicAdd(&h[bin_of(len[i], bb)], 1u);
   __syncthreads();
   if (threadIdx.x < NB) counts[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
@@ -75,7 +76,8 @@ __global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, u
 // scattered 8- and 2-byte reads that each fetch a whole 64-byte sector)
 __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t n,
                                                   uint64_t per_block, const uint32_t *offs,
-                                                  uint32_t *perm, BinDesc bdesc) {
+                                                  uint32_t *perm, BinDesc bdesc,
+                                                  BinBounds bb) {
   __shared__ uint32_t cursor[NB];
   __shared__ uint32_t wcnt[NWARP][NB];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t 
   for (uint64_t c0 = lo; c0 < hi; c0 += BT) {
     const uint64_t i = c0 + threadIdx.x;
     const bool ok = i < hi;
-    const int b = ok ? bin_of(len[i]) : -1;
+    const int b = ok ? bin_of(len[i], bb) : -1;
     uint32_t rank = 0;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
@@ -141,16 +143,17 @@ const uint32_t *bin_table(const void *scratch, int grid) {
 }
 
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm, void *scratch,
-                      hipStream_t s, int grid, const BinDesc &bdesc) {
+                      hipStream_t s, int grid, const BinDesc &bdesc,
+                      const BinBounds &bounds) {
   if (n == 0) return hipSuccess;
   const uint64_t per_block = ((n + grid - 1) / grid + BT - 1) / BT * BT;
   const int g = (int)((n + per_block - 1) / per_block);
   uint32_t *counts = (uint32_t *)scratch;
-  hipLaunchKernelGGL(bin_count, dim3(g), dim3(BT), 0, s, len, n, per_block, counts);
+  hipLaunchKernelGGL(bin_count, dim3(g), dim3(BT), 0, s, len, n, per_block, counts, bounds);
   hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, s, counts, (uint32_t)(NB * g),
                      counts + (size_t)NB * grid);
   hipLaunchKernelGGL(bin_scatter, dim3(g), dim3(BT), 0, s, len, n, per_block,
-                     (const uint32_t *)counts, perm, bdesc);
+                     (const uint32_t *)counts, perm, bdesc, bounds);
   return hipGetLastError();
 }
 

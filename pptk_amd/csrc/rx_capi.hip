@@ -720,6 +720,34 @@ int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const ui
   return hip_err(launch_mss_clamp(a, grid, (hipStream_t)stream));
 }
 
+// The length groups of the mixed path: kGroupMaxLen, or (A/B experiment)
+// PPTK_RX_BIN_BOUNDS="b0,b1", non-decreasing upper bounds of groups 0 and 1
+// (equal neighbours leave a group empty; it is not launched).
+static const BinBounds &bin_bounds() {
+  static const BinBounds bb = [] {
+    BinBounds r;
+    for (int k = 0; k < kGroups - 1; ++k) r.b[k] = kGroupMaxLen[k];
+    const char *e = getenv("PPTK_RX_BIN_BOUNDS");
+    if (!e) return r;
+    BinBounds t = r;
+    for (int k = 0; k < kGroups - 1; ++k) {
+      char *end = nullptr;
+      const unsigned long v = strtoul(e, &end, 10);
+      if (end == e || v > 65535 || (k && v < t.b[k - 1])) return r;
+      t.b[k] = (uint32_t)v;
+      e = *end == ',' ? end + 1 : end;
+    }
+    return t;
+  }();
+  return bb;
+}
+
+static bool default_bounds(const BinBounds &bb) {
+  for (int k = 0; k < kGroups - 1; ++k)
+    if (bb.b[k] != kGroupMaxLen[k]) return false;
+  return true;
+}
+
 int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
                                uint32_t *d_perm, void *d_scratch, void *stream) {
   int rc = check_batch(c, b);
@@ -732,7 +760,9 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
   // the group launches stream them instead of gathering them through d_perm
   BinDesc bd{b->d_off, b->stride, bin_desc_off(d_scratch, kBinGrid),
              bin_desc_len(d_scratch, kBinGrid, b->n)};
-  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid, bd);
+  const BinBounds &bb = bin_bounds();
+  const bool dflt = default_bounds(bb);
+  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid, bd, bb);
   if (e != hipSuccess) return -EIO;
   RxKArgs a = batch_args(c, b);
   a.perm = d_perm;
@@ -745,8 +775,11 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
   for (int g = 0; g < kGroups; ++g) {
     // the group holding max_len also takes every group above it (all empty
     // when the hint is right; a wrong hint costs speed, never results)
-    const bool last = g == kGroups - 1 || kGroupMaxLen[g] >= maxlen;
-    const int variant = fv >= 0 && fv != RX_L4 ? fv : kGroupVariant[g];
+    const bool last = g == kGroups - 1 || bb.b[g] >= maxlen;
+    if (!last && g > 0 && bb.b[g] == bb.b[g - 1]) continue;   // empty by its bounds
+    const int variant = fv >= 0 && fv != RX_L4 ? fv
+                        : dflt || g == kGroups - 1 ? kGroupVariant[g]
+                                                   : pick_variant(bb.b[g] + 15);
     a.range_lo = tab + g;
     a.range_hi = tab + (last ? kGroups : g + 1);
     a.tune = pick_tune(c, variant, true);
@@ -817,7 +850,7 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *c, const uint16_t *d_len, uint64_t n,
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, kBinGrid,
-                            BinDesc{nullptr, 0, nullptr, nullptr}));
+                            BinDesc{nullptr, 0, nullptr, nullptr}, bin_bounds()));
 }
 
 static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {

@@ -93,11 +93,15 @@ enum RxVariant {
 // Length groups of pptk_rx_batch_device_mixed: group g holds the frames with
 // len <= kGroupMaxLen[g] (and above the previous bound) and is streamed by
 // kGroupVariant[g], whose 16*T*S-byte shape covers len + 15 bytes of chunk
-// misalignment; the last group takes everything longer (tail loop).
-constexpr int kGroups = 6;
-constexpr uint32_t kGroupMaxLen[kGroups] = {113, 241, 497, 1009, 1521, 0xffffffffu};
-constexpr int kGroupVariant[kGroups] = {RX_T4S2, RX_T8S2, RX_T16S2, RX_T16S4, RX_T16S6,
-                                        RX_T64S2};
+// misalignment; the last group takes everything longer (tail loop).  Three
+// groups: every finer split measured slower on CMIX (six groups 3.54 ms,
+// 64..241 / rest 3.20, 64..113 / rest 3.13, one group 3.03, batch order
+// 2.82; DESIGN.md "Binned CMIX"): each group launch sweeps the whole buffer
+// for its frames, and the team-streamed kernel has no per-lane length
+// divergence for binning to remove.
+constexpr int kGroups = 3;
+constexpr uint32_t kGroupMaxLen[kGroups] = {113, 1521, 0xffffffffu};
+constexpr int kGroupVariant[kGroups] = {RX_T4S2, RX_T16S6, RX_T64S2};
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
 // tx second pass: frames[base(i) + off] = value (big-endian) for the
@@ -119,8 +123,14 @@ struct BinDesc {
   uint64_t *boff;        // binned offsets (scratch), or null
   uint16_t *blen;        // binned lengths (scratch)
 };
+// Upper length bounds of groups 0 .. kGroups-2 (the last takes the rest):
+// kGroupMaxLen, or a coarser grouping (equal neighbours = empty groups).
+struct BinBounds {
+  uint32_t b[kGroups - 1];
+};
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm,
-                      void *scratch, hipStream_t s, int grid, const BinDesc &bdesc);
+                      void *scratch, hipStream_t s, int grid, const BinDesc &bdesc,
+                      const BinBounds &bounds);
 size_t bin_scratch_bytes(uint64_t n, int grid);
 const uint32_t *bin_table(const void *scratch, int grid);
 uint64_t *bin_desc_off(void *scratch, int grid);

@@ -140,7 +140,7 @@ def test_binned_order_and_hash_out(name, dev):
     assert np.array_equal(perm, np.argsort(_group_of(z["len"]), kind="stable"))
 
 
-GROUP_MAX_LEN = [113, 241, 497, 1009, 1521]   # rx_internal.h kGroupMaxLen
+GROUP_MAX_LEN = [113, 1521]   # rx_internal.h kGroupMaxLen
 
 
 def _group_of(lens):
@@ -207,8 +207,8 @@ def test_mixed_empty_trailing_groups_perm_own_allocation(dev):
     """Advisor round 1: with max_len = 0 every length group is launched, and
     an empty trailing group's range starts at n -- one past the permutation.
     The permutation here is its own page-sized hipMalloc (1 024 entries) and
-    no frame is longer than 1 009 bytes, so the last two groups are empty:
-    their launches must return before reading any descriptor."""
+    no frame is longer than 1 009 bytes, so the last group (past 1 521 bytes)
+    is empty: its launch must return before reading any descriptor."""
     import framegen
     from oracle.oracle import Oracle, make_opts
     rng = np.random.default_rng(1009)

@@ -15,6 +15,8 @@ measurement functions; prints one JSON line with the timing and
 of the write-amplification ratio WRITE_SIZE / changed bytes."""
 import argparse
 import json
+
+import numpy as np
 import os
 import sys
 
@@ -144,6 +146,30 @@ def main():
         b = make_batch("cmix", n, dev)
         r = bench.binned_bench(ctx, b, n, dev, args.steps, args.warmup)
         r["changed_bytes_per_launch"] = 64 * n
+    elif op == "binned_ab":
+        # batch order and binned on the same CMIX batch and record buffer,
+        # alternating rounds (PPTK_RX_BIN_BOUNDS sets the binned groups)
+        b = make_batch("cmix", n, dev)
+        recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"], recs=recs)
+        bo, bi = [], []
+        for _ in range(3):
+            for _ in range(args.warmup):
+                ctx.batch_device(b["frames"], n, **kw)
+            torch.cuda.synchronize(dev)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.steps)]
+            for a, z in evs:
+                a.record()
+                ctx.batch_device(b["frames"], n, **kw)
+                z.record()
+            torch.cuda.synchronize(dev)
+            bo += [a.elapsed_time(z) for a, z in evs]
+            bi.append(bench.binned_bench(ctx, b, n, dev, args.steps, args.warmup,
+                                         recs=recs)["ms_per_batch"])
+        r = {"batch_order_ms": round(float(np.median(bo)), 4),
+             "binned_ms": round(float(np.median(bi)), 4),
+             "bounds": os.environ.get("PPTK_RX_BIN_BOUNDS", "default")}
     elif op in ("allgather", "allgather_copy"):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
