@@ -184,7 +184,7 @@ int pptk_rx_batch_pending(const struct pptk_rx_ctx *ctx);
 /* Zero-copy rx rings: register a host region (e.g. a netmap ring's buffer
  * area or a socket ring) once; pptk_rx_batch() calls whose frames all lie in
  * one registered ring skip the host gather into staging: a chunk whose
- * frames fill >= 80 % of the ring span they cover (and that span > 8 MiB)
+ * frames fill >= 80 % of the ring span they cover (and that span > 2 MiB)
  * is copied down by DMA as one span, any other chunk is read by the GPU in
  * place over PCIe (PPTK_RX_RING_DMA_PCT sets the fraction).  Every frame's
  * end rounded up to 16 bytes must lie inside the region.  A registered

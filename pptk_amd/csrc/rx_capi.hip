@@ -904,11 +904,14 @@ static bool fit_span(RxSlot &sl, size_t bytes) {
 // pinned memory over PCIe: one kernel launch per chunk instead of three
 // host-to-device copies, the launch and a device-to-host copy -- when the
 // frames come from a registered ring (the kernel reads them over PCIe
-// anyway) or the staged frame bytes are at most this many (8 MiB: above
-// it the DMA copy of bulky frames beats the kernel's PCIe reads; measured,
-// DESIGN.md "Small LDP-sized batches").  PPTK_RX_DIRECT_MAX_BYTES overrides.
+// anyway) or the staged frame bytes are at most this many.  2 MiB: with
+// four chunks in flight the DMA copy beats the kernel's PCIe reads from
+// there on (1 M-frame C64 calls 375 -> 449 Mpkt/s staged, ring spans
+// 325 -> 408; 4 096-frame C1500 calls 278 -> 238 us), while calls of up to
+// ~1 400 1500-byte frames keep the single launch (DESIGN.md "End-to-end").
+// PPTK_RX_DIRECT_MAX_BYTES overrides.
 static size_t direct_max_bytes() {
-  static const long v = env_long("PPTK_RX_DIRECT_MAX_BYTES", 8l << 20);
+  static const long v = env_long("PPTK_RX_DIRECT_MAX_BYTES", 2l << 20);
   return v < 0 ? 0 : (size_t)v;
 }
 
