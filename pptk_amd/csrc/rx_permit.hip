@@ -29,6 +29,7 @@
 // Bucket values come from the records the rx kernel wrote (src_bucket, the
 // reference's own hash of the masked source, iphash/iphash.c:157-162).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -165,12 +166,44 @@ __global__ __launch_bounds__(PT) void tokens_refill(uint32_t *tokens, uint32_t s
 // Onesweep with 9-bit digits: the keys (log2(hash_size) + 1 bits, 17 for
 // 2^16 buckets) sort in two passes instead of the default 8-bit digits'
 // three; the values are the frame indices, read from a counting iterator
-// (no index array is written).
-using SortConfig = rocprim::radix_sort_config<
+// (no index array is written).  Blocks of 1024 threads x 8 keys: 16 M
+// records 0.529 ms per batch, against 0.61 with 512 x 16, 0.76 with
+// 256 x 16, 0.67 with 512 x 8, 0.60 with 1024 x 12, 0.57 with 1024 x 16
+// and 0.66 with 1024 x 4 (tools/opbench.py permit).
+// PPTK_RX_PERMIT_SORT (A/B only): 1 = 512 x 16, 2 = 256 x 16, 3 = 512 x 8.
+template <unsigned BS, unsigned IPT>
+using OnesweepConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 16>,
-                                        rocprim::kernel_config<512, 16>, 9,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<BS, IPT>,
+                                        rocprim::kernel_config<BS, IPT>, 9,
                                         rocprim::block_radix_rank_algorithm::match>>;
+
+int sort_variant() {
+  static const int v = [] {
+    const char *e = getenv("PPTK_RX_PERMIT_SORT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <class Cfg>
+hipError_t sort_pairs_cfg(void *tmp, size_t &tb, const uint32_t *keys, uint32_t *skeys,
+                          uint32_t *svals, size_t n, unsigned bits, hipStream_t st) {
+  return rocprim::radix_sort_pairs<Cfg>(tmp, tb, keys, skeys,
+                                        rocprim::counting_iterator<uint32_t>(0), svals, n, 0,
+                                        bits, st);
+}
+
+// (tmp == nullptr: the temporary size of the chosen shape into tb)
+hipError_t sort_pairs(void *tmp, size_t &tb, const uint32_t *keys, uint32_t *skeys,
+                      uint32_t *svals, size_t n, unsigned bits, hipStream_t st) {
+  switch (sort_variant()) {
+    case 1: return sort_pairs_cfg<OnesweepConfig<512, 16>>(tmp, tb, keys, skeys, svals, n, bits, st);
+    case 2: return sort_pairs_cfg<OnesweepConfig<256, 16>>(tmp, tb, keys, skeys, svals, n, bits, st);
+    case 3: return sort_pairs_cfg<OnesweepConfig<512, 8>>(tmp, tb, keys, skeys, svals, n, bits, st);
+    default: return sort_pairs_cfg<OnesweepConfig<1024, 8>>(tmp, tb, keys, skeys, svals, n, bits, st);
+  }
+}
 
 int key_bits(uint32_t hash_size) {
   int b = 0;
@@ -188,10 +221,8 @@ struct PermitScratch {
 
 hipError_t layout(uint64_t n, uint32_t hash_size, void *base, PermitScratch &s) {
   size_t sort_tmp = 0;
-  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
-      nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
-      rocprim::counting_iterator<uint32_t>(0), (uint32_t *)nullptr, (size_t)n, 0,
-      (unsigned)key_bits(hash_size));
+  hipError_t e = sort_pairs(nullptr, sort_tmp, nullptr, nullptr, nullptr, (size_t)n,
+                            (unsigned)key_bits(hash_size), 0);
   if (e != hipSuccess) return e;
   uint8_t *p = (uint8_t *)base;
   size_t off = 0;
@@ -230,9 +261,8 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   if ((e = hipMemsetAsync(s.first, 0, (size_t)a.hash_size * 8, st)) != hipSuccess) return e;
   hipLaunchKernelGGL(permit_keys, dim3(blocks(a.n)), dim3(PT), 0, st, a, s.keys);
   size_t tb = s.tmp_bytes;
-  e = rocprim::radix_sort_pairs<SortConfig>(s.tmp, tb, s.keys, s.skeys,
-                                            rocprim::counting_iterator<uint32_t>(0), s.svals,
-                                            (size_t)a.n, 0, (unsigned)key_bits(a.hash_size), st);
+  e = sort_pairs(s.tmp, tb, s.keys, s.skeys, s.svals, (size_t)a.n,
+                 (unsigned)key_bits(a.hash_size), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(permit_bounds, dim3(blocks((a.n + 3) / 4)), dim3(PT), 0, st, a, s.skeys,
                      s.first, s.end);
