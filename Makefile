@@ -28,7 +28,7 @@ $(OBJDIR)/host/%.o: pptk_amd/csrc/host/%.c $(HDRS)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(LIB): $(HIP_OBJS) $(C_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl
 
 oracle:
 	$(MAKE) -C oracle

@@ -84,8 +84,21 @@ def dist_setup(ngpus):
     return ws, rank, dev
 
 
+# (ctx, stream) pairs that carry all-gathers: barrier() waits for them with
+# pptk_rx_comm_sync (bounded, RCCL errors surfaced) before the device-wide
+# synchronize, so a rank whose peer died exits with an error instead of
+# hanging in hipDeviceSynchronize (include/pptk_rx.h "Failure containment")
+GATHER_STREAMS = []
+COMM_SYNC_TIMEOUT_MS = 120000
+
+
 def barrier(ws, dev):
     import torch
+    for ctx, s in GATHER_STREAMS:
+        rc = ctx.comm_sync(s, COMM_SYNC_TIMEOUT_MS)
+        if rc != 0:
+            raise RuntimeError(f"all-gather stream failed: pptk_rx_comm_sync {rc} "
+                               "(-110 timeout: a peer stopped; -5 RCCL error; -125 aborted)")
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     if dist_on(ws):
@@ -306,6 +319,9 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
 
     main = torch.cuda.current_stream(dev)
     gs = torch.cuda.Stream(dev) if gbs else None
+    del GATHER_STREAMS[:]
+    if gbs:
+        GATHER_STREAMS.extend([(ctx, main), (ctx, gs)])
     kdone = [torch.cuda.Event() for _ in range(2)]
     gdone = [torch.cuda.Event() for _ in range(2)]
 
@@ -430,22 +446,27 @@ def gathered_check(prim, gbs, n, dev, k=64):
 
 def mix_sol(b, recs, n):
     """(ms, description) of the speed of light of an rx launch's traffic mix
-    on this GPU: a trivial kernel (tools/rwmix.hip) reading the same frame
-    bytes in the same 64-frame tiles and writing the same 4 KB of records
-    per tile, nothing computed; the faster of its plain and non-temporal
-    forms.  Offset-described batches (CMIX): the frame buffer read as
-    equal tiles of its whole length (the 10-byte descriptors, ~1 % of the
-    bytes, left out); None if the shapes do not fit."""
-    from tools.rwmix import mix_ms
+    on this GPU (tools/rwmix.py sol_ms): the fastest of several trivial
+    kernels reading the launch's frame bytes in its 64-frame tiles -- the
+    fixed-stride tile, or for offset-described batches (CMIX: frames packed
+    in batch order) each tile's actual span after its 10-byte descriptors --
+    and writing the tile's records, nothing computed; None if the shapes do
+    not fit.  A real ceiling only if the rx kernel never beats it
+    (roofline.mix_sol_frac <= 1)."""
+    from tools.rwmix import sol_ms
     ntiles = n // 64
     if ntiles == 0:
         return None
-    rb = 64 * b["stride"] if "off" not in b else (b["frames"].numel() - 64) // ntiles // 16 * 16
     wb = 64 * (recs.shape[1] if recs.dim() == 2 else 64)
-    if rb % 16 or rb == 0:
+    if "off" in b:
+        ms, how = sol_ms(b["frames"], n, recs, wb, off=b["off"], lens=b["lens"])
+        return round(ms, 4), (f"{ntiles} tiles, each its frames' span read after its "
+                              f"descriptors + {wb} B written, {how}")
+    rb = 64 * b["stride"]
+    if rb % 16:
         return None
-    ms = min(mix_ms(b["frames"], rb, ntiles, recs, wb, nt=nt) for nt in (0, 1))
-    return round(ms, 4), f"{ntiles} tiles x {rb} B read + {wb} B written, grid-strided, no compute"
+    ms, how = sol_ms(b["frames"], n, recs, wb, rb=rb)
+    return round(ms, 4), f"{ntiles} tiles x {rb} B read + {wb} B written, {how}"
 
 
 def binned_bench(ctx, b, n, dev, steps, warmup, recs=None):
@@ -745,34 +766,77 @@ def mss_bench(ctx, n, dev, steps, warmup, stride=80):
 
 
 def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
-    """Batched ip_permitted over the records of a C64
-    batch: buckets of the /24 source prefixes in 2^16 buckets, every IPv4
-    frame a subject, one token array carried across the timed batches."""
+    """Batched ip_permitted over a C64 batch: buckets of
+    the /24 source prefixes in 2^16 buckets, every IPv4 frame a subject, one
+    token array carried across the timed batches.  Three runs:
+      records       pptk_rx_permit_device on the 64-byte records;
+      keys          pptk_rx_permit_keys_device on the dense 4-byte keys the
+                    same rx launch wrote (pptk_rx_dev_batch.d_key);
+      keys_denying  the same with tokens refilled to 128 per bucket before
+                    every batch: ~half the frames denied, so the per-bucket
+                    resolve pass runs in every histogram block.
+    Roofline: the algorithmic bytes of a verdict are its 4-byte key read and
+    1-byte verdict written (records: the 16-byte slice of the record the key
+    is in -- a DRAM burst of 64 bytes is what the memory moves for it), plus
+    the token array read and written."""
     import torch
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch
     b = make_batch("c64", n, dev, first=rank * n)
     ctx = RxContext(dev.index, KEY, 24, 0, hash_size)
-    recs = ctx.batch_device(b["frames"], n, stride=b["stride"], fixed_len=b["fixed_len"])
+    keys = torch.empty(n, dtype=torch.int32, device=dev)
+    recs = ctx.batch_device(b["frames"], n, stride=b["stride"], fixed_len=b["fixed_len"],
+                            key_out=keys)
     del b
-    tok = torch.full((hash_size,), 1 << 20, dtype=torch.int32, device=dev)
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
     scratch = torch.empty(ctx._L.pptk_rx_permit_scratch_bytes(n, hash_size), dtype=torch.uint8,
                           device=dev)
-    for _ in range(warmup):
-        ctx.permit_device(recs, 4, tok, verdict=verdict, scratch=scratch)
-    torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
-    for a, z in ev:
-        a.record()
-        ctx.permit_device(recs, 4, tok, verdict=verdict, scratch=scratch)
-        z.record()
-    torch.cuda.synchronize(dev)
-    ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
-    return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "ms_per_batch": round(ms, 4),
-            "frames": n, "hash_size": hash_size,
-            "workload": "C64 records, IPv4 /24 buckets, all frames subject"}
+
+    def timed(call, refill=None):
+        tok = torch.full((hash_size,), 1 << 20, dtype=torch.int32, device=dev)
+        for _ in range(warmup):
+            if refill:
+                refill(tok)
+            call(tok)
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        for a, z in ev:
+            if refill:
+                refill(tok)
+            a.record()
+            call(tok)
+            z.record()
+        torch.cuda.synchronize(dev)
+        ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
+        v = verdict.cpu().numpy()
+        return ms, {"permitted": int((v == 1).sum()), "denied": int((v == 0).sum()),
+                    "not_subject": int((v == 2).sum())}
+
+    def line(ms, per_frame_bytes, what, counts):
+        alg = n * per_frame_bytes + 2 * 4 * hash_size
+        ach = alg / (ms * 1e-3) / 1e9
+        return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "ms_per_batch": round(ms, 4),
+                "frames": n, "hash_size": hash_size, "workload": what, "verdicts": counts,
+                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                             "algorithmic_bytes_per_launch": alg, "traffic": None}}
+
+    out = {}
+    ms, c = timed(lambda tok: ctx.permit_device(recs, 4, tok, verdict=verdict, scratch=scratch))
+    out = line(ms, 64 + 1, "C64 records (64 B each), IPv4 /24 buckets, all frames subject", c)
+    ms, c = timed(lambda tok: ctx.permit_keys_device(keys, 4, tok, verdict=verdict,
+                                                     scratch=scratch))
+    out["keys"] = line(ms, 4 + 1, "dense 4-byte keys of the same batch (d_key)", c)
+    ms, c = timed(lambda tok: ctx.permit_keys_device(keys, 4, tok, verdict=verdict,
+                                                     scratch=scratch),
+                  refill=lambda tok: tok.fill_(128))
+    out["keys_denying"] = line(ms, 4 + 1, "dense keys, 128 tokens per bucket before each batch "
+                                          "(~half the frames denied: resolve pass in every block)",
+                               c)
+    del recs, keys, verdict, scratch
+    torch.cuda.empty_cache()
+    return out
 
 
 def gather_bench(ctx, gb, ws, dev, steps):
@@ -780,6 +844,7 @@ def gather_bench(ctx, gb, ws, dev, steps):
     (pptk_rx_allgather_hash): time and bandwidths."""
     import torch
     main = torch.cuda.current_stream(dev)
+    GATHER_STREAMS[:] = [(ctx, main)]
     for _ in range(3):
         gb.gather(ctx, stream=main)
     barrier(ws, dev)

@@ -1,10 +1,10 @@
 /*
  * rx_multigpu.c -- one process driving every GPU of the node: one rx thread
- * and one pptk_rx_ctx per GPU, one RCCL communicator over all of them
- * (pptk_rx_comm_create_all), the batch sharded by pptk_rx_shard_range, and
- * the flow hashes all-gathered so every GPU holds the hash of every frame
- * (the C8G configuration of BASELINE.json, single-process form; bench.py
- * runs the one-process-per-GPU form).
+ * and one pptk_rx_ctx per GPU, one RCCL communicator over all of them, the
+ * batch sharded by pptk_rx_shard_range, and the flow hashes all-gathered so
+ * every GPU holds the hash of every frame (the C8G configuration of
+ * BASELINE.json, single-process form; bench.py runs the one-process-per-GPU
+ * form).
  *
  * Each thread, like an ldp/ldprecvmt.c:16-67 queue thread: copies its shard
  * of the frame set to its GPU, runs pptk_rx_batch_device with d_hash aimed
@@ -12,22 +12,81 @@
  * place on the same stream, and checks its records and the whole gathered
  * hash array against the expected records of the set file.
  *
+ * Failure containment.  The reference's queue threads share nothing
+ * (ldp/ldprecvmt.c:174-182), so one failing thread cannot stall the others;
+ * here the gather ties them together, so a thread that fails anywhere calls
+ * fail_all(), which aborts every context's communicator
+ * (pptk_rx_comm_abort): siblings waiting for a gather it will never join
+ * get -ECANCELED from pptk_rx_comm_sync (never hipStreamSynchronize on a
+ * gather stream) and the process exits non-zero instead of hanging.  A rank
+ * that never joins at all makes the others' pptk_rx_comm_create return
+ * -ETIMEDOUT after opts.comm_timeout_ms.
+ *
  *   gcc -O2 -pthread -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude \
  *       examples/rx_multigpu.c -Lpptk_amd -lpptkrx -L/opt/rocm/lib -lamdhip64 -o rx_multigpu
- *   ./rx_multigpu frames.rxq [gpus [rounds]]
+ *   ./rx_multigpu frames.rxq [ranks [rounds]]
+ *
+ * ranks defaults to the visible GPUs; rank r runs on GPU r % visible.
+ * Environment (tests, drills):
+ *   RX_MULTIGPU_JOIN=threads   every thread joins with pptk_rx_comm_create on
+ *                              a uid made by main (the per-process form, in
+ *                              threads) instead of pptk_rx_comm_create_all
+ *   RX_MULTIGPU_FAIL=r         rank r's thread fails: before joining (JOIN=
+ *                              threads) or before its first gather
+ *   RX_MULTIGPU_TIMEOUT_MS=t   opts.comm_timeout_ms
+ *   RX_MULTIGPU_TRACE=1        progress lines on stderr
  */
+#include <errno.h>
 #include <pthread.h>
+#include <stdarg.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
 #include "pptk_rx.h"
 #include "rxq_file.h"
 
+#define MAXR 64
+
+static struct pptk_rx_ctx *g_ctx[MAXR];
+static int g_nranks;
+static atomic_int g_failed;
+static int g_join_threads, g_fail_rank = -1;
+static uint8_t g_uid[PPTK_RX_COMM_UID_BYTES];
+static int g_trace;
+
+static void trace(const char *fmt, ...)
+{
+  struct timespec ts;
+  va_list ap;
+  if (!g_trace)
+    return;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  fprintf(stderr, "[%ld.%03ld] ", (long)ts.tv_sec, ts.tv_nsec / 1000000);
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fputc('\n', stderr);
+}
+
+/* Cancel every communicator once: no sibling keeps waiting for a gather
+ * the failed thread will not issue. */
+static void fail_all(void)
+{
+  if (atomic_exchange(&g_failed, 1))
+    return;
+  for (int i = 0; i < g_nranks; i++) {
+    int rc = pptk_rx_comm_abort(g_ctx[i]);   /* -EINVAL if it has none (yet) */
+    trace("fail_all: abort rank %d: %d", i, rc);
+  }
+}
+
 struct gpu_thread {
-  int rank, nranks, rounds;
+  int rank, nranks, rounds, device;
   struct pptk_rx_ctx *ctx;
   const struct rxq_set *set;
   unsigned long rec_mismatches, hash_mismatches;
@@ -37,7 +96,7 @@ struct gpu_thread {
 #define CHECK_HIP(x)                 \
   do {                               \
     if ((x) != hipSuccess) {         \
-      t->rc = -5;                    \
+      t->rc = -EIO;                  \
       goto out;                      \
     }                                \
   } while (0)
@@ -56,6 +115,17 @@ static void *thrfn(void *arg)
   uint64_t lo = 0, hi = 0;
   struct pptk_rx_dev_batch b;
 
+  if (g_join_threads) {   /* collective: every rank's thread joins */
+    if (t->rank == g_fail_rank) {
+      t->rc = -ECANCELED;   /* drill: this rank never joins */
+      goto out;
+    }
+    trace("rank %d: joining", t->rank);
+    t->rc = pptk_rx_comm_create(t->ctx, t->nranks, t->rank, g_uid);
+    trace("rank %d: pptk_rx_comm_create %d", t->rank, t->rc);
+    if (t->rc != 0)
+      goto out;
+  }
   pptk_rx_shard_range(n, t->nranks, t->rank, &first, &count, &per);
   if (count) {   /* the shard's bytes, offsets rebased to its first frame */
     lo = s->off[first];
@@ -67,7 +137,7 @@ static void *thrfn(void *arg)
         hi = e;
     }
   }
-  CHECK_HIP(hipSetDevice(t->rank));   /* rank i = ctxs[i] = device i */
+  CHECK_HIP(hipSetDevice(t->device));
   CHECK_HIP(hipStreamCreate(&st));
   CHECK_HIP(hipMalloc((void **)&d_frames, hi - lo + 64));
   CHECK_HIP(hipMalloc((void **)&d_off, count * 8 + 8));
@@ -79,7 +149,7 @@ static void *thrfn(void *arg)
   h_out = malloc(per * (uint64_t)t->nranks * 8 + 8);
   h_recs = malloc(count * sizeof(struct pptk_rx_rec) + 64);
   if (!h_off || !h_out || !h_recs) {
-    t->rc = -12;
+    t->rc = -ENOMEM;
     goto out;
   }
   for (uint64_t i = 0; i < count; i++)
@@ -87,6 +157,10 @@ static void *thrfn(void *arg)
   CHECK_HIP(hipMemcpy(d_frames, s->buf + lo, hi - lo + 16, hipMemcpyHostToDevice));
   CHECK_HIP(hipMemcpy(d_off, h_off, count * 8, hipMemcpyHostToDevice));
   CHECK_HIP(hipMemcpy(d_len, s->len + first, count * 2, hipMemcpyHostToDevice));
+  if (!g_join_threads && t->rank == g_fail_rank) {
+    t->rc = -ECANCELED;   /* drill: fail before the first gather */
+    goto out;
+  }
 
   memset(&b, 0, sizeof(b));
   b.d_frames = d_frames;
@@ -99,11 +173,13 @@ static void *thrfn(void *arg)
   for (int r = 0; r < t->rounds && t->rc == 0; r++) {
     if ((t->rc = pptk_rx_batch_device(t->ctx, &b, st)) != 0)
       break;
-    t->rc = pptk_rx_allgather_hash(t->ctx, b.d_hash, per, d_out, st);
+    if ((t->rc = pptk_rx_allgather_hash(t->ctx, b.d_hash, per, d_out, st)) != 0)
+      break;
+    /* bounded wait with RCCL error checks: -ECANCELED once a sibling failed */
+    t->rc = pptk_rx_comm_sync(t->ctx, st, 0);
   }
   if (t->rc)
     goto out;
-  CHECK_HIP(hipStreamSynchronize(st));
   CHECK_HIP(hipMemcpy(h_recs, d_recs, count * sizeof(struct pptk_rx_rec), hipMemcpyDeviceToHost));
   CHECK_HIP(hipMemcpy(h_out, d_out, per * (uint64_t)t->nranks * 8, hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < count; i++)
@@ -113,8 +189,13 @@ static void *thrfn(void *arg)
     if (h_out[i] != s->want[i].flow_hash)
       t->hash_mismatches++;
 out:
-  if (st)
+  trace("rank %d: done, rc %d", t->rank, t->rc);
+  if (t->rc)
+    fail_all();
+  if (st) {   /* drained: aborted gathers return, pptk_rx_comm_sync waited */
+    (void)pptk_rx_comm_sync(t->ctx, st, 0);
     (void)hipStreamDestroy(st);
+  }
   (void)hipFree(d_frames);
   (void)hipFree(d_off);
   (void)hipFree(d_len);
@@ -123,6 +204,7 @@ out:
   free(h_off);
   free(h_out);
   free(h_recs);
+  trace("rank %d: exit", t->rank);
   return NULL;
 }
 
@@ -130,55 +212,80 @@ int main(int argc, char **argv)
 {
   struct rxq_set set;
   int ndev = pptk_rx_device_count();
-  int ngpu = argc > 2 ? atoi(argv[2]) : ndev, rounds = argc > 3 ? atoi(argv[3]) : 3;
-  struct pptk_rx_ctx *ctxs[64];
-  struct gpu_thread thr[64];
-  pthread_t pth[64];
+  int nr = argc > 2 ? atoi(argv[2]) : ndev, rounds = argc > 3 ? atoi(argv[3]) : 3;
+  const char *e;
+  uint32_t timeout_ms = 0;
+  struct gpu_thread thr[MAXR];
+  pthread_t pth[MAXR];
   unsigned long bad = 0;
   int i, rc, failed = 0;
 
   if (argc < 2 || rxq_load(argv[1], &set) != 0) {
-    fprintf(stderr, "usage: rx_multigpu frames.rxq [gpus [rounds]]\n");
+    fprintf(stderr, "usage: rx_multigpu frames.rxq [ranks [rounds]]\n");
     return 1;
   }
-  if (ngpu < 1 || ngpu > ndev || ngpu > 64) {
-    fprintf(stderr, "%d GPUs requested, %d visible\n", ngpu, ndev);
+  if (ndev < 1 || nr < 1 || nr > MAXR) {
+    fprintf(stderr, "%d ranks requested, %d GPUs visible\n", nr, ndev);
     return 1;
   }
-  for (i = 0; i < ngpu; i++) {
+  g_join_threads = (e = getenv("RX_MULTIGPU_JOIN")) && !strcmp(e, "threads");
+  if ((e = getenv("RX_MULTIGPU_FAIL")))
+    g_fail_rank = atoi(e);
+  g_trace = (e = getenv("RX_MULTIGPU_TRACE")) && *e == '1';
+  if ((e = getenv("RX_MULTIGPU_TIMEOUT_MS")))
+    timeout_ms = (uint32_t)strtoul(e, NULL, 10);
+  g_nranks = nr;
+  for (i = 0; i < nr; i++) {
     struct pptk_rx_opts o;
     pptk_rx_opts_default(&o);
-    o.device = i;
+    o.device = i % ndev;
     memcpy(o.key, set.h.key, 16);
     o.iphash_bits4 = 24;
     o.iphash_bits6 = 48;
     o.iphash_size = 4096;
-    if ((rc = pptk_rx_ctx_create(&ctxs[i], &o)) != 0) {
+    if (timeout_ms)
+      o.comm_timeout_ms = timeout_ms;
+    if ((rc = pptk_rx_ctx_create(&g_ctx[i], &o)) != 0) {
       fprintf(stderr, "pptk_rx_ctx_create(%d): %d\n", i, rc);
       return 1;
     }
   }
-  if ((rc = pptk_rx_comm_create_all(ctxs, ngpu)) != 0) {
-    fprintf(stderr, "pptk_rx_comm_create_all: %d\n", rc);
+  if (g_join_threads)
+    rc = pptk_rx_comm_uid(g_uid);
+  else
+    rc = pptk_rx_comm_create_all(g_ctx, nr);
+  if (rc != 0) {
+    fprintf(stderr, "%s: %d\n", g_join_threads ? "pptk_rx_comm_uid" : "pptk_rx_comm_create_all",
+            rc);
     return 1;
   }
-  for (i = 0; i < ngpu; i++) {
-    thr[i] = (struct gpu_thread){.rank = i, .nranks = ngpu, .rounds = rounds, .ctx = ctxs[i],
-                                 .set = &set};
-    pthread_create(&pth[i], NULL, thrfn, &thr[i]);
+  for (i = 0; i < nr; i++) {
+    thr[i] = (struct gpu_thread){.rank = i, .nranks = nr, .rounds = rounds, .device = i % ndev,
+                                 .ctx = g_ctx[i], .set = &set};
+    if (pthread_create(&pth[i], NULL, thrfn, &thr[i]) != 0) {
+      fail_all();
+      nr = i;   /* join the ones started */
+      failed = 1;
+      break;
+    }
   }
-  for (i = 0; i < ngpu; i++) {
-    int nr = 0, r = -1;
+  for (i = 0; i < nr; i++) {
+    int cr = 0, r = -1;
     pthread_join(pth[i], NULL);
-    pptk_rx_comm_info(ctxs[i], &nr, &r);
-    printf("GPU %d (rank %d of %d): %lu record mismatches, %lu gathered-hash mismatches, rc %d\n",
-           i, r, nr, thr[i].rec_mismatches, thr[i].hash_mismatches, thr[i].rc);
+    pptk_rx_comm_info(g_ctx[i], &cr, &r);
+    printf("rank %d (GPU %d; communicator rank %d of %d): %lu record mismatches, "
+           "%lu gathered-hash mismatches, rc %d\n",
+           i, thr[i].device, r, cr, thr[i].rec_mismatches, thr[i].hash_mismatches, thr[i].rc);
     failed |= thr[i].rc != 0;
     bad += thr[i].rec_mismatches + thr[i].hash_mismatches;
   }
-  for (i = 0; i < ngpu; i++)
-    pptk_rx_ctx_destroy(ctxs[i]);   /* destroys the communicator too */
-  printf("rx_multigpu: %d GPUs, %u frames, %lu mismatches\n", ngpu, set.h.n, bad);
+  for (i = 0; i < g_nranks; i++) {
+    trace("destroying context %d", i);
+    pptk_rx_ctx_destroy(g_ctx[i]);   /* destroys the communicator too */
+  }
+  trace("contexts destroyed");
+  printf("rx_multigpu: %d ranks on %d GPUs, %u frames, %lu mismatches%s\n", g_nranks,
+         g_nranks < ndev ? g_nranks : ndev, set.h.n, bad, failed ? ", FAILED" : "");
   rxq_free(&set);
   return failed ? 1 : bad ? 2 : 0;
 }

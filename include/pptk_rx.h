@@ -22,7 +22,8 @@
  *
  * Plain C types only: no HIP, torch or RCCL types appear in signatures.
  * Every function returns 0 or a negative errno (-EINVAL, -ENOMEM, -EIO for
- * HIP/RCCL failures).  Nothing aborts on packet content: per-packet problems
+ * HIP/RCCL failures; the multi-GPU calls also -ETIMEDOUT, -ECANCELED and
+ * -ENOSYS, see there).  Nothing aborts on packet content: per-packet problems
  * are reported in pptk_rx_rec.flags.
  */
 #ifndef PPTK_RX_H
@@ -132,7 +133,12 @@ struct pptk_rx_opts {
   uint32_t iphash_size; /* struct ip_hash.hash_size (power of two)         */
   uint32_t max_batch;   /* pptk_rx_batch chunk (frames per staged transfer) */
   uint32_t max_frame;   /* largest frame accepted by pptk_rx_batch (<=65535)*/
+  uint32_t comm_timeout_ms; /* bound on every multi-GPU wait (communicator
+                           creation, a gather's enqueue, pptk_rx_comm_sync,
+                           teardown); 0 = PPTK_RX_COMM_TIMEOUT_MS          */
 };
+
+#define PPTK_RX_COMM_TIMEOUT_MS 60000u
 
 void pptk_rx_opts_default(struct pptk_rx_opts *opts);
 
@@ -220,6 +226,10 @@ struct pptk_rx_dev_batch {
   uint64_t *d_hash;       /* nullable                                     */
   struct pptk_rx_rec32 *d_recs32; /* nullable: compact records instead */
   struct pptk_rx_frag *d_frag;    /* nullable: fragment side records    */
+  uint32_t *d_key;        /* nullable: dense rate-limiter key per frame:
+                             src_bucket of a PARSED IPv4 frame, src_bucket |
+                             0x80000000 of a PARSED IPv6 frame, 0xffffffff
+                             otherwise (pptk_rx_permit_keys_device)      */
 };
 
 int pptk_rx_batch_device(struct pptk_rx_ctx *ctx,
@@ -269,6 +279,14 @@ int pptk_rx_permit_device(struct pptk_rx_ctx *ctx, const struct pptk_rx_rec *d_r
                           const uint8_t *d_subject, uint32_t *d_tokens,
                           uint8_t *d_verdict, void *d_scratch, void *stream);
 
+/* The same from the dense keys the receive transform wrote into
+ * pptk_rx_dev_batch.d_key (4 bytes per frame instead of a 16-byte slice of
+ * each record).  Results are those of pptk_rx_permit_device on the
+ * records of the same batch; same scratch size. */
+int pptk_rx_permit_keys_device(struct pptk_rx_ctx *ctx, const uint32_t *d_keys, uint64_t n,
+                               int family, const uint8_t *d_subject, uint32_t *d_tokens,
+                               uint8_t *d_verdict, void *d_scratch, void *stream);
+
 /* The token refill timer (batch_timer_fn, reference iphash/iphash.c:
  * 290-350) for buckets [start, end): tokens = min(tokens + add, initial).
  * Asynchronous; order it with pptk_rx_permit_device on one stream. */
@@ -286,19 +304,21 @@ int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *ctx, uint32_t *d_tokens,
  * transform verifies every such frame (IP_OK / L4_OK).  Layout arguments as
  * in pptk_rx_dev_batch; max_len is a tuning hint.  Asynchronous.
  * Fixed-stride batches run in two passes (checksums into a side array of 8
- * bytes per frame that the context allocates on first use and keeps, then
- * the field writes); PPTK_TX_TWO_PASS=0 stores the fields in place. */
+ * bytes per frame, then the field writes).  The side array is allocated and
+ * freed on `stream` from a stream-ordered pool the context owns, so tx calls
+ * of one context may run concurrently on different streams. */
 int pptk_tx_cksum_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const uint64_t *d_off,
                          const uint16_t *d_len, uint64_t stride, uint32_t fixed_len,
                          uint64_t n, uint32_t max_len, void *stream);
 
 /* The two-pass side array from the caller: `frames` * 8 bytes of device
- * memory (8-byte aligned) that the context uses instead of allocating its
- * own, e.g. a buffer placed like a record ring (its writes beside the
- * frame reads cost what record writes cost: pptk_rx_place_records).  The
- * buffer must stay valid until the context is destroyed or another buffer
- * (or NULL: back to the context's own) is set; batches larger than
- * `frames` make the context allocate its own again. */
+ * memory (8-byte aligned) that the context uses instead of its pool, e.g. a
+ * buffer placed like a record ring (its writes beside the frame reads cost
+ * what record writes cost: pptk_rx_place_records).  Every tx call of the
+ * context that fits uses this ONE buffer: such calls must not overlap (use
+ * one stream, or order the streams).  The buffer must stay valid until the
+ * context is destroyed or another buffer (or NULL: back to the pool) is
+ * set; batches larger than `frames` use the pool. */
 int pptk_tx_set_side_buffer(struct pptk_rx_ctx *ctx, void *d_side, uint64_t frames);
 
 /* Header rewrite with incremental checksum update (NAT / forwarding),
@@ -414,7 +434,18 @@ int pptk_rx_autotune(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *ba
  * per GPU, driven by one process per GPU (pptk_rx_comm_uid +
  * pptk_rx_comm_create) or by one thread per GPU of a single process
  * (pptk_rx_comm_create_all).  The communicator belongs to its context and is
- * destroyed with it (or by pptk_rx_comm_destroy). */
+ * destroyed with it (or by pptk_rx_comm_destroy).
+ *
+ * Failure containment: the reference's queue threads share nothing, so one
+ * failing thread never stalls the others; ranks of a collective do wait for
+ * each other.  So no call here waits without a bound: creation gives up
+ * after opts.comm_timeout_ms (-ETIMEDOUT, e.g. a rank that never joins),
+ * pptk_rx_comm_sync waits for a stream with a deadline and surfaces RCCL's
+ * asynchronous errors (a dead peer: -EIO), and pptk_rx_comm_abort lets any
+ * thread cancel a communicator other threads are waiting on.  After
+ * -ETIMEDOUT / -EIO from a gather or a sync, or an abort, the communicator
+ * is dead (calls on it return -ECANCELED): destroy it and create a new one.
+ * RCCL is loaded on first use; without it these calls return -ENOSYS. */
 #define PPTK_RX_COMM_UID_BYTES 128
 
 /* Number of visible GPUs (>= 0), or -EIO. */
@@ -425,17 +456,44 @@ int pptk_rx_device_count(void);
 int pptk_rx_comm_uid(uint8_t uid[PPTK_RX_COMM_UID_BYTES]);
 
 /* Join `ctx` (one context per GPU) to communicator `uid` as rank `rank` of
- * `nranks`.  Collective: blocks until every rank has called it.  -EINVAL if
- * the context already has a communicator. */
+ * `nranks`.  Collective: blocks until every rank has called it, at most
+ * opts.comm_timeout_ms (then -ETIMEDOUT and the context has no
+ * communicator, so it may try again with a new uid).  -EINVAL if the
+ * context already has a communicator. */
 int pptk_rx_comm_create(struct pptk_rx_ctx *ctx, int nranks, int rank,
                         const uint8_t uid[PPTK_RX_COMM_UID_BYTES]);
 
 /* Single process, one thread per GPU: one communicator over ctxs[0..n)
  * (each on a different device), rank i = ctxs[i].  Call from one thread;
- * afterwards each rx thread uses its own context concurrently. */
+ * afterwards each rx thread uses its own context concurrently.  Bounded by
+ * ctxs[0]'s opts.comm_timeout_ms; on any failure no context keeps one. */
 int pptk_rx_comm_create_all(struct pptk_rx_ctx *const *ctxs, int n);
 
+/* Orderly teardown (flushes enqueued gathers, bounded; an abort if the
+ * flush does not finish).  The context may then create a new one. */
 int pptk_rx_comm_destroy(struct pptk_rx_ctx *ctx);
+
+/* Cancel the context's communicator now, from any thread: RCCL's kernels
+ * of pending gathers return (so their streams drain, with wrong gathered
+ * data), waits in pptk_rx_comm_sync / pptk_rx_allgather_hash on it return
+ * -ECANCELED, and so does every later call on it until
+ * pptk_rx_comm_destroy.  An rx thread that fails calls this on every
+ * context of the job, so no sibling waits for a gather it will never join
+ * (examples/rx_multigpu.c).  -EINVAL without a communicator (also while
+ * the context's pptk_rx_comm_create is still running: that call ends at its
+ * own deadline).  It must not race with pptk_rx_comm_destroy or
+ * pptk_rx_ctx_destroy of the same context. */
+int pptk_rx_comm_abort(struct pptk_rx_ctx *ctx);
+
+/* Wait until everything enqueued on `stream` (gathers included) is done,
+ * for at most timeout_ms (0 = opts.comm_timeout_ms), watching the
+ * communicator for RCCL's asynchronous errors.  0: done.  -ETIMEDOUT: the
+ * deadline passed (a peer never issued its part); -EIO: RCCL reported an
+ * error (a peer died); in both cases the communicator is aborted, so the
+ * stream drains.  -ECANCELED: it was aborted (pptk_rx_comm_abort).  Use it
+ * instead of hipStreamSynchronize on a stream that carries gathers.
+ * Without a communicator: a bounded stream wait (-ETIMEDOUT). */
+int pptk_rx_comm_sync(struct pptk_rx_ctx *ctx, void *stream, uint32_t timeout_ms);
 
 /* The context's communicator size and rank; -EINVAL without one. */
 int pptk_rx_comm_info(const struct pptk_rx_ctx *ctx, int *nranks, int *rank);
@@ -451,7 +509,11 @@ void pptk_rx_shard_range(uint64_t n, int nranks, int rank, uint64_t *first, uint
 /* d_out[r * n + i] = d_hash[i] of rank r, for every rank r (n u64 per rank,
  * the same n on every rank; d_hash may be d_out + rank * n).  Asynchronous
  * on `stream`; collective: every rank calls it, in the same order relative
- * to its other collectives. */
+ * to its other collectives.  -EIO if an earlier gather failed
+ * asynchronously, -ECANCELED on an aborted communicator, -ETIMEDOUT (and
+ * the communicator aborted) if RCCL's enqueue -- the connection setup with
+ * the peers at the first gather -- does not finish in opts.comm_timeout_ms.
+ * Completion: pptk_rx_comm_sync. */
 int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint64_t n,
                            uint64_t *d_out, void *stream);
 

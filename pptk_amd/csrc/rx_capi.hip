@@ -155,9 +155,12 @@ struct pptk_rx_ctx {
   pptk_rx_opts opts{};
   RxKArgs tmpl{};      // key/iphash part of the kernel arguments
   void *d_zero = nullptr;  // 64 zeroed device bytes (RxKArgs::zero)
-  uint64_t *d_txside = nullptr;   // two-pass tx: 8 B per frame (grown on demand)
-  uint64_t txside_n = 0;
-  bool txside_owned = true;       // false: the caller's (pptk_tx_set_side_buffer)
+  // two-pass tx side arrays (8 B per frame): per call from this stream-
+  // ordered pool (allocated and freed on the call's stream, so concurrent
+  // tx calls on different streams never share one), or the caller's buffer
+  hipMemPool_t txpool = nullptr;
+  uint64_t *d_txuser = nullptr;   // pptk_tx_set_side_buffer
+  uint64_t txuser_n = 0;
   int ncu = 256;
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
@@ -173,12 +176,17 @@ struct pptk_rx_ctx {
   int async_n = 0;     // outstanding submissions (0..PPTK_RX_MAX_INFLIGHT)
   std::vector<RxRing> rings;
   WorkerPool *pool = nullptr;   // started by the first host batch
-  void *comm = nullptr;         // RCCL communicator (rx_comm.hip), or null
+  // RCCL communicator (rx_comm.hip), or null; atomic: pptk_rx_comm_abort
+  // may read it from another rx thread while this one creates it
+  std::atomic<void *> comm{nullptr};
 };
 
 namespace pptk {
 int ctx_device(const pptk_rx_ctx *c) { return c->device; }
-void **ctx_comm_slot(pptk_rx_ctx *c) { return &c->comm; }
+std::atomic<void *> *ctx_comm_slot(pptk_rx_ctx *c) { return &c->comm; }
+uint32_t ctx_comm_timeout_ms(const pptk_rx_ctx *c) {
+  return c->opts.comm_timeout_ms ? c->opts.comm_timeout_ms : PPTK_RX_COMM_TIMEOUT_MS;
+}
 }  // namespace pptk
 
 static int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
@@ -190,6 +198,14 @@ static long env_long(const char *name, long dflt) {
   const char *e = getenv(name);
   return e ? atol(e) : dflt;
 }
+
+// An A/B knob: read from the environment in experiment builds only
+// (rx_internal.h kDiag); a product build uses the default.
+#ifdef PPTK_RX_EXPERIMENTS
+#define EXP_KNOB(name, dflt) env_long(name, dflt)
+#else
+#define EXP_KNOB(name, dflt) ((long)(dflt))
+#endif
 
 static uint64_t le64(const uint8_t *p) {
   uint64_t v = 0;
@@ -209,6 +225,7 @@ void pptk_rx_opts_default(struct pptk_rx_opts *o) {
   o->iphash_size = 1;
   o->max_batch = 8192;
   o->max_frame = 9216;
+  o->comm_timeout_ms = PPTK_RX_COMM_TIMEOUT_MS;
 }
 
 int pptk_rx_ctx_create(struct pptk_rx_ctx **out, const struct pptk_rx_opts *opts) {
@@ -289,7 +306,10 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
   free_staging(c);
   delete c->pool;
   (void)hipFree(c->d_zero);
-  if (c->txside_owned) (void)hipFree(c->d_txside);
+  if (c->txpool) {   // its frees are queued on the callers' streams
+    (void)hipDeviceSynchronize();
+    (void)hipMemPoolDestroy(c->txpool);
+  }
   for (const RxRing &r : c->rings) (void)hipHostUnregister(r.host);
   delete c;
 }
@@ -342,11 +362,11 @@ static int forced_variant(const pptk_rx_ctx *c) {
 static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n) {
   const uint64_t ntiles = (n + 63) / 64;
   const uint64_t want_blocks = (ntiles + 3) / 4;
-  static const long grid_mult = std::max(1l, env_long("PPTK_RX_GRID_MULT", 1));
+  static const long grid_mult = std::max(1l, EXP_KNOB("PPTK_RX_GRID_MULT", 1));
   // PPTK_RX_RESERVE_CUS: leave that many CUs' worth of resident blocks
   // free, so a concurrent kernel (an RCCL collective overlapping the batch)
   // finds room on the chip instead of waiting for the persistent grid.
-  static const int reserve = (int)std::max(0l, env_long("PPTK_RX_RESERVE_CUS", 0));
+  static const int reserve = (int)std::max(0l, EXP_KNOB("PPTK_RX_RESERVE_CUS", 0));
   const uint64_t ncu = (uint64_t)std::max(1, c->ncu - std::min(reserve, c->ncu - 1));
   const uint64_t cap = ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, cap));
@@ -384,6 +404,7 @@ static RxKArgs batch_args(const pptk_rx_ctx *c, const pptk_rx_dev_batch *b) {
   a.recs32 = b->d_recs32;
   a.hash = b->d_hash;
   a.frag = b->d_frag;
+  a.key = b->d_key;
   return a;
 }
 
@@ -581,7 +602,7 @@ int pptk_rx_place_records(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch 
 // PPTK_TX_TWO_PASS=0: the fields are stored in place by the streaming pass
 // (A/B).
 static bool tx_two_pass() {
-  static const long v = env_long("PPTK_TX_TWO_PASS", 1);
+  static const long v = EXP_KNOB("PPTK_TX_TWO_PASS", 1);
   return v != 0;
 }
 
@@ -638,18 +659,29 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
     // fields stored beside it cost less than the second pass.
     if (c->forced_flags < 0)
       a.tune = pick_tune(c, variant, false);
-    if (c->txside_n < n) {
-      uint64_t *p = nullptr;
-      if (hipMalloc((void **)&p, n * 8) != hipSuccess) return -ENOMEM;
-      if (c->txside_owned)
-        (void)hipFree(c->d_txside);   // (synchronous: earlier tx batches are done with it)
-      c->d_txside = p;
-      c->txside_n = n;
-      c->txside_owned = true;
+    uint64_t *side = c->d_txuser && c->txuser_n >= n ? c->d_txuser : nullptr;
+    const bool pooled = side == nullptr;
+    if (pooled) {   // stream-ordered: this call's own array, freed behind it
+      if (!c->txpool) {
+        hipMemPoolProps pp;
+        memset(&pp, 0, sizeof(pp));
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = c->device;
+        if (hipMemPoolCreate(&c->txpool, &pp) != hipSuccess) {
+          c->txpool = nullptr;
+          return -ENOMEM;
+        }
+        uint64_t keep = UINT64_MAX;   // keep freed blocks for the next call
+        (void)hipMemPoolSetAttribute(c->txpool, hipMemPoolAttrReleaseThreshold, &keep);
+      }
+      if (hipMallocFromPoolAsync((void **)&side, n * 8, c->txpool, s) != hipSuccess)
+        return -ENOMEM;
     }
-    a.txside = c->d_txside;
+    a.txside = side;
     hipError_t e = launch_rx(variant, a, grid_for(c, variant, n), s);
-    if (e == hipSuccess) e = launch_tx_apply(c->d_txside, d_frames, d_off, stride, n, s);
+    if (e == hipSuccess) e = launch_tx_apply(side, d_frames, d_off, stride, n, s);
+    if (pooled && hipFreeAsync(side, s) != hipSuccess && e == hipSuccess) e = hipErrorUnknown;
     return hip_err(e);
   }
   return hip_err(launch_rx(variant, a, grid_for(c, variant, n), s));
@@ -659,10 +691,8 @@ int pptk_tx_set_side_buffer(struct pptk_rx_ctx *c, void *d_side, uint64_t frames
   if (!c || (!d_side && frames) || ((uintptr_t)d_side & 7u)) return -EINVAL;
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
-  if (c->txside_owned) (void)hipFree(c->d_txside);
-  c->d_txside = (uint64_t *)d_side;
-  c->txside_n = d_side ? frames : 0;
-  c->txside_owned = d_side == nullptr;
+  c->d_txuser = (uint64_t *)d_side;
+  c->txuser_n = d_side ? frames : 0;
   return 0;
 }
 
@@ -727,7 +757,11 @@ static const BinBounds &bin_bounds() {
   static const BinBounds bb = [] {
     BinBounds r;
     for (int k = 0; k < kGroups - 1; ++k) r.b[k] = kGroupMaxLen[k];
+#ifdef PPTK_RX_EXPERIMENTS
     const char *e = getenv("PPTK_RX_BIN_BOUNDS");
+#else
+    const char *e = nullptr;
+#endif
     if (!e) return r;
     BinBounds t = r;
     for (int k = 0; k < kGroups - 1; ++k) {
@@ -807,22 +841,23 @@ size_t pptk_rx_permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
   return permit_scratch_bytes(n, hash_size);
 }
 
-int pptk_rx_permit_device(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs,
-                          const struct pptk_rx_rec32 *d_recs32, uint64_t n, int family,
-                          const uint8_t *d_subject, uint32_t *d_tokens, uint8_t *d_verdict,
-                          void *d_scratch, void *stream) {
+static int permit_common(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs,
+                         const struct pptk_rx_rec32 *d_recs32, const uint32_t *d_keys,
+                         uint64_t n, int family, const uint8_t *d_subject, uint32_t *d_tokens,
+                         uint8_t *d_verdict, void *d_scratch, void *stream) {
   if (!c || (family != 4 && family != 6) || n > 0xffffffffull) return -EINVAL;
   if ((family == 4 && !c->opts.iphash_bits4) || (family == 6 && !c->opts.iphash_bits6))
     return -EINVAL;   // the records carry no bucket for that family
   const uint32_t hs = c->opts.iphash_size;
   if (hs == 0 || (hs & (hs - 1))) return -EINVAL;
   if (n == 0) return 0;
-  if ((!d_recs && !d_recs32) || !d_tokens || !d_verdict || !d_scratch) return -EINVAL;
+  if ((!d_recs && !d_recs32 && !d_keys) || !d_tokens || !d_verdict || !d_scratch) return -EINVAL;
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   PermitArgs a{};
-  a.recs = d_recs32 ? nullptr : d_recs;
-  a.recs32 = d_recs32;
+  a.recs = d_recs32 || d_keys ? nullptr : d_recs;
+  a.recs32 = d_keys ? nullptr : d_recs32;
+  a.keys_in = d_keys;
   a.n = n;
   a.subject = d_subject;
   a.tokens = d_tokens;
@@ -830,6 +865,23 @@ int pptk_rx_permit_device(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_rec
   a.hash_size = hs;
   a.family = family;
   return hip_err(launch_permit(a, d_scratch, (hipStream_t)stream));
+}
+
+int pptk_rx_permit_device(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs,
+                          const struct pptk_rx_rec32 *d_recs32, uint64_t n, int family,
+                          const uint8_t *d_subject, uint32_t *d_tokens, uint8_t *d_verdict,
+                          void *d_scratch, void *stream) {
+  if (!d_recs && !d_recs32) return -EINVAL;
+  return permit_common(c, d_recs, d_recs32, nullptr, n, family, d_subject, d_tokens, d_verdict,
+                       d_scratch, stream);
+}
+
+int pptk_rx_permit_keys_device(struct pptk_rx_ctx *c, const uint32_t *d_keys, uint64_t n,
+                               int family, const uint8_t *d_subject, uint32_t *d_tokens,
+                               uint8_t *d_verdict, void *d_scratch, void *stream) {
+  if (!d_keys && n) return -EINVAL;
+  return permit_common(c, nullptr, nullptr, d_keys, n, family, d_subject, d_tokens, d_verdict,
+                       d_scratch, stream);
 }
 
 int pptk_rx_tokens_refill_device(struct pptk_rx_ctx *c, uint32_t *d_tokens, uint32_t start,
@@ -923,7 +975,7 @@ static size_t direct_max_bytes() {
 // per 65 536-frame chunk beside its 2.2 ms frame copy (DESIGN.md
 // "End-to-end").  PPTK_RX_SPLIT=0 restores the copies (A/B).
 static bool split_chunks() {
-  static const long v = env_long("PPTK_RX_SPLIT", 1);
+  static const long v = EXP_KNOB("PPTK_RX_SPLIT", 1);
   return v != 0;
 }
 
@@ -947,7 +999,7 @@ static double ring_dma_density() {
 // up to the next 16-byte boundary are zero (the kernel never uses them).
 // PPTK_RX_NT_GATHER=0: plain memcpy (A/B).
 static bool nt_gather() {
-  static const long v = env_long("PPTK_RX_NT_GATHER", 1);
+  static const long v = EXP_KNOB("PPTK_RX_NT_GATHER", 1);
   return v != 0;
 }
 
@@ -1114,7 +1166,10 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
         const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
         sl.h_off[i] = o;
         d.lo = std::min<size_t>(d.lo, o);
-        d.hi = std::max<size_t>(d.hi, o + ((sz + 15) & ~(size_t)15));
+        // (the frame's chunk-rounded END, clamped to the region: a span
+        // copy must not read past the registered memory; the kernel's reads
+        // past a frame's end stay inside the span's 16-byte slack)
+        d.hi = std::max<size_t>(d.hi, std::min<size_t>((o + sz + 15) & ~(size_t)15, ring->bytes));
         d.fbytes += sz;
       } else if (gather) {
         sl.h_off[i] = pos;

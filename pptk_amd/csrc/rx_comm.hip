@@ -17,27 +17,107 @@
 // multi-queue loops run one thread per queue (reference ldp/ldprecvmt.c:
 // 174-182): pptk_rx_comm_create_all over one context per GPU.
 //
+// Failure containment.  The reference's queue threads share nothing, so one
+// failing thread cannot stall the others; a collective can: a rank that
+// never joins (or dies, or skips a gather) leaves every other rank waiting
+// inside RCCL.  So every wait here is bounded by opts.comm_timeout_ms:
+// creation (init plus a warm-up gather that makes RCCL connect the ring)
+// runs on a helper thread the caller stops waiting for at the deadline
+// (-ETIMEDOUT; bounded_init below says why RCCL's own non-blocking mode is
+// not enough); pptk_rx_comm_sync waits for a stream with the same deadline,
+// surfaces RCCL's asynchronous errors (-EIO) and aborts the communicator on
+// either, which makes RCCL's kernels give up so the stream drains;
+// pptk_rx_comm_abort (any thread) cancels a communicator that other threads
+// may be waiting on (-ECANCELED from then on).
+//
+// RCCL is loaded on first use (dlopen): a single-GPU application never maps
+// the 570 MB library, and a box without it gets -ENOSYS from these entry
+// points only.
+//
 // Errors: 0 or -errno; contract violations -EINVAL before RCCL is called,
 // RCCL argument errors -EINVAL, every other RCCL or HIP failure -EIO.
+#include <dlfcn.h>
 #include <errno.h>
 #include <string.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <new>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
-#include <rccl/rccl.h>
+#include <rccl/rccl.h>   // types and constants only: the functions are dlsym'd
 
 #include "rx_internal.h"
 
 using namespace pptk;
 
+// Experiment builds: PPTK_RX_COMM_TRACE=1 traces the communicator calls.
+#ifdef PPTK_RX_EXPERIMENTS
+#include <stdio.h>
+#include <stdlib.h>
+#define COMM_TRACE(...)                                              \
+  do {                                                               \
+    static const bool on_ = getenv("PPTK_RX_COMM_TRACE") != nullptr; \
+    if (on_) {                                                       \
+      fprintf(stderr, "[pptk comm] " __VA_ARGS__);                   \
+      fputc('\n', stderr);                                           \
+    }                                                                \
+  } while (0)
+#else
+#define COMM_TRACE(...) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace {
 
-struct RxComm {
-  ncclComm_t comm = nullptr;
-  int nranks = 0;
-  int rank = 0;
+// The RCCL entry points used here, resolved once from librccl.so.1.
+struct Rccl {
+  ncclResult_t (*GetUniqueId)(ncclUniqueId *);
+  ncclResult_t (*CommInitRankConfig)(ncclComm_t *, int, ncclUniqueId, int, ncclConfig_t *);
+  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t *);
+  ncclResult_t (*CommFinalize)(ncclComm_t);
+  ncclResult_t (*CommDestroy)(ncclComm_t);
+  ncclResult_t (*CommAbort)(ncclComm_t);
+  ncclResult_t (*GroupStart)(void);
+  ncclResult_t (*GroupEnd)(void);
+  ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
+                            hipStream_t);
+  bool ok;
 };
+
+const Rccl *rccl() {
+  static Rccl r{};
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void *h = nullptr;
+    // the RCCL this library was compiled against first (ncclConfig_t is
+    // versioned), then whatever the process already maps
+    for (const char *name : {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!h) return;
+    bool all = true;
+    auto sym = [&](auto &fp, const char *name) {
+      fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+      all = all && fp != nullptr;
+    };
+    sym(r.GetUniqueId, "ncclGetUniqueId");
+    sym(r.CommInitRankConfig, "ncclCommInitRankConfig");
+    sym(r.CommGetAsyncError, "ncclCommGetAsyncError");
+    sym(r.CommFinalize, "ncclCommFinalize");
+    sym(r.CommDestroy, "ncclCommDestroy");
+    sym(r.CommAbort, "ncclCommAbort");
+    sym(r.GroupStart, "ncclGroupStart");
+    sym(r.GroupEnd, "ncclGroupEnd");
+    sym(r.AllGather, "ncclAllGather");
+    r.ok = all;   // (the handle stays open for the life of the process)
+  });
+  return r.ok ? &r : nullptr;
+}
 
 int nccl_err(ncclResult_t r) {
   if (r == ncclSuccess) return 0;
@@ -45,7 +125,226 @@ int nccl_err(ncclResult_t r) {
   return -EIO;
 }
 
-RxComm *comm_of(const pptk_rx_ctx *c) { return (RxComm *)*ctx_comm_slot((pptk_rx_ctx *)c); }
+using Clock = std::chrono::steady_clock;
+
+struct Deadline {
+  Clock::time_point t;
+  explicit Deadline(uint32_t ms) : t(Clock::now() + std::chrono::milliseconds(ms)) {}
+  bool passed() const { return Clock::now() >= t; }
+};
+
+// Poll back-off: tight for the first millisecond (a gather that is about
+// to finish), then 100 us sleeps.
+struct Backoff {
+  Clock::time_point t0 = Clock::now();
+  void pause() {
+    if (Clock::now() - t0 < std::chrono::milliseconds(1)) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+};
+
+struct RxComm {
+  std::mutex mu;          // guards comm against a concurrent abort
+  ncclComm_t comm = nullptr;
+  int nranks = 0;
+  int rank = 0;
+  bool aborted = false;   // comm is gone (aborted); only the struct remains
+};
+
+RxComm *comm_of(const pptk_rx_ctx *c) {
+  return (RxComm *)ctx_comm_slot((pptk_rx_ctx *)c)->load(std::memory_order_acquire);
+}
+
+void set_comm(pptk_rx_ctx *c, RxComm *m) {
+  ctx_comm_slot(c)->store(m, std::memory_order_release);
+}
+
+// Wait while RCCL reports the communicator's last call in progress; the
+// final state, or ncclInProgress if the deadline passed first.
+ncclResult_t wait_ready(const Rccl *R, ncclComm_t comm, const Deadline &d) {
+  Backoff b;
+  for (;;) {
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t r = R->CommGetAsyncError(comm, &st);
+    if (r != ncclSuccess) return r;
+    if (st != ncclInProgress || d.passed()) return st;
+    b.pause();
+  }
+}
+
+// Abort under the lock, once.
+void abort_locked(const Rccl *R, RxComm *m) {
+  if (m->aborted) return;
+  (void)R->CommAbort(m->comm);
+  m->comm = nullptr;
+  m->aborted = true;
+}
+
+// Orderly teardown of a healthy communicator: finalize (flushes what was
+// enqueued), bounded wait, destroy; abort if the flush does not finish.
+void teardown(const Rccl *R, RxComm *m, uint32_t timeout_ms) {
+  std::lock_guard<std::mutex> g(m->mu);
+  if (m->aborted) return;
+  const Deadline d(timeout_ms);
+  ncclResult_t r = R->CommFinalize(m->comm);
+  if (r == ncclSuccess || r == ncclInProgress) r = wait_ready(R, m->comm, d);
+  if (r == ncclSuccess) {
+    (void)R->CommDestroy(m->comm);
+    m->comm = nullptr;
+    m->aborted = true;
+  } else {
+    abort_locked(R, m);
+  }
+}
+
+ncclConfig_t nonblocking_config() {
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+#ifdef PPTK_RX_EXPERIMENTS
+  if (getenv("PPTK_RX_COMM_BLOCKING")) cfg.blocking = 1;
+#endif
+  return cfg;
+}
+
+// Communicator creation, bounded whatever RCCL does.  The init runs on a
+// helper thread and the caller waits for it until the deadline.  RCCL is
+// meant to return from a non-blocking init at once (ncclConfig_t.blocking =
+// 0, then poll ncclCommGetAsyncError; torch's bundled RCCL 2.26.6 does), but
+// /opt/rocm's RCCL 2.27.7 runs the init synchronously inside
+// ncclCommInitRankConfig, in a group or not (measured: with a rank that never
+// joins the call did not return for 30 s).  So the helper does the whole
+// init -- the call, then the polling of a non-blocking one -- and if the
+// caller gives up first it marks the job abandoned and returns -ETIMEDOUT:
+// the helper aborts whatever it built once RCCL lets it go (at once for a
+// non-blocking init; for one stuck inside RCCL, when the missing rank
+// appears or the process exits).  The job is shared, so either side may
+// finish last.
+struct InitJob {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false, abandoned = false;
+  ncclResult_t r = ncclSuccess;
+  std::vector<ncclComm_t> comms;
+};
+
+void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
+              std::vector<int> devs, std::vector<int> ranks, int nranks) {
+  const size_t k = devs.size();
+  std::vector<ncclComm_t> comms(k, nullptr);
+  std::vector<ncclConfig_t> cfg(k, nonblocking_config());
+  auto going = [](ncclResult_t x) { return x == ncclSuccess || x == ncclInProgress; };
+  ncclResult_t r = k > 1 ? R->GroupStart() : ncclSuccess;   // (ncclCommInitAll's form)
+  for (size_t i = 0; i < k && going(r); ++i) {
+    if (hipSetDevice(devs[i]) != hipSuccess) r = ncclUnhandledCudaError;
+    else r = R->CommInitRankConfig(&comms[i], nranks, id, ranks[i], &cfg[i]);
+  }
+  if (k > 1) {
+    const ncclResult_t re = R->GroupEnd();
+    if (going(r)) r = re;
+  }
+  COMM_TRACE("init job: init calls returned %d", (int)r);
+  // a non-blocking init goes on in RCCL: poll until it is done, or until
+  // the caller has given up
+  Backoff b;
+  for (size_t i = 0; i < k && going(r);) {
+    ncclResult_t st = ncclInProgress;
+    if (!comms[i] || R->CommGetAsyncError(comms[i], &st) != ncclSuccess) st = ncclInternalError;
+    if (st != ncclInProgress) {
+      r = st;
+      ++i;
+      continue;
+    }
+    {
+      std::lock_guard<std::mutex> g(job->mu);
+      if (job->abandoned) break;
+    }
+    b.pause();
+  }
+  // Warm-up gather of one element on every new communicator: RCCL sets
+  // up its ring connections with the peers lazily, at the first collective,
+  // and that setup can block inside ncclAllGather; doing it here puts it
+  // under the same deadline, so the product's gathers only enqueue.
+  if (r == ncclSuccess) {
+    std::vector<hipStream_t> st(k, nullptr);
+    std::vector<uint64_t *> buf(k, nullptr);
+    for (size_t i = 0; i < k && r == ncclSuccess; ++i)
+      if (hipSetDevice(devs[i]) != hipSuccess ||
+          hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess ||
+          hipMalloc((void **)&buf[i], (size_t)nranks * 8) != hipSuccess ||
+          hipMemsetAsync(buf[i], 0, (size_t)nranks * 8, st[i]) != hipSuccess)
+        r = ncclUnhandledCudaError;
+    if (r == ncclSuccess && k > 1) r = R->GroupStart();
+    for (size_t i = 0; i < k && going(r); ++i) {
+      (void)hipSetDevice(devs[i]);
+      r = R->AllGather(buf[i] + ranks[i], buf[i], 1, ncclUint64, comms[i], st[i]);
+    }
+    if (k > 1 && going(r)) r = R->GroupEnd();
+    for (size_t i = 0; i < k && going(r); ++i) {   // enqueued; now let it finish
+      ncclResult_t st2 = ncclInProgress;
+      while (R->CommGetAsyncError(comms[i], &st2) == ncclSuccess && st2 == ncclInProgress)
+        b.pause();
+      r = st2;
+      (void)hipSetDevice(devs[i]);
+      if (r == ncclSuccess && hipStreamSynchronize(st[i]) != hipSuccess)
+        r = ncclUnhandledCudaError;
+    }
+    for (size_t i = 0; i < k; ++i) {
+      (void)hipSetDevice(devs[i]);
+      if (buf[i]) (void)hipFree(buf[i]);
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+    }
+    COMM_TRACE("init job: warm-up gather %d", (int)r);
+  }
+  bool abandoned;
+  {
+    std::lock_guard<std::mutex> g(job->mu);
+    abandoned = job->abandoned;
+    if (!abandoned) {
+      job->r = r;
+      job->comms = comms;
+      job->done = true;
+    }
+  }
+  if (abandoned) {   // the caller returned -ETIMEDOUT: nobody owns these
+    COMM_TRACE("init job: abandoned, aborting");
+    for (size_t i = 0; i < k; ++i)
+      if (comms[i] && hipSetDevice(devs[i]) == hipSuccess) (void)R->CommAbort(comms[i]);
+  } else {
+    job->cv.notify_all();
+  }
+}
+
+// Start the init of ranks[i] on devs[i] (i < devs.size()) of an
+// nranks-rank communicator and wait for it, at most timeout_ms.  0 with
+// comms filled, or -errno with nothing left behind for the caller.
+int bounded_init(const Rccl *R, const ncclUniqueId &id, const std::vector<int> &devs,
+                 const std::vector<int> &ranks, int nranks, uint32_t timeout_ms,
+                 std::vector<ncclComm_t> &comms) {
+  std::shared_ptr<InitJob> job;
+  try {
+    job = std::make_shared<InitJob>();
+    std::thread(init_run, R, job, id, devs, ranks, nranks).detach();
+  } catch (...) {
+    return -EAGAIN;
+  }
+  const auto until = Clock::now() + std::chrono::milliseconds(timeout_ms);
+  std::unique_lock<std::mutex> g(job->mu);
+  if (!job->cv.wait_until(g, until, [&] { return job->done; })) {
+    job->abandoned = true;
+    COMM_TRACE("create: deadline passed, init abandoned");
+    return -ETIMEDOUT;
+  }
+  const ncclResult_t r = job->r;
+  comms = job->comms;
+  g.unlock();
+  if (r == ncclSuccess) return 0;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  for (size_t i = 0; i < comms.size(); ++i)
+    if (comms[i] && hipSetDevice(devs[i]) == hipSuccess) (void)R->CommAbort(comms[i]);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return r == ncclInProgress ? -ETIMEDOUT : nccl_err(r);
+}
 
 }  // namespace
 
@@ -54,9 +353,9 @@ namespace pptk {
 void comm_release(pptk_rx_ctx *c) {
   RxComm *m = comm_of(c);
   if (!m) return;
-  (void)ncclCommDestroy(m->comm);
+  if (const Rccl *R = rccl()) teardown(R, m, ctx_comm_timeout_ms(c));
+  set_comm(c, nullptr);
   delete m;
-  *ctx_comm_slot(c) = nullptr;
 }
 
 }  // namespace pptk
@@ -72,8 +371,10 @@ int pptk_rx_device_count(void) {
 int pptk_rx_comm_uid(uint8_t uid[PPTK_RX_COMM_UID_BYTES]) {
   static_assert(sizeof(ncclUniqueId) == PPTK_RX_COMM_UID_BYTES, "RCCL unique id size");
   if (!uid) return -EINVAL;
+  const Rccl *R = rccl();
+  if (!R) return -ENOSYS;
   ncclUniqueId id;
-  const int rc = nccl_err(ncclGetUniqueId(&id));
+  const int rc = nccl_err(R->GetUniqueId(&id));
   if (rc == 0) memcpy(uid, &id, sizeof(id));
   return rc;
 }
@@ -82,22 +383,24 @@ int pptk_rx_comm_create(struct pptk_rx_ctx *c, int nranks, int rank,
                         const uint8_t uid[PPTK_RX_COMM_UID_BYTES]) {
   if (!c || !uid || nranks < 1 || rank < 0 || rank >= nranks) return -EINVAL;
   if (comm_of(c)) return -EINVAL;   // one communicator per context
+  const Rccl *R = rccl();
+  if (!R) return -ENOSYS;
   RxComm *m = new (std::nothrow) RxComm();
   if (!m) return -ENOMEM;
   ncclUniqueId id;
   memcpy(&id, uid, sizeof(id));
-  int rc;
-  {
-    DeviceScope ds(ctx_device(c));
-    rc = ds.ok ? nccl_err(ncclCommInitRank(&m->comm, nranks, id, rank)) : -EIO;
-  }
+  COMM_TRACE("create: init rank %d of %d", rank, nranks);
+  std::vector<ncclComm_t> comms;
+  const int rc = bounded_init(R, id, {ctx_device(c)}, {rank}, nranks, ctx_comm_timeout_ms(c), comms);
+  COMM_TRACE("create: %d", rc);
+  if (rc == 0) m->comm = comms[0];
   if (rc != 0) {
     delete m;
     return rc;
   }
   m->nranks = nranks;
   m->rank = rank;
-  *ctx_comm_slot(c) = m;
+  set_comm(c, m);
   return 0;
 }
 
@@ -110,26 +413,34 @@ int pptk_rx_comm_create_all(struct pptk_rx_ctx *const *ctxs, int n) {
     for (int k = 0; k < i; ++k)   // one rank per GPU
       if (devs[(size_t)k] == devs[(size_t)i] || ctxs[k] == ctxs[i]) return -EINVAL;
   }
-  std::vector<ncclComm_t> comms((size_t)n, nullptr);
-  int rc;
-  {
-    DeviceScope ds(devs[0]);   // (ncclCommInitAll sets each device itself)
-    rc = nccl_err(ncclCommInitAll(comms.data(), n, devs.data()));
-  }
+  const Rccl *R = rccl();
+  if (!R) return -ENOSYS;
+  ncclUniqueId id;
+  int rc = nccl_err(R->GetUniqueId(&id));
   if (rc != 0) return rc;
-  for (int i = 0; i < n; ++i) {
-    RxComm *m = new (std::nothrow) RxComm();
-    if (!m) {
-      for (int k = 0; k < n; ++k) {
-        if (k < i) comm_release(ctxs[k]);
-        else (void)ncclCommDestroy(comms[(size_t)k]);
-      }
-      return -ENOMEM;
+  // one group of per-device inits (what ncclCommInitAll does), bounded
+  std::vector<int> ranks((size_t)n);
+  for (int i = 0; i < n; ++i) ranks[(size_t)i] = i;
+  std::vector<ncclComm_t> comms;
+  rc = bounded_init(R, id, devs, ranks, n, ctx_comm_timeout_ms(ctxs[0]), comms);
+  if (rc != 0) return rc;
+  std::vector<RxComm *> ms((size_t)n, nullptr);
+  for (int i = 0; i < n && rc == 0; ++i)
+    if (!(ms[(size_t)i] = new (std::nothrow) RxComm())) rc = -ENOMEM;
+  if (rc != 0) {
+    for (int i = 0; i < n; ++i) {
+      DeviceScope ds(devs[(size_t)i]);
+      (void)R->CommAbort(comms[(size_t)i]);
+      delete ms[(size_t)i];
     }
+    return rc;
+  }
+  for (int i = 0; i < n; ++i) {
+    RxComm *m = ms[(size_t)i];
     m->comm = comms[(size_t)i];
     m->nranks = n;
     m->rank = i;
-    *ctx_comm_slot(ctxs[i]) = m;
+    set_comm(ctxs[i], m);
   }
   return 0;
 }
@@ -138,6 +449,18 @@ int pptk_rx_comm_destroy(struct pptk_rx_ctx *c) {
   if (!c) return -EINVAL;
   DeviceScope ds(ctx_device(c));
   comm_release(c);
+  return 0;
+}
+
+int pptk_rx_comm_abort(struct pptk_rx_ctx *c) {
+  if (!c) return -EINVAL;
+  RxComm *m = comm_of(c);
+  if (!m) return -EINVAL;
+  const Rccl *R = rccl();
+  if (!R) return -ENOSYS;
+  DeviceScope ds(ctx_device(c));
+  std::lock_guard<std::mutex> g(m->mu);
+  abort_locked(R, m);
   return 0;
 }
 
@@ -171,10 +494,98 @@ int pptk_rx_allgather_hash(struct pptk_rx_ctx *c, const uint64_t *d_hash, uint64
   if (!m) return -EINVAL;
   if (n == 0) return 0;
   if (!d_hash || !d_out) return -EINVAL;
+  const Rccl *R = rccl();
+  if (!R) return -ENOSYS;
   DeviceScope ds(ctx_device(c));
   if (!ds.ok) return -EIO;
-  return nccl_err(ncclAllGather(d_hash, d_out, (size_t)n, ncclUint64, m->comm,
-                                (hipStream_t)stream));
+  const Deadline d(ctx_comm_timeout_ms(c));
+  Backoff b;
+  std::unique_lock<std::mutex> g(m->mu);
+  if (m->aborted) return -ECANCELED;
+  ncclResult_t st = ncclSuccess;
+  if (R->CommGetAsyncError(m->comm, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
+    return -EIO;   // an earlier collective failed: sync/abort, then a new communicator
+  ncclResult_t r = R->AllGather(d_hash, d_out, (size_t)n, ncclUint64, m->comm, (hipStream_t)stream);
+  // A non-blocking communicator may return while the enqueue (e.g. RCCL's
+  // lazy connection setup with the peers at the first collective) goes on;
+  // the call is complete once the state leaves ncclInProgress.  The lock is
+  // dropped between polls so pptk_rx_comm_abort can cancel the wait.
+  while (r == ncclInProgress) {
+    ncclResult_t now = ncclInProgress;
+    if (R->CommGetAsyncError(m->comm, &now) != ncclSuccess) return -EIO;
+    r = now;
+    if (r != ncclInProgress) break;
+    if (d.passed()) {
+      abort_locked(R, m);
+      return -ETIMEDOUT;
+    }
+    g.unlock();
+    b.pause();
+    g.lock();
+    if (m->aborted) return -ECANCELED;
+  }
+  return nccl_err(r);
+}
+
+int pptk_rx_comm_sync(struct pptk_rx_ctx *c, void *stream, uint32_t timeout_ms) {
+  if (!c) return -EINVAL;
+  RxComm *m = comm_of(c);
+  const Rccl *R = m ? rccl() : nullptr;
+  DeviceScope ds(ctx_device(c));
+  if (!ds.ok) return -EIO;
+  const hipStream_t s = (hipStream_t)stream;
+  const Deadline d(timeout_ms ? timeout_ms : ctx_comm_timeout_ms(c));
+  Backoff b;
+  int rc = 0;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) return -EIO;
+    if (m && R) {
+      std::lock_guard<std::mutex> g(m->mu);
+      if (m->aborted) {
+        rc = -ECANCELED;
+        break;
+      }
+      ncclResult_t st = ncclSuccess;
+      if (R->CommGetAsyncError(m->comm, &st) != ncclSuccess ||
+          (st != ncclSuccess && st != ncclInProgress)) {
+        abort_locked(R, m);
+        rc = -EIO;
+        break;
+      }
+      if (d.passed()) {
+        abort_locked(R, m);
+        rc = -ETIMEDOUT;
+        break;
+      }
+    } else if (d.passed()) {
+      return -ETIMEDOUT;   // no communicator to cancel: the stream is just slow
+    }
+    b.pause();
+  }
+  if (rc == 0) {
+    if (m && R) {   // an error reported after the last kernel finished
+      std::lock_guard<std::mutex> g(m->mu);
+      ncclResult_t st = ncclSuccess;
+      if (!m->aborted && (R->CommGetAsyncError(m->comm, &st) != ncclSuccess ||
+                          (st != ncclSuccess && st != ncclInProgress))) {
+        abort_locked(R, m);
+        return -EIO;
+      }
+    }
+    return 0;
+  }
+  // Aborted: RCCL's kernels see the abort flag and return, so the stream
+  // drains; wait for that (bounded: this call must not become the hang).
+  const Deadline drain(10000);
+  Backoff b2;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q != hipErrorNotReady || drain.passed()) break;
+    b2.pause();
+  }
+  return rc;
 }
 
 }  // extern "C"

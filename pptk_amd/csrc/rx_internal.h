@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/pptk_rx.h"
 
 namespace pptk {
@@ -28,8 +30,21 @@ struct DeviceScope {
 
 // Context internals shared with the multi-GPU module (rx_comm.hip).
 int ctx_device(const pptk_rx_ctx *c);
-void **ctx_comm_slot(pptk_rx_ctx *c);
+std::atomic<void *> *ctx_comm_slot(pptk_rx_ctx *c);
+uint32_t ctx_comm_timeout_ms(const pptk_rx_ctx *c);   // opts.comm_timeout_ms (0 -> default)
 void comm_release(pptk_rx_ctx *c);   // destroys the context's communicator, if any
+
+// Diagnostic tune bits (RxKArgs::tune 3, 4, 7, 9: skip record stores, the
+// per-frame phase, half the record bytes, the tx writes -- output invalid,
+// for profiling) and the A/B environment knobs of the host code exist only
+// in experiment builds (`make abvariant NAME=exp DEFS=-DPPTK_RX_EXPERIMENTS`):
+// in the product library the branches are compiled out and the knobs are
+// constants (INTEGRATION.md section 6 lists the knobs a product build reads).
+#if defined(PPTK_RX_EXPERIMENTS) || defined(PPTK_RX_DIAG)
+constexpr bool kDiag = true;
+#else
+constexpr bool kDiag = false;
+#endif
 
 // Kernel arguments (by value; a handful of SGPRs).
 struct RxKArgs {
@@ -43,6 +58,7 @@ struct RxKArgs {
   pptk_rx_rec32 *recs32; // nullable: compact records instead of recs
   uint64_t *hash;        // nullable
   pptk_rx_frag *frag;    // nullable: fragment side records
+  uint32_t *key;         // nullable: dense rate-limiter keys (pptk_rx_dev_batch.d_key)
   uint64_t k0, k1;       // SipHash key words (LE loads of key[0..7], key[8..15])
   uint64_t mask6_0, mask6_1;  // ipv6_permitted prefix mask over the 16 address bytes
   uint32_t mask4;        // ip_permitted prefix mask (host order)
@@ -140,6 +156,7 @@ uint16_t *bin_desc_len(void *scratch, int grid, uint64_t n);
 struct PermitArgs {
   const pptk_rx_rec *recs;      // one of recs / recs32
   const pptk_rx_rec32 *recs32;
+  const uint32_t *keys_in;      // or the rx kernel's dense keys (pptk_rx_dev_batch.d_key)
   uint64_t n;
   const uint8_t *subject;       // nullable: every parsed frame of the family
   uint32_t *tokens;             // hash_size counters

@@ -643,7 +643,7 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
     }
     if (a.txside)
       o.tx = tx_entry(txp, txv);
-    else if (a.frames_w && !(a.tune & 512u))   // bit 9: diagnostics, no tx writes
+    else if (a.frames_w && !(kDiag && (a.tune & 512u)))   // bit 9: diagnostics, no tx writes
       tx_store(a, base, txp, txv);
     uint32_t bucket = 0;
     if (a.recs || a.recs32 || a.hash) {   // tx batches need no hashes
@@ -769,6 +769,10 @@ __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, 
   const uint32_t *w = o.w;
   if (a.hash)
     a.hash[idx] = o.fh;
+  if (a.key)   // rate-limiter key: src_bucket (word 14), IPv6 bit 31; ~0 unparsed
+    a.key[idx] = !(o.flags & PPTK_RX_F_PARSED) ? 0xffffffffu
+                 : (o.flags & PPTK_RX_F_IPV6)  ? (w[14] | 0x80000000u)
+                                               : w[14];
   if (a.frag)
     ((GLB_AS u32x4 *)a.frag)[idx] = o.frag;
   if (!a.recs && !a.recs32)
@@ -810,9 +814,6 @@ __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, 
 // lane's frame index (~0: no record).
 __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uint8_t *wimg, uint64_t tile,
                                               int lane, uint32_t my_idx, bool scatter) {
-#ifdef PPTK_RX_EXP_NO_FLUSH
-  return;
-#endif
   const bool c32 = a.recs32 != nullptr;
   __builtin_amdgcn_wave_barrier();
   const LDS_AS u32x4 *st = (const LDS_AS u32x4 *)wimg;
@@ -821,7 +822,7 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
   const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
   const int lg = c32 ? 1 : 2;                 // log2 16-byte pieces per record
   int kmax = c32 ? 2 : 4;
-  if (a.tune & 128u) kmax >>= 1;              // bit 7: diagnostics, half the bytes
+  if (kDiag && (a.tune & 128u)) kmax >>= 1;   // bit 7: diagnostics, half the bytes
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int e = k * WAVE + lane;   // 16-byte piece e of the tile's records
@@ -1006,7 +1007,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     const bool stage = !(a.tune & 2u);
     const bool scatter = GATHER && a.perm;
     // tune bit 4 (diagnostics only, output invalid): skip the lane phase
-    if (dc.idx != 0xffffffffu && !(a.tune & 16u)) {
+    if (dc.idx != 0xffffffffu && !(kDiag && (a.tune & 16u))) {
       const int m = (int)(dc.base & 15);
       if (UNROLL) {  // unrolled variants: chunks past the staged S*T, summed here (rare)
         const int ma = (int)(dc.base & ALM);
@@ -1028,7 +1029,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
       // program order) for the coalesced store below
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
     }
-    if (stage && !(a.tune & 8u) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
+    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
       flush_records(a, wimg, tile, lane, dc.idx, scatter);
     tile += step;
     dc = dn;
@@ -1064,7 +1065,7 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
                                           const u32x4 c[4], LDS_AS uint8_t *wimg) {
   const uint64_t i = tile * WAVE + lane;
   LDS_AS uint8_t *slot = wimg + lane * LSLOT;
-  if (i < a.n && !(a.tune & 16u)) {
+  if (i < a.n && !(kDiag && (a.tune & 16u))) {
     const uint32_t len = a.fixed_len;
     uint32_t d[16];
 #pragma unroll
@@ -1091,7 +1092,7 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
     }
     emit_record(a, o, (uint32_t)i, (LDS_AS u32x4 *)slot, true);
   }
-  if (!(a.tune & 8u) && (a.recs || a.recs32))
+  if (!(kDiag && (a.tune & 8u)) && (a.recs || a.recs32))
     flush_records(a, wimg, tile, lane, 0u, false);
 }
 

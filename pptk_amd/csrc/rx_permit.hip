@@ -27,7 +27,30 @@
 // array shared by all eight XCDs -- made step 1 take 0.72 of the batch's
 // 1.37 ms; the bounds pass reads the 64 MB of sorted keys once.)
 // Bucket values come from the records the rx kernel wrote (src_bucket, the
-// reference's own hash of the masked source, iphash/iphash.c:157-162).
+// reference's own hash of the masked source, iphash/iphash.c:157-162), or
+// from the dense per-frame key array it can write beside them
+// (pptk_rx_dev_batch.d_key: 4 bytes per frame instead of a 16-byte slice of
+// each 64-byte record, whose read costs the DRAM the whole 64-byte burst).
+//
+// That sort is the fallback (hash_size > 2^16).  The main path needs no sort,
+// because the verdict of a frame only depends on whether its rank passes
+// T_b, and that is decided per BLOCK of frames for all but one block per
+// bucket:
+//   H. histogram: block c of HB = 65535 consecutive frames counts its
+//      subject frames per bucket in LDS (u16 pairs, 128 KB for 2^16
+//      buckets) and writes the row bh[c][*]; it also writes each frame's
+//      subject key (bucket, or ~0) densely for the later passes;
+//   S. per bucket, down the column: count_b, and the block c* holding the
+//      T_b-th frame and the rank need_b of that frame inside c*; lim[b] =
+//      "all" when count_b <= T_b, 0 when T_b == 0, else pending; T_b -=
+//      min(T_b, count_b);
+//   R. only blocks that are some bucket's c* (none when no bucket runs out
+//      of tokens): walk the block's frames in order (staged through LDS,
+//      one wave ranks them with ballots, LDS counters per bucket) and set
+//      lim[b] = index of the need_b-th frame of b + 1;
+//   V. verdicts in frame order from the dense keys and lim[].
+// 16 M frames, 2^16 buckets: the histogram table is 32 MB, the passes read
+// the keys twice -- no 64 MB x (2 passes x 3 arrays) radix sort.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -61,15 +84,162 @@ __device__ __forceinline__ void rec_fields(const PermitArgs &a, uint64_t i, uint
   }
 }
 
+// The bucket of frame i if it is a subject of this call, else NOSUBJ:
+// from the record, or from the rx kernel's dense key (bucket of a parsed
+// IPv4 frame; bucket | 0x80000000 of a parsed IPv6 frame; ~0 otherwise).
+constexpr uint32_t NOSUBJ = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t subject_key(const PermitArgs &a, uint64_t i) {
+  bool subj;
+  uint32_t bucket;
+  if (a.keys_in) {
+    const uint32_t k = a.keys_in[i];
+    subj = k != NOSUBJ && ((k >> 31) == (a.family == 6 ? 1u : 0u));
+    bucket = k & 0x7fffffffu;
+  } else {
+    uint32_t flags;
+    rec_fields(a, i, flags, bucket);
+    const bool v6 = flags & PPTK_RX_F_IPV6;
+    subj = (flags & PPTK_RX_F_PARSED) && (a.family == 6 ? v6 : !v6);
+  }
+  if (a.subject) subj = subj && a.subject[i];
+  return subj ? bucket : NOSUBJ;
+}
+
+// (sort fallback: non-subjects get key hash_size, sorted last)
 __global__ __launch_bounds__(PT) void permit_keys(PermitArgs a, uint32_t *keys) {
   const uint64_t i = (uint64_t)blockIdx.x * PT + threadIdx.x;
   if (i >= a.n) return;
-  uint32_t flags, bucket;
-  rec_fields(a, i, flags, bucket);
-  const bool v6 = flags & PPTK_RX_F_IPV6;
-  bool subj = (flags & PPTK_RX_F_PARSED) && (a.family == 6 ? v6 : !v6);
-  if (a.subject) subj = subj && a.subject[i];
-  keys[i] = subj ? bucket : a.hash_size;   // (verdict 2, written by permit_verdicts)
+  const uint32_t k = subject_key(a, i);
+  keys[i] = k == NOSUBJ ? a.hash_size : k;   // (verdict 2, written by permit_verdicts)
+}
+
+// ---- the sort-free path (hash_size <= 2^16) ------------------------------
+constexpr uint32_t HB = 65535;       // frames per histogram block (u16 counts)
+constexpr int HT = 1024;             // threads of the histogram / resolve blocks
+constexpr uint32_t HMAX = 1u << 16;  // largest hash_size of the sort-free path
+constexpr uint32_t LIM_ALL = 0xffffffffu;
+constexpr uint32_t NOBLK = 0xffffffffu;
+constexpr int RCH = 2048;            // frames staged per resolve chunk
+
+__device__ __forceinline__ uint32_t hwords(uint32_t hash_size) { return (hash_size + 1) / 2; }
+
+// H: per-block histogram (u16 pairs in LDS, one word = buckets 2w, 2w + 1)
+// and the dense subject keys
+__global__ __launch_bounds__(HT) void permit_hist(PermitArgs a, uint32_t *ckey, uint32_t *bh,
+                                                  uint32_t *blk_flag) {
+  __shared__ uint32_t h[HMAX / 2];
+  const uint32_t words = hwords(a.hash_size);
+  for (uint32_t w = threadIdx.x; w < words; w += HT) h[w] = 0;
+  if (threadIdx.x == 0) blk_flag[blockIdx.x] = 0;
+  __syncthreads();
+  const uint64_t lo = (uint64_t)blockIdx.x * HB;
+  const uint64_t hi = min(lo + HB, a.n);
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += HT) {
+    const uint32_t k = subject_key(a, i);
+    ckey[i] = k;
+    if (k != NOSUBJ) atomicAdd(&h[k >> 1], 1u << ((k & 1u) * 16u));
+  }
+  __syncthreads();
+  uint32_t *row = bh + (uint64_t)blockIdx.x * words;
+  for (uint32_t w = threadIdx.x; w < words; w += HT) row[w] = h[w];
+}
+
+// S: one thread per bucket, down its column of the histogram table
+__global__ __launch_bounds__(PT) void permit_scan(PermitArgs a, const uint32_t *bh, uint32_t nblk,
+                                                  uint32_t *lim, uint32_t *need, uint32_t *pend,
+                                                  uint32_t *blk_flag) {
+  const uint32_t b = blockIdx.x * PT + threadIdx.x;
+  if (b >= a.hash_size) return;
+  const uint16_t *col = (const uint16_t *)bh + b;
+  const uint64_t pitch = 2ull * hwords(a.hash_size);   // u16 entries per row
+  const uint32_t t = a.tokens[b];
+  uint32_t acc = 0, cstar = NOBLK, prior = 0;
+  uint32_t c = 0;
+  for (; c + 8 <= nblk; c += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = col[(uint64_t)(c + u) * pitch];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (cstar == NOBLK && acc + v[u] >= t) {
+        cstar = c + u;
+        prior = acc;
+      }
+      acc += v[u];
+    }
+  }
+  for (; c < nblk; ++c) {
+    const uint32_t v = col[(uint64_t)c * pitch];
+    if (cstar == NOBLK && acc + v >= t) {
+      cstar = c;
+      prior = acc;
+    }
+    acc += v;
+  }
+  uint32_t l = LIM_ALL, p = NOBLK;
+  if (acc > t) {
+    if (t == 0) {
+      l = 0;
+    } else {   // the T_b-th frame lies in block cstar: resolved by permit_resolve
+      p = cstar;
+      need[b] = t - prior;
+      blk_flag[cstar] = 1;
+    }
+  }
+  lim[b] = l;
+  pend[b] = p;
+  a.tokens[b] = t > acc ? t - acc : 0u;
+}
+
+// R: the blocks holding some bucket's T_b-th frame walk their frames in
+// order.  All threads stage a chunk's keys (only frames of buckets pending
+// in this block; ~0 else) and their need_b; wave 0 ranks them in frame
+// order: per distinct bucket of a 64-frame step one ballot, the rank base
+// from an LDS counter (u16 pairs), and the lane whose rank reaches need_b
+// sets lim[b].
+__global__ __launch_bounds__(HT) void permit_resolve(PermitArgs a, const uint32_t *ckey,
+                                                     const uint32_t *need, const uint32_t *pend,
+                                                     const uint32_t *blk_flag, uint32_t *lim) {
+  if (blk_flag[blockIdx.x] == 0) return;
+  __shared__ uint32_t cnt[HMAX / 2];
+  __shared__ uint32_t sk[RCH], sn[RCH];
+  const uint32_t words = hwords(a.hash_size);
+  for (uint32_t w = threadIdx.x; w < words; w += HT) cnt[w] = 0;
+  const uint32_t c = blockIdx.x;
+  const uint64_t lo = (uint64_t)c * HB;
+  const uint64_t hi = min(lo + HB, a.n);
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint64_t s0 = lo; s0 < hi; s0 += RCH) {
+    __syncthreads();   // (the walk of the previous chunk is done with sk/sn)
+    for (int j = threadIdx.x; j < RCH; j += HT) {
+      const uint64_t i = s0 + (uint64_t)j;
+      uint32_t k = i < hi ? ckey[i] : NOSUBJ;
+      if (k != NOSUBJ && pend[k] != c) k = NOSUBJ;
+      sk[j] = k;
+      sn[j] = k != NOSUBJ ? need[k] : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      for (int st = 0; st < RCH; st += 64) {
+        const uint32_t k = sk[st + lane];
+        uint64_t todo = __ballot(k != NOSUBJ);
+        while (todo) {
+          const int leader = __ffsll((unsigned long long)todo) - 1;
+          const uint32_t b = __shfl(k, leader);
+          const uint64_t m = __ballot(k == b);
+          const uint32_t sh = (b & 1u) * 16u;
+          const uint32_t base = (cnt[b >> 1] >> sh) & 0xffffu;
+          if (k == b && base + (uint32_t)__popcll(m & lt) + 1u == sn[st + lane])
+            lim[b] = (uint32_t)(s0 + (uint64_t)(st + lane)) + 1u;
+          if (lane == leader)
+            cnt[b >> 1] += (uint32_t)__popcll(m) << sh;   // (one wave: no atomics)
+          todo &= ~m;
+        }
+      }
+    }
+  }
 }
 
 // Run boundaries of the sorted keys: first[b] and end[b] of every bucket
@@ -170,21 +340,12 @@ __global__ __launch_bounds__(PT) void tokens_refill(uint32_t *tokens, uint32_t s
 // records 0.529 ms per batch, against 0.61 with 512 x 16, 0.76 with
 // 256 x 16, 0.67 with 512 x 8, 0.60 with 1024 x 12, 0.57 with 1024 x 16
 // and 0.66 with 1024 x 4 (tools/opbench.py permit).
-// PPTK_RX_PERMIT_SORT (A/B only): 1 = 512 x 16, 2 = 256 x 16, 3 = 512 x 8.
 template <unsigned BS, unsigned IPT>
 using OnesweepConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<BS, IPT>,
                                         rocprim::kernel_config<BS, IPT>, 9,
                                         rocprim::block_radix_rank_algorithm::match>>;
-
-int sort_variant() {
-  static const int v = [] {
-    const char *e = getenv("PPTK_RX_PERMIT_SORT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 
 template <class Cfg>
 hipError_t sort_pairs_cfg(void *tmp, size_t &tb, const uint32_t *keys, uint32_t *skeys,
@@ -197,12 +358,7 @@ hipError_t sort_pairs_cfg(void *tmp, size_t &tb, const uint32_t *keys, uint32_t 
 // (tmp == nullptr: the temporary size of the chosen shape into tb)
 hipError_t sort_pairs(void *tmp, size_t &tb, const uint32_t *keys, uint32_t *skeys,
                       uint32_t *svals, size_t n, unsigned bits, hipStream_t st) {
-  switch (sort_variant()) {
-    case 1: return sort_pairs_cfg<OnesweepConfig<512, 16>>(tmp, tb, keys, skeys, svals, n, bits, st);
-    case 2: return sort_pairs_cfg<OnesweepConfig<256, 16>>(tmp, tb, keys, skeys, svals, n, bits, st);
-    case 3: return sort_pairs_cfg<OnesweepConfig<512, 8>>(tmp, tb, keys, skeys, svals, n, bits, st);
-    default: return sort_pairs_cfg<OnesweepConfig<1024, 8>>(tmp, tb, keys, skeys, svals, n, bits, st);
-  }
+  return sort_pairs_cfg<OnesweepConfig<1024, 8>>(tmp, tb, keys, skeys, svals, n, bits, st);
 }
 
 int key_bits(uint32_t hash_size) {
@@ -212,6 +368,33 @@ int key_bits(uint32_t hash_size) {
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// sort-free path scratch: dense keys, the histogram table, per-bucket lim /
+// need / pend, per-block flags
+struct HistScratch {
+  uint32_t *ckey, *bh, *lim, *need, *pend, *blk_flag;
+  uint32_t nblk;
+  size_t total;
+};
+
+void hist_layout(uint64_t n, uint32_t hash_size, void *base, HistScratch &s) {
+  uint8_t *p = (uint8_t *)base;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    uint8_t *q = p ? p + off : nullptr;
+    off += align256(bytes);
+    return (uint32_t *)q;
+  };
+  s.nblk = (uint32_t)((n + HB - 1) / HB);
+  const size_t words = (hash_size + 1) / 2;
+  s.ckey = take(n * 4);
+  s.bh = take((size_t)s.nblk * words * 4);
+  s.lim = take((size_t)hash_size * 4);
+  s.need = take((size_t)hash_size * 4);
+  s.pend = take((size_t)hash_size * 4);
+  s.blk_flag = take((size_t)s.nblk * 4);
+  s.total = off;
+}
 
 struct PermitScratch {
   uint32_t *keys, *skeys, *svals, *first, *end, *lim;
@@ -248,6 +431,11 @@ unsigned blocks(uint64_t n) { return (unsigned)((n + PT - 1) / PT); }
 }  // namespace
 
 size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
+  if (hash_size <= HMAX) {
+    HistScratch h;
+    hist_layout(n, hash_size, nullptr, h);
+    return h.total;
+  }
   PermitScratch s;
   if (layout(n, hash_size, nullptr, s) != hipSuccess) return 0;
   return s.total;
@@ -255,6 +443,18 @@ size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
 
 hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   if (a.n == 0) return hipSuccess;
+  if (a.hash_size <= HMAX) {
+    HistScratch h;
+    hist_layout(a.n, a.hash_size, scratch, h);
+    hipLaunchKernelGGL(permit_hist, dim3(h.nblk), dim3(HT), 0, st, a, h.ckey, h.bh, h.blk_flag);
+    hipLaunchKernelGGL(permit_scan, dim3(blocks(a.hash_size)), dim3(PT), 0, st, a, h.bh, h.nblk,
+                       h.lim, h.need, h.pend, h.blk_flag);
+    hipLaunchKernelGGL(permit_resolve, dim3(h.nblk), dim3(HT), 0, st, a, h.ckey, h.need, h.pend,
+                       h.blk_flag, h.lim);
+    hipLaunchKernelGGL(permit_verdicts, dim3(blocks((a.n + 3) / 4)), dim3(PT), 0, st, a, h.ckey,
+                       h.lim);
+    return hipGetLastError();
+  }
   PermitScratch s;
   hipError_t e = layout(a.n, a.hash_size, scratch, s);
   if (e != hipSuccess) return e;

@@ -4,6 +4,7 @@ The product is the C-ABI library; this module only marshals torch/numpy
 buffers into it.  There is no Python or CPU fallback: if the library is
 missing, importing this module raises.
 """
+import collections
 import ctypes
 import os
 
@@ -19,7 +20,8 @@ class RxOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("key", ctypes.c_uint8 * 16),
                 ("iphash_bits4", ctypes.c_uint8), ("iphash_bits6", ctypes.c_uint8),
                 ("gather_threads", ctypes.c_uint16), ("iphash_size", ctypes.c_uint32),
-                ("max_batch", ctypes.c_uint32), ("max_frame", ctypes.c_uint32)]
+                ("max_batch", ctypes.c_uint32), ("max_frame", ctypes.c_uint32),
+                ("comm_timeout_ms", ctypes.c_uint32)]
 
 
 class RxDevBatch(ctypes.Structure):
@@ -28,7 +30,8 @@ class RxDevBatch(ctypes.Structure):
                 ("stride", ctypes.c_uint64), ("fixed_len", ctypes.c_uint32),
                 ("max_len", ctypes.c_uint32), ("n", ctypes.c_uint64),
                 ("d_recs", ctypes.c_void_p), ("d_hash", ctypes.c_void_p),
-                ("d_recs32", ctypes.c_void_p), ("d_frag", ctypes.c_void_p)]
+                ("d_recs32", ctypes.c_void_p), ("d_frag", ctypes.c_void_p),
+                ("d_key", ctypes.c_void_p)]
 
 
 class LdpPacket(ctypes.Structure):
@@ -38,14 +41,14 @@ class LdpPacket(ctypes.Structure):
 
 
 assert ctypes.sizeof(LdpPacket) == 24
-assert ctypes.sizeof(RxOpts) == 36
+assert ctypes.sizeof(RxOpts) == 40
 
 EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_batch", "pptk_rx_batch_submit", "pptk_rx_batch_complete",
            "pptk_rx_batch_pending", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
-           "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device",
+           "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device", "pptk_rx_permit_keys_device",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_set_side_buffer",
            "pptk_tx_rewrite_device",
            "pptk_tcp_mss_clamp_device", "pptk_rx_autotune", "pptk_rx_place_records",
@@ -53,6 +56,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            # multi-GPU (RCCL)
            "pptk_rx_device_count", "pptk_rx_comm_uid", "pptk_rx_comm_create",
            "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
+           "pptk_rx_comm_abort", "pptk_rx_comm_sync",
            "pptk_rx_shard_range", "pptk_rx_allgather_hash",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
@@ -128,6 +132,10 @@ def lib(path=None):
             L.pptk_rx_permit_device.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp,
                                                 vp, vp, vp, vp]
             L.pptk_rx_permit_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_permit_keys_device"):   # absent from older A/B builds
+            L.pptk_rx_permit_keys_device.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_int, vp,
+                                                     vp, vp, vp, vp]
+            L.pptk_rx_permit_keys_device.restype = ctypes.c_int
             L.pptk_rx_tokens_refill_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32,
                                                        ctypes.c_uint32, ctypes.c_uint32, vp]
             L.pptk_rx_tokens_refill_device.restype = ctypes.c_int
@@ -154,6 +162,11 @@ def lib(path=None):
             L.pptk_rx_shard_range.restype = None
             L.pptk_rx_allgather_hash.argtypes = [vp, vp, ctypes.c_uint64, vp, vp]
             L.pptk_rx_allgather_hash.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_comm_sync"):            # absent from older A/B builds
+            L.pptk_rx_comm_abort.argtypes = [vp]
+            L.pptk_rx_comm_abort.restype = ctypes.c_int
+            L.pptk_rx_comm_sync.argtypes = [vp, vp, ctypes.c_uint32]
+            L.pptk_rx_comm_sync.restype = ctypes.c_int
         L.pptk_rx_version.restype = ctypes.c_char_p
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
@@ -193,7 +206,7 @@ class RxContext:
 
     def __init__(self, device=0, key=bytes(16), iphash_bits4=0, iphash_bits6=0,
                  iphash_size=1, max_batch=8192, max_frame=9216, gather_threads=1,
-                 lib_path=None):
+                 lib_path=None, comm_timeout_ms=0):
         self._L = L = lib(lib_path)
         o = RxOpts()
         L.pptk_rx_opts_default(ctypes.byref(o))
@@ -202,7 +215,10 @@ class RxContext:
             o.key[i] = b
         o.iphash_bits4, o.iphash_bits6, o.iphash_size = iphash_bits4, iphash_bits6, iphash_size
         o.max_batch, o.max_frame, o.gather_threads = max_batch, max_frame, gather_threads
+        if comm_timeout_ms:
+            o.comm_timeout_ms = comm_timeout_ms
         self._ctx = ctypes.c_void_p()
+        self._inflight = collections.deque()   # (pkts, out) of submitted host batches
         rc = L.pptk_rx_ctx_create(ctypes.byref(self._ctx), ctypes.byref(o))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_ctx_create failed ({rc})")
@@ -220,8 +236,9 @@ class RxContext:
 
     def close(self):
         if self._ctx:
-            self._L.pptk_rx_ctx_destroy(self._ctx)
+            self._L.pptk_rx_ctx_destroy(self._ctx)   # (waits for outstanding submissions)
             self._ctx = ctypes.c_void_p()
+            self._inflight.clear()
 
     def __del__(self):
         try:
@@ -231,11 +248,12 @@ class RxContext:
 
     def batch_device(self, frames, n, off=None, lens=None, stride=0, fixed_len=0,
                      perm=None, recs=None, hash_out=None, max_len=0, stream=None,
-                     compact=False, frag_out=None):
+                     compact=False, frag_out=None, key_out=None):
         """Asynchronous device batch on `stream` (torch stream or None = current).
         frames/off/lens/perm/recs/hash_out are torch CUDA tensors; compact:
         32-byte struct pptk_rx_rec32 records (recs is (n, 32) bytes);
-        frag_out: (n, 16) uint8 tensor of struct pptk_rx_frag side records."""
+        frag_out: (n, 16) uint8 tensor of struct pptk_rx_frag side records;
+        key_out: (n,) int32 tensor of dense rate-limiter keys (d_key)."""
         import torch
         rb = 32 if compact else 64
         if recs is None:
@@ -246,7 +264,8 @@ class RxContext:
                        max_len, n, None if compact else recs.data_ptr(),
                        None if hash_out is None else hash_out.data_ptr(),
                        recs.data_ptr() if compact else None,
-                       None if frag_out is None else frag_out.data_ptr())
+                       None if frag_out is None else frag_out.data_ptr(),
+                       None if key_out is None else key_out.data_ptr())
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
         rc = self._L.pptk_rx_batch_device(self._ctx, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
@@ -372,6 +391,25 @@ class RxContext:
             raise OSError(-rc, f"pptk_rx_permit_device failed ({rc})")
         return verdict
 
+    def permit_keys_device(self, keys, family, tokens, subject=None, verdict=None, scratch=None,
+                           stream=None):
+        """pptk_rx_permit_keys_device: the rate limiter from the dense keys
+        (torch int32 (n,)) a batch wrote through key_out."""
+        import torch
+        n = keys.numel()
+        if verdict is None:
+            verdict = torch.empty(n, dtype=torch.uint8, device=keys.device)
+        if scratch is None:
+            scratch = torch.empty(self._L.pptk_rx_permit_scratch_bytes(n, tokens.numel()),
+                                  dtype=torch.uint8, device=keys.device)
+        s = stream if stream is not None else torch.cuda.current_stream(keys.device)
+        rc = self._L.pptk_rx_permit_keys_device(self._ctx, _dp(keys), n, family, _dp(subject),
+                                                _dp(tokens), _dp(verdict), _dp(scratch),
+                                                ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_permit_keys_device failed ({rc})")
+        return verdict
+
     def tokens_refill_device(self, tokens, start, end, add, initial, stream=None):
         import torch
         s = stream if stream is not None else torch.cuda.current_stream(tokens.device)
@@ -441,6 +479,20 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_comm_destroy failed ({rc})")
 
+    def comm_abort(self):
+        """pptk_rx_comm_abort: cancel the communicator (any thread)."""
+        rc = self._L.pptk_rx_comm_abort(self._ctx)
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_comm_abort failed ({rc})")
+
+    def comm_sync(self, stream=None, timeout_ms=0):
+        """pptk_rx_comm_sync: bounded wait for `stream` (torch stream, None =
+        current) with RCCL error checks; returns 0 or the negative errno
+        (-ETIMEDOUT / -EIO / -ECANCELED: the communicator is then dead)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return self._L.pptk_rx_comm_sync(self._ctx, ctypes.c_void_p(s.cuda_stream), timeout_ms)
+
     def comm_info(self):
         """(nranks, rank) of the context's communicator, or None."""
         nr, r = ctypes.c_int(), ctypes.c_int()
@@ -509,6 +561,9 @@ class RxContext:
                                           ctypes.c_void_p(out.ctypes.data))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch_submit failed ({rc})")
+        # the library holds pointers into both until the batch completes:
+        # keep the Python objects alive until then (FIFO, as completions)
+        self._inflight.append((pkts, out))
 
     def complete_host(self):
         """pptk_rx_batch_complete: wait for the oldest outstanding batch;
@@ -516,6 +571,7 @@ class RxContext:
         rc = self._L.pptk_rx_batch_complete(self._ctx)
         if rc < 0:
             raise OSError(-rc, f"pptk_rx_batch_complete failed ({rc})")
+        self._inflight.popleft()
         return rc
 
     def pending_host(self):

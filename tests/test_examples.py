@@ -106,6 +106,43 @@ def test_rx_multigpu_allgather_bit_exact(tmp_path):
 
 
 @pytest.mark.gpu
+def test_rx_multigpu_thread_join_bit_exact(tmp_path):
+    """The per-process join form in threads (RX_MULTIGPU_JOIN=threads: a uid
+    from main, pptk_rx_comm_create in every rank's thread), one rank per GPU:
+    bit-exact as above."""
+    p = str(tmp_path / "s.rxq")
+    n = write_rxq(p)
+    env = dict(os.environ, RX_MULTIGPU_JOIN="threads")
+    out = subprocess.run([build(tmp_path, "rx_multigpu", hip=True), p], capture_output=True,
+                         text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert f"{n} frames, 0 mismatches" in out.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("join,ranks", [("all", 1), ("threads", 2)])
+def test_rx_multigpu_failed_thread_exits_nonzero(tmp_path, join, ranks):
+    """Failure containment: the last rank's thread fails (RX_MULTIGPU_FAIL).
+    create_all form: it fails before its first gather and aborts every
+    communicator.  Thread-join form, two ranks: it never joins, so rank 0's
+    pptk_rx_comm_create must give up at the deadline (ETIMEDOUT, -110)
+    instead of blocking forever.  Either way the process exits 1, promptly."""
+    import time
+    p = str(tmp_path / "s.rxq")
+    write_rxq(p, ("edge",))
+    env = dict(os.environ, RX_MULTIGPU_JOIN=join, RX_MULTIGPU_FAIL=str(ranks - 1),
+               RX_MULTIGPU_TIMEOUT_MS="3000")
+    t0 = time.monotonic()
+    out = subprocess.run([build(tmp_path, "rx_multigpu", hip=True), p, str(ranks), "2"],
+                         capture_output=True, text=True, timeout=120, env=env)
+    took = time.monotonic() - t0
+    assert out.returncode == 1, out.stdout + out.stderr
+    assert "FAILED" in out.stdout and took < 60, (took, out.stdout)
+    if join == "threads":
+        assert "rc -110" in out.stdout, out.stdout          # rank 0: ETIMEDOUT
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nbytes", [1500, 64])
 def test_rx_perf_device_resident_from_c(tmp_path, nbytes):
     """examples/rx_perf.c: the device-resident throughput timed from a plain

@@ -215,3 +215,71 @@ def test_sharded_layout_n_ranks_one_gpu(dev, name, world):
     pad = np.concatenate([h[r * per + max(0, min(per, n - r * per)):(r + 1) * per]
                           for r in range(world)])
     assert (pad == np.uint64(0xFFFFFFFFFFFFFFFF)).all()
+
+
+ETIMEDOUT, ECANCELED = 110, 125
+
+
+def test_comm_rank_never_joins_times_out_then_recovers(dev):
+    """Failure containment (pptk_rx.h "Multi-GPU"): a 2-rank communicator
+    whose rank 1 never joins.  pptk_rx_comm_create must give up with
+    ETIMEDOUT within opts.comm_timeout_ms (plus RCCL's abort), leave the
+    context without a communicator, and the same context must then build a
+    1-rank communicator whose gather equals the golden flow hashes."""
+    import time
+    from pptk_amd.rx import RxContext, comm_uid
+    z = load_golden("edge")
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_frame=65535, comm_timeout_ms=3000)
+    t0 = time.monotonic()
+    with pytest.raises(OSError) as e:
+        ctx.comm_create(2, 0, comm_uid())
+    took = time.monotonic() - t0
+    assert e.value.errno == ETIMEDOUT, e.value
+    assert 2.5 < took < 30, took
+    assert ctx.comm_info() is None
+    ctx.comm_create(1, 0, comm_uid())
+    got, _ = _gather_set(ctx, z, dev)
+    assert np.array_equal(got, as_records(z["recs"])["flow_hash"])
+    assert ctx.comm_sync() == 0
+    ctx.close()
+
+
+def test_comm_sync_and_abort(dev):
+    """pptk_rx_comm_sync after gathers returns 0 with the golden hashes in
+    place; after pptk_rx_comm_abort every call on the communicator returns
+    ECANCELED until it is destroyed, and a new one works."""
+    from pptk_amd.rx import comm_uid
+    z = load_golden("cmix")
+    ctx = _ctx(z)
+    want = as_records(z["recs"])["flow_hash"]
+    ctx.comm_create(1, 0, comm_uid())
+    s = torch.cuda.Stream(dev)
+    n = len(z["off"])
+    from pptk_amd.shard import GatherBuffer
+    gb = GatherBuffer(n, 1, 0, dev)
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    with torch.cuda.stream(s):
+        for _ in range(4):
+            ctx.batch_device(frames, n, off=off, lens=lens, max_len=int(z["len"].max()),
+                             hash_out=gb.local[:n], stream=s)
+            gb.gather(ctx, stream=s)
+    assert ctx.comm_sync(s, 10000) == 0
+    assert np.array_equal(gb.out[:n].cpu().numpy().view(np.uint64), want)
+    ctx.comm_abort()
+    ctx.comm_abort()                                        # once is enough; no error
+    with pytest.raises(OSError) as e:
+        gb.gather(ctx, stream=s)
+    assert e.value.errno == ECANCELED
+    assert ctx.comm_info() == (1, 0)
+    ctx.comm_destroy()
+    with pytest.raises(OSError) as e:                       # no communicator
+        ctx.comm_abort()
+    assert e.value.errno == EINVAL
+    assert ctx.comm_sync(s, 1000) == 0                      # plain bounded stream wait
+    ctx.comm_create(1, 0, comm_uid())
+    got, _ = _gather_set(ctx, z, dev)
+    assert np.array_equal(got, want)
+    ctx.close()

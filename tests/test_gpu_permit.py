@@ -155,3 +155,82 @@ def test_permit_ragged_batch_unaligned_verdicts(n, dev):
     assert got[0] == 0xEE and (got[n + 1:] == 0xEE).all()
     assert np.array_equal(tok.cpu().numpy().view(np.uint32), th)
     assert v.data_ptr() == vbuf.data_ptr() + 1
+
+
+def _dense_keys(r):
+    """The d_key encoding (include/pptk_rx.h) of host records r."""
+    from pptk_amd.records import F_IPV6, F_PARSED
+    k = r["src_bucket"].astype(np.uint32)
+    k = np.where(r["flags"] & F_IPV6, k | np.uint32(0x80000000), k)
+    return np.where(r["flags"] & F_PARSED, k, np.uint32(0xFFFFFFFF)).astype(np.uint32)
+
+
+def test_dense_keys_written_by_rx_and_permit_from_keys(dev):
+    """pptk_rx_dev_batch.d_key: the rx kernel's dense keys equal the encoding
+    of the golden records, and pptk_rx_permit_keys_device on them gives the
+    reference's verdicts and tokens for every golden case."""
+    z = load_golden("permit")
+    ctx = _ctx(z)
+    n = len(z["off"])
+    frames = torch.zeros(z["buf"].size + 64, dtype=torch.uint8, device=dev)
+    frames[:z["buf"].size] = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    keys = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.batch_device(frames, n, off=off, lens=lens, max_len=int(z["len"].max()), key_out=keys)
+    torch.cuda.synchronize()
+    want = z["recs"].reshape(-1).view(REC_DTYPE)
+    assert np.array_equal(keys.cpu().numpy().view(np.uint32), _dense_keys(want))
+    for k, (fam, init, has_subj) in enumerate(z["case_meta"]):
+        tok = torch.from_numpy(z["case_tok_in"][k].view(np.int32).copy()).to(dev)
+        subj = torch.from_numpy(z["case_subject"][k]).to(dev) if has_subj else None
+        v = ctx.permit_keys_device(keys, int(fam), tok, subject=subj)
+        torch.cuda.synchronize()
+        assert np.array_equal(v.cpu().numpy(), z["case_verdict"][k]), (fam, init, has_subj)
+        assert np.array_equal(tok.cpu().numpy().view(np.uint32), z["case_tok_out"][k])
+
+
+@pytest.mark.parametrize("case", ["heavy_hitter", "all_over_budget", "mixed_v6", "big_table",
+                                  "tiny_table"])
+def test_permit_regimes_against_oracle(case, dev):
+    """The block-histogram path in the regimes that exercise its resolve
+    pass (one bucket holding most frames and running out inside a late block;
+    every bucket over budget; IPv6 with a subject mask), the sort fallback
+    (hash_size 2^17) and a 2-bucket table, on records and on dense keys: GPU ==
+    frame-by-frame restatement."""
+    from oracle.oracle import Oracle
+    from pptk_amd.records import F_IPV6, F_PARSED
+    rng = np.random.default_rng(sum(case.encode()))
+    n = (3 << 20) + 17
+    hs = {"big_table": 1 << 17, "tiny_table": 2}.get(case, 1 << 16)
+    r = np.zeros(n, dtype=REC_DTYPE)
+    fam = 6 if case == "mixed_v6" else 4
+    r["flags"] = np.where(rng.random(n) < 0.97, F_PARSED, 0) | np.where(
+        rng.random(n) < (0.6 if fam == 6 else 0.1), F_IPV6, 0)
+    if case == "heavy_hitter":
+        b = np.where(rng.random(n) < 0.9, 7, rng.integers(0, hs, n))
+        tok_h = rng.integers(0, 40, hs).astype(np.uint32)
+        tok_h[7] = 2_000_000            # runs out inside a late histogram block
+    elif case == "all_over_budget":
+        b = rng.integers(0, hs, n)
+        tok_h = rng.integers(0, 30, hs).astype(np.uint32)
+    else:
+        b = np.minimum(rng.zipf(1.2, n) - 1, hs - 1)
+        tok_h = rng.integers(0, 300, hs).astype(np.uint32)
+    r["src_bucket"] = b
+    subj = (rng.random(n) < 0.8).astype(np.uint8) if case == "mixed_v6" else None
+    ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+    vh, th = Oracle().permit_batch(r, fam, subj, tok_h)
+    assert (vh == 0).sum() > 100 and (vh == 1).sum() > 100
+    sub_t = None if subj is None else torch.from_numpy(subj).to(dev)
+    for via_keys in (False, True):
+        tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
+        if via_keys:
+            keys = torch.from_numpy(_dense_keys(r).view(np.int32)).to(dev)
+            v = ctx.permit_keys_device(keys, fam, tok, subject=sub_t)
+        else:
+            recs = torch.from_numpy(r.view(np.uint8).reshape(n, 64)).to(dev)
+            v = ctx.permit_device(recs, fam, tok, subject=sub_t)
+        torch.cuda.synchronize()
+        assert np.array_equal(v.cpu().numpy(), vh), via_keys
+        assert np.array_equal(tok.cpu().numpy().view(np.uint32), th), via_keys

@@ -22,7 +22,54 @@ def _lib():
     vp = ctypes.c_void_p
     L.rwmix_run.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                             ctypes.c_int, ctypes.c_int, vp, vp]
+    L.sol_run.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32,
+                          ctypes.c_uint32, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.sol_run.restype = ctypes.c_int
     return L
+
+
+def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
+    """Speed of light of an rx launch's traffic on this GPU: the fastest of
+    several trivial kernels (tools/rwmix.hip sol_kernel: plain / non-
+    temporal, 4 or 16 loads per lane in flight, 2 / 4 / 8 blocks per CU)
+    reading the launch's frame bytes in 64-frame tiles -- fixed tiles of rb
+    bytes, or (off/lens given: frames packed in batch order) each tile's
+    actual span after its descriptors -- and writing wb record bytes per
+    tile.  Returns (ms, setting)."""
+    import torch
+    L = _lib()
+    dev = inp.device
+    ntiles = n // 64
+    assert ntiles > 0 and out.numel() >= ntiles * wb and wb % 16 == 0
+    gather = off is not None
+    if not gather:
+        assert inp.numel() >= ntiles * rb
+    sink = torch.zeros(64, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    best = (float("inf"), None)
+    for mode in (0, 1, 4, 5):
+        m = mode | (2 if gather else 0)
+        for mult in (2, 4, 8):
+            ts = []
+            for k in range(reps + 2):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                rc = L.sol_run(inp.data_ptr(), off.data_ptr() if gather else None,
+                               lens.data_ptr() if gather else None, n, out.data_ptr(), ntiles,
+                               rb, wb, m, ncu * mult, sink.data_ptr(),
+                               ctypes.c_void_p(s.cuda_stream))
+                b.record()
+                torch.cuda.synchronize(dev)
+                assert rc == 0
+                if k >= 2:
+                    ts.append(a.elapsed_time(b))
+            ts.sort()
+            med = ts[len(ts) // 2]
+            if med < best[0]:
+                best = (med, {"nt": bool(mode & 1), "loads_in_flight": 4 if mode & 4 else 16,
+                              "blocks_per_cu": mult * 1})
+    return best
 
 
 def mix_ms(inp, rb, ntiles, out, wb, nt=1, reps=8):
