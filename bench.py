@@ -492,9 +492,13 @@ def binned_bench(ctx, b, n, dev, steps, warmup, recs=None):
     torch.cuda.synchronize(dev)
     ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
     ach = b["bytes"] / (ms * 1e-3) / 1e9
+    p = perm[:min(n, 1 << 20)].cpu()
+    binned = bool((p != torch.arange(p.numel(), dtype=p.dtype)).any().item())
     return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "ms_per_batch": round(ms, 4),
-            "workload": "CMIX, pptk_rx_batch_device_mixed: device length binning + one launch "
-                        "per length group, records at the frames' own indices",
+            "workload": f"{b['cfg'].upper()}, pptk_rx_batch_device_mixed: device length histogram; "
+                        "binned (one launch per length group) when >= 40 % of the frames are "
+                        "<= 113 B, else batch order; records at the frames' own indices",
+            "binned_by_plan": binned,
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
 
@@ -506,7 +510,7 @@ def summary(r, n):
     ks = r["kernel_ms"] * 1e-3
     ach = r["bytes"] / ks / 1e9
     rw = (r["bytes"] + r["rec_bytes"]) / ks / 1e9
-    return {"value": round(r["mpkts"], 1), "unit": "Mpkts/s",
+    out = {"value": round(r["mpkts"], 1), "unit": "Mpkts/s",
             "kernel_ms": round(r["kernel_ms"], 4), "kernel_variant": r.get("variant"),
             "frames_per_gpu": n, "frame_bytes": r["bytes"], "record_bytes": r["rec_bytes"],
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -515,6 +519,21 @@ def summary(r, n):
             "full_batch_check": r.get("full_batch_check"),
             "oracle_sample": r.get("oracle_sample"),
             "record_placement": r.get("placement")}
+    out["roofline"].update(as_allocated(r))
+    return out
+
+
+def as_allocated(r):
+    """{"frac_as_allocated": ...}: the read-roofline fraction of the same
+    launch into the buffers as first allocated (the placement probe's pair
+    0), beside the placed pair's `frac` -- what a caller that does not place
+    its rings gets on this GPU."""
+    p = r.get("placement") or {}
+    ms = p.get("as_allocated_ms")
+    if not ms:
+        return {}
+    return {"frac_as_allocated": round(r["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "as_allocated_ms": ms}
 
 
 def oracle_sample(b, recs, n, dev, k=4096, compact=False):
@@ -971,6 +990,7 @@ def main():
                 "traffic_source": tsrc,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_ms": round(kernel_ms, 4), "kernel_variant": prim["variant"]}
+    roofline.update(as_allocated(prim))
     if box and "mix_ms" in box:
         # fraction of this GPU's speed of light for the same read/write mix
         # (a trivial kernel moving the same bytes, tools/rwmix.hip)
@@ -1017,7 +1037,7 @@ def main():
 
     secondary = {}
     if not args.no_secondary and args.only is None:
-        for cfg in ("c64", "cmix"):
+        for cfg in ("c64", "cmix", "imix"):
             r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None, check,
                            args.settle, first=first, place=place)
             secondary[cfg] = summary(r, n)
@@ -1026,7 +1046,7 @@ def main():
                 if sol:
                     secondary[cfg]["roofline"]["mix_sol_ms"] = sol[0]
                     secondary[cfg]["roofline"]["mix_sol_frac"] = round(sol[0] / r["kernel_ms"], 4)
-            if cfg == "cmix":
+            if cfg in ("cmix", "imix"):
                 secondary[cfg]["binned"] = binned_bench(ctx, r["_batch"], n, dev, args.steps,
                                                         args.warmup, recs=r["_recs"])
             if cfg == "c64" and not args.no_rec32:

@@ -57,8 +57,10 @@ __global__ __launch_bounds__(BT) void bin_count(const uint16_t *len, uint64_t n,
 }
 
 // exclusive scan of m = NB * nblocks counters (bin-major), one block; then
-// table[k] = start of bin k, table[NB] = total
-__global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, uint32_t *table) {
+// table[k] = start of bin k, table[NB] = total, table[NB + 1] = plan (1 =
+// bin; adaptive: only with >= kBinShortPct % of the frames in group 0)
+__global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, uint32_t *table,
+                                                 uint32_t adaptive) {
   __shared__ uint32_t part[1024];
   const uint32_t per = (m + 1023) / 1024;
   const uint32_t lo = threadIdx.x * per;
@@ -83,6 +85,10 @@ __global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, u
   const uint32_t g = m / NB;
   if (threadIdx.x <= (unsigned)NB)
     table[threadIdx.x] = threadIdx.x < (unsigned)NB ? counts[threadIdx.x * g] : part[1023];
+  if (threadIdx.x == 0) {   // group 0 holds [0, start of group 1)
+    const uint64_t total = part[1023], short0 = NB > 1 ? counts[g] : total;
+    table[NB + 1] = !adaptive || short0 * 100u >= (uint64_t)kBinShortPct * total ? 1u : 0u;
+  }
 }
 
 // (bdesc: optionally also the frames' descriptors in binned order -- offset
@@ -93,10 +99,15 @@ __global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, u
 __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t n,
                                                   uint64_t per_block, const uint32_t *offs,
                                                   uint32_t *perm, BinDesc bdesc,
-                                                  BinBounds bb) {
+                                                  BinBounds bb, const uint32_t *plan) {
   __shared__ uint32_t cursor[NB];
   __shared__ uint32_t wcnt[NWARP][NB];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (*plan == 0) {   // not binned: the identity order, no binned descriptors
+    const uint64_t lo = blockIdx.x * per_block, hi = min(lo + per_block, n);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += BT) perm[i] = (uint32_t)i;
+    return;
+  }
   if (threadIdx.x < NB) cursor[threadIdx.x] = offs[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
   __syncthreads();
   const uint64_t lo = blockIdx.x * per_block;
@@ -136,10 +147,11 @@ __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t 
 
 }  // namespace
 
-// scratch: counters (NB x grid), the group table (NB + 1), then (16-byte
-// aligned) the binned descriptors: n u64 offsets and n u16 lengths
+// scratch: counters (NB x grid), the group table (NB + 1) and the plan
+// word, then (16-byte aligned) the binned descriptors: n u64 offsets and n
+// u16 lengths
 static size_t table_end(int grid) {
-  return ((((size_t)NB * (size_t)grid + NB + 1) * sizeof(uint32_t)) + 15) & ~(size_t)15;
+  return ((((size_t)NB * (size_t)grid + NB + 2) * sizeof(uint32_t)) + 15) & ~(size_t)15;
 }
 
 size_t bin_scratch_bytes(uint64_t n, int grid) {
@@ -160,16 +172,18 @@ const uint32_t *bin_table(const void *scratch, int grid) {
 
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm, void *scratch,
                       hipStream_t s, int grid, const BinDesc &bdesc,
-                      const BinBounds &bounds) {
+                      const BinBounds &bounds, bool adaptive) {
   if (n == 0) return hipSuccess;
   const uint64_t per_block = ((n + grid - 1) / grid + BT - 1) / BT * BT;
   const int g = (int)((n + per_block - 1) / per_block);
   uint32_t *counts = (uint32_t *)scratch;
   hipLaunchKernelGGL(bin_count, dim3(g), dim3(BT), 0, s, len, n, per_block, counts, bounds);
-  hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, s, counts, (uint32_t)(NB * g),
-                     counts + (size_t)NB * grid);
+  uint32_t *table = counts + (size_t)NB * grid;
+  hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, s, counts, (uint32_t)(NB * g), table,
+                     adaptive ? 1u : 0u);
   hipLaunchKernelGGL(bin_scatter, dim3(g), dim3(BT), 0, s, len, n, per_block,
-                     (const uint32_t *)counts, perm, bdesc, bounds);
+                     (const uint32_t *)counts, perm, bdesc, bounds,
+                     (const uint32_t *)table + NB + 1);
   return hipGetLastError();
 }
 

@@ -796,7 +796,7 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
              bin_desc_len(d_scratch, kBinGrid, b->n)};
   const BinBounds &bb = bin_bounds();
   const bool dflt = default_bounds(bb);
-  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid, bd, bb);
+  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid, bd, bb, true);
   if (e != hipSuccess) return -EIO;
   RxKArgs a = batch_args(c, b);
   a.perm = d_perm;
@@ -804,6 +804,9 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
   a.len = bd.blen;
   a.by_pos = 1;
   const uint32_t *tab = bin_table(d_scratch, kBinGrid);
+  a.plan = tab + kGroups + 1;
+  a.off0 = b->d_off;
+  a.len0 = b->d_len;
   const uint32_t maxlen = b->max_len ? b->max_len : 65535u;
   const int fv = forced_variant(c);
   for (int g = 0; g < kGroups; ++g) {
@@ -811,9 +814,14 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
     // when the hint is right; a wrong hint costs speed, never results)
     const bool last = g == kGroups - 1 || bb.b[g] >= maxlen;
     if (!last && g > 0 && bb.b[g] == bb.b[g - 1]) continue;   // empty by its bounds
-    const int variant = fv >= 0 && fv != RX_L4 ? fv
-                        : dflt || g == kGroups - 1 ? kGroupVariant[g]
-                                                   : pick_variant(bb.b[g] + 15);
+    int variant = fv >= 0 && fv != RX_L4 ? fv
+                  : dflt || g == kGroups - 1 ? kGroupVariant[g]
+                                             : pick_variant(bb.b[g] + 15);
+    // (the last launch also runs the whole batch when it is not binned:
+    // pptk_rx_autotune's choice for its shape applies, as in batch order)
+    if (last && fv < 0 && c->tuned[1][variant] >= 0 && c->tuned[1][variant] != RX_L4)
+      variant = c->tuned[1][variant];
+    a.plan_all = last ? 1u : 0u;
     a.range_lo = tab + g;
     a.range_hi = tab + (last ? kGroups : g + 1);
     a.tune = pick_tune(c, variant, true);
@@ -864,6 +872,7 @@ static int permit_common(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs
   a.verdict = d_verdict;
   a.hash_size = hs;
   a.family = family;
+  a.ncu = c->ncu;
   return hip_err(launch_permit(a, d_scratch, (hipStream_t)stream));
 }
 
@@ -902,7 +911,7 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *c, const uint16_t *d_len, uint64_t n,
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   return hip_err(launch_bin(d_len, n, d_perm, d_scratch, (hipStream_t)stream, kBinGrid,
-                            BinDesc{nullptr, 0, nullptr, nullptr}, bin_bounds()));
+                            BinDesc{nullptr, 0, nullptr, nullptr}, bin_bounds(), false));
 }
 
 static int ensure_slot(pptk_rx_ctx *c, RxSlot &sl, size_t pkts, size_t bytes) {

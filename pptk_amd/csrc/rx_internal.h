@@ -92,6 +92,14 @@ struct RxKArgs {
   // MSS clamping (pptk_tcp_mss_clamp_device): new MSS, PPTK_MSS_* flags;
   // the per-frame status goes to rw_status
   uint32_t mss, mss_flags;
+  // binned launches of pptk_rx_batch_device_mixed: the binning's plan word
+  // (device; 0 = the batch is not worth binning: batch order), the caller's
+  // own descriptors for that case (off0 nullable: stride), and whether this
+  // launch is the one that then takes every frame
+  const uint32_t *plan;
+  const uint64_t *off0;
+  const uint16_t *len0;
+  uint32_t plan_all;
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S
@@ -129,8 +137,15 @@ hipError_t launch_mss_clamp(const RxKArgs &a, int grid, hipStream_t s);
 int rx_variant_blocks_per_cu(int variant);
 
 // Stable counting sort of 0..n-1 into kGroups length groups.  After it,
-// bin_table(scratch, grid)[g] is the first position of group g in perm and
-// [kGroups] = n (device memory, written by the launch).
+// bin_table(scratch, grid)[g] is the first position of group g in perm,
+// [kGroups] = n and [kGroups + 1] the plan word (device memory, written by
+// the launch).  With `adaptive` the binning first decides whether the batch
+// is worth binning at all: only if at least kBinShortPct % of its frames are
+// in group 0 (the short frames a small kernel shape streams many per round;
+// CMIX's uniform 64-1500 B has 3 %, IMIX 58 %).  Otherwise the plan word is
+// 0, perm is the identity and the group launches run the batch in batch
+// order (every split of a uniform mix measured slower: DESIGN.md).
+constexpr uint32_t kBinShortPct = 40;
 constexpr int kBinGrid = 2048;   // blocks of the binning sort (scratch layout)
 // Optional binned copy of the descriptors (boff/blen null: perm only).
 struct BinDesc {
@@ -146,7 +161,7 @@ struct BinBounds {
 };
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm,
                       void *scratch, hipStream_t s, int grid, const BinDesc &bdesc,
-                      const BinBounds &bounds);
+                      const BinBounds &bounds, bool adaptive);
 size_t bin_scratch_bytes(uint64_t n, int grid);
 const uint32_t *bin_table(const void *scratch, int grid);
 uint64_t *bin_desc_off(void *scratch, int grid);
@@ -163,6 +178,7 @@ struct PermitArgs {
   uint8_t *verdict;             // 1 permitted, 0 denied, 2 not subject
   uint32_t hash_size;
   int family;                   // 4 or 6
+  int ncu;                      // compute units (grid of the persistent verdict pass)
 };
 size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size);
 hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t s);

@@ -874,7 +874,21 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // length-group launch (pptk_rx_batch_device_mixed): this launch owns
     // positions [*range_lo, *range_hi) of the binned order, known on the
     // device only
-    if (a.range_lo) {
+    if (a.range_lo && a.plan && *a.plan == 0) {
+      // the binning found the batch not worth binning: the launch marked
+      // plan_all runs every frame in batch order from the caller's own
+      // descriptors (records in whole 4 KB runs), the others nothing
+      if (!a.plan_all) return;
+      a.perm = nullptr;
+      a.perm_ld = (const uint32_t *)a.zero;
+      a.perm_msk = 0u;
+      a.off_ld = a.off0 ? a.off0 : (const uint64_t *)a.zero;
+      a.off_msk = a.off0 ? ~0u : 0u;
+      a.stride_g = a.off0 ? 0u : a.stride;
+      a.len_ld = a.len0;
+      a.len_msk = ~0u;
+      a.by_pos = 0;
+    } else if (a.range_lo) {
       const uint32_t lo = *a.range_lo, hi = *a.range_hi;
       a.perm_ld += lo;
       if (a.by_pos) {

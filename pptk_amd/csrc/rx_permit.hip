@@ -45,9 +45,9 @@
 //      "all" when count_b <= T_b, 0 when T_b == 0, else pending; T_b -=
 //      min(T_b, count_b);
 //   R. only blocks that are some bucket's c* (none when no bucket runs out
-//      of tokens): walk the block's frames in order (staged through LDS,
-//      one wave ranks them with ballots, LDS counters per bucket) and set
-//      lim[b] = index of the need_b-th frame of b + 1;
+//      of tokens): list the block's frames of such buckets in frame order
+//      and walk the list (one wave ranks them with ballots, LDS counters
+//      per bucket): lim[b] = index of the need_b-th frame of b + 1;
 //   V. verdicts in frame order from the dense keys and lim[].
 // 16 M frames, 2^16 buckets: the histogram table is 32 MB, the passes read
 // the keys twice -- no 64 MB x (2 passes x 3 arrays) radix sort.
@@ -115,17 +115,57 @@ __global__ __launch_bounds__(PT) void permit_keys(PermitArgs a, uint32_t *keys) 
 }
 
 // ---- the sort-free path (hash_size <= 2^16) ------------------------------
-constexpr uint32_t HB = 65535;       // frames per histogram block (u16 counts)
-constexpr int HT = 1024;             // threads of the histogram / resolve blocks
+constexpr uint32_t HB = 65532;       // frames per histogram block (u16 counts; 4 | HB)
+constexpr int HT = 1024;             // threads of the histogram / resolve / verdict blocks
 constexpr uint32_t HMAX = 1u << 16;  // largest hash_size of the sort-free path
-constexpr uint32_t LIM_ALL = 0xffffffffu;
 constexpr uint32_t NOBLK = 0xffffffffu;
-constexpr int RCH = 2048;            // frames staged per resolve chunk
+// code[b] (u16), what the verdict of a frame of bucket b depends on:
+constexpr uint16_t CODE_ALL = 0xffff;    // every frame of b permitted
+constexpr uint16_t CODE_NONE = 0xfffe;   // none (T_b == 0)
+                                         // else c*: permitted below block c*,
+                                         // denied above, lim[b] inside it
+constexpr uint32_t MAX_BLOCKS = 0xfffd;  // block ids below CODE_NONE
 
 __device__ __forceinline__ uint32_t hwords(uint32_t hash_size) { return (hash_size + 1) / 2; }
 
-// H: per-block histogram (u16 pairs in LDS, one word = buckets 2w, 2w + 1)
-// and the dense subject keys
+// Subject key of frame i for the passes after the histogram: straight from
+// the caller's dense keys, or from the histogram pass's copy (records).
+__device__ __forceinline__ uint32_t key_at(const PermitArgs &a, const uint32_t *ckey, uint64_t i) {
+  return a.keys_in ? subject_key(a, i) : ckey[i];
+}
+
+__device__ __forceinline__ uint32_t filter_key(const PermitArgs &a, uint32_t k) {
+  return k != NOSUBJ && ((k >> 31) == (a.family == 6 ? 1u : 0u)) ? (k & 0x7fffffffu) : NOSUBJ;
+}
+
+// Subject keys of frames i .. i + 3 (i + 4 <= n): one 16-byte load when the
+// key array allows it (vec), else four.
+__device__ __forceinline__ void keys4(const PermitArgs &a, const uint32_t *ckey, uint64_t i,
+                                      bool vec, uint32_t k[4]) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  if (vec) {
+    const u32x4 q = *(const u32x4 *)((a.keys_in ? a.keys_in : ckey) + i);
+    k[0] = q.x;
+    k[1] = q.y;
+    k[2] = q.z;
+    k[3] = q.w;
+    if (a.keys_in) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) k[u] = filter_key(a, k[u]);
+      if (a.subject) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) k[u] = a.subject[i + u] ? k[u] : NOSUBJ;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = key_at(a, ckey, i + u);
+  }
+}
+
+// H: per-block histogram (u16 pairs in LDS, one word = buckets 2w, 2w + 1);
+// from records it also writes each frame's subject key densely (ckey), so
+// the later passes read 4 bytes per frame instead of the record again
 __global__ __launch_bounds__(HT) void permit_hist(PermitArgs a, uint32_t *ckey, uint32_t *bh,
                                                   uint32_t *blk_flag) {
   __shared__ uint32_t h[HMAX / 2];
@@ -135,10 +175,23 @@ __global__ __launch_bounds__(HT) void permit_hist(PermitArgs a, uint32_t *ckey, 
   __syncthreads();
   const uint64_t lo = (uint64_t)blockIdx.x * HB;
   const uint64_t hi = min(lo + HB, a.n);
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += HT) {
-    const uint32_t k = subject_key(a, i);
-    ckey[i] = k;
-    if (k != NOSUBJ) atomicAdd(&h[k >> 1], 1u << ((k & 1u) * 16u));
+  // HU frames per thread and step, their loads issued together (frame
+  // base + u * HT + tid: each load instruction reads consecutive frames; a
+  // step of four had left the pass waiting on load latency, 37 us)
+  constexpr int HU = 16;
+  for (uint64_t b0 = lo; b0 < hi; b0 += HU * HT) {
+    uint32_t k[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const uint64_t i = b0 + (uint64_t)(u * HT) + threadIdx.x;
+      k[u] = i < hi ? subject_key(a, i) : NOSUBJ;
+    }
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const uint64_t i = b0 + (uint64_t)(u * HT) + threadIdx.x;
+      if (!a.keys_in && i < hi) ckey[i] = k[u];
+      if (k[u] != NOSUBJ) atomicAdd(&h[k[u] >> 1], 1u << ((k[u] & 1u) * 16u));
+    }
   }
   __syncthreads();
   uint32_t *row = bh + (uint64_t)blockIdx.x * words;
@@ -147,7 +200,7 @@ __global__ __launch_bounds__(HT) void permit_hist(PermitArgs a, uint32_t *ckey, 
 
 // S: one thread per bucket, down its column of the histogram table
 __global__ __launch_bounds__(PT) void permit_scan(PermitArgs a, const uint32_t *bh, uint32_t nblk,
-                                                  uint32_t *lim, uint32_t *need, uint32_t *pend,
+                                                  uint32_t *lim, uint32_t *need, uint16_t *code,
                                                   uint32_t *blk_flag) {
   const uint32_t b = blockIdx.x * PT + threadIdx.x;
   if (b >= a.hash_size) return;
@@ -156,12 +209,12 @@ __global__ __launch_bounds__(PT) void permit_scan(PermitArgs a, const uint32_t *
   const uint32_t t = a.tokens[b];
   uint32_t acc = 0, cstar = NOBLK, prior = 0;
   uint32_t c = 0;
-  for (; c + 8 <= nblk; c += 8) {
-    uint32_t v[8];
+  for (; c + 16 <= nblk; c += 16) {
+    uint32_t v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = col[(uint64_t)(c + u) * pitch];
+    for (int u = 0; u < 16; ++u) v[u] = col[(uint64_t)(c + u) * pitch];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       if (cstar == NOBLK && acc + v[u] >= t) {
         cstar = c + u;
         prior = acc;
@@ -177,66 +230,177 @@ __global__ __launch_bounds__(PT) void permit_scan(PermitArgs a, const uint32_t *
     }
     acc += v;
   }
-  uint32_t l = LIM_ALL, p = NOBLK;
+  uint16_t cd = CODE_ALL;
   if (acc > t) {
     if (t == 0) {
-      l = 0;
+      cd = CODE_NONE;
+      lim[b] = 0;
     } else {   // the T_b-th frame lies in block cstar: resolved by permit_resolve
-      p = cstar;
+      cd = (uint16_t)cstar;
       need[b] = t - prior;
       blk_flag[cstar] = 1;
     }
   }
-  lim[b] = l;
-  pend[b] = p;
+  code[b] = cd;
   a.tokens[b] = t > acc ? t - acc : 0u;
 }
 
-// R: the blocks holding some bucket's T_b-th frame walk their frames in
-// order.  All threads stage a chunk's keys (only frames of buckets pending
-// in this block; ~0 else) and their need_b; wave 0 ranks them in frame
-// order: per distinct bucket of a 64-frame step one ballot, the rank base
-// from an LDS counter (u16 pairs), and the lane whose rank reaches need_b
-// sets lim[b].
-__global__ __launch_bounds__(HT) void permit_resolve(PermitArgs a, const uint32_t *ckey,
-                                                     const uint32_t *need, const uint32_t *pend,
-                                                     const uint32_t *blk_flag, uint32_t *lim) {
-  if (blk_flag[blockIdx.x] == 0) return;
-  __shared__ uint32_t cnt[HMAX / 2];
-  __shared__ uint32_t sk[RCH], sn[RCH];
+// Stage code[0, hash_size) into LDS (as 32-bit pairs).
+__device__ __forceinline__ void stage_code(const PermitArgs &a, const uint16_t *code, uint16_t *tab) {
   const uint32_t words = hwords(a.hash_size);
-  for (uint32_t w = threadIdx.x; w < words; w += HT) cnt[w] = 0;
+  const uint32_t *src = (const uint32_t *)code;
+  uint32_t *dst = (uint32_t *)tab;
+  for (uint32_t w = threadIdx.x; w < words; w += HT) dst[w] = src[w];
+}
+
+// R: the blocks holding some bucket's T_b-th frame.  code[] is staged in
+// LDS.  A: every thread takes 64 consecutive frames of the block and marks
+// its candidates (frames of a bucket b with code[b] == this block); their
+// buckets' LDS entries then become rem[b] = need_b; after a block scan of
+// the counts the candidates are appended in frame order to the block's
+// slice of a list (frame offset in the block << 16 | bucket).  B: every
+// wave walks the list, 64 candidates a step, acting on its sixteenth of the
+// buckets: per distinct bucket of the step one ballot; the lane at rank
+// rem[b] sets lim[b]; rem[b] drops by the step's count (0: resolved).  Only
+// the candidates are walked in order, and the walk waits on nothing but
+// the list.
+constexpr int RPER = 64;   // frames per thread in pass A (HT * RPER >= HB)
+static_assert(HT * RPER >= (int)HB, "one pass over a histogram block");
+
+__global__ __launch_bounds__(HT) void permit_resolve(PermitArgs a, const uint32_t *ckey,
+                                                     const uint32_t *need, const uint16_t *code,
+                                                     const uint32_t *blk_flag, uint32_t *clist,
+                                                     uint32_t *lim) {
+  if (blk_flag[blockIdx.x] == 0) return;
+  __shared__ uint16_t tab[HMAX];   // code[b], then rem[b] for this block's buckets
+  __shared__ uint32_t wsum[HT / 64];
+  stage_code(a, code, tab);
   const uint32_t c = blockIdx.x;
   const uint64_t lo = (uint64_t)c * HB;
   const uint64_t hi = min(lo + HB, a.n);
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (uint64_t s0 = lo; s0 < hi; s0 += RCH) {
-    __syncthreads();   // (the walk of the previous chunk is done with sk/sn)
-    for (int j = threadIdx.x; j < RCH; j += HT) {
-      const uint64_t i = s0 + (uint64_t)j;
-      uint32_t k = i < hi ? ckey[i] : NOSUBJ;
-      if (k != NOSUBJ && pend[k] != c) k = NOSUBJ;
-      sk[j] = k;
-      sn[j] = k != NOSUBJ ? need[k] : 0u;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t f0 = lo + (uint64_t)threadIdx.x * RPER;
+  __syncthreads();
+  // A1: this thread's candidates (bit j: frame f0 + j), 16 frames per round
+  uint64_t mask = 0;
+#pragma unroll
+  for (int j0 = 0; j0 < RPER; j0 += 16) {
+    uint32_t k[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const uint64_t i = f0 + (uint64_t)(j0 + u);
+      k[u] = i < hi ? key_at(a, ckey, i) : NOSUBJ;
     }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      for (int st = 0; st < RCH; st += 64) {
-        const uint32_t k = sk[st + lane];
-        uint64_t todo = __ballot(k != NOSUBJ);
-        while (todo) {
-          const int leader = __ffsll((unsigned long long)todo) - 1;
-          const uint32_t b = __shfl(k, leader);
-          const uint64_t m = __ballot(k == b);
-          const uint32_t sh = (b & 1u) * 16u;
-          const uint32_t base = (cnt[b >> 1] >> sh) & 0xffffu;
-          if (k == b && base + (uint32_t)__popcll(m & lt) + 1u == sn[st + lane])
-            lim[b] = (uint32_t)(s0 + (uint64_t)(st + lane)) + 1u;
-          if (lane == leader)
-            cnt[b >> 1] += (uint32_t)__popcll(m) << sh;   // (one wave: no atomics)
-          todo &= ~m;
-        }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (k[u] != NOSUBJ && tab[k[u]] == (uint16_t)c) mask |= 1ull << (j0 + u);
+  }
+  __syncthreads();   // every candidate test has read tab[] as code
+  for (uint64_t m = mask; m; m &= m - 1) {   // code -> rem (same value from every candidate)
+    const uint32_t k = key_at(a, ckey, f0 + (uint64_t)(__ffsll((unsigned long long)m) - 1));
+    tab[k] = (uint16_t)need[k];
+  }
+  // A2: block exclusive scan of the counts
+  const uint32_t cnt = (uint32_t)__popcll(mask);
+  uint32_t inc = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(inc, d);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (int w = 0; w < HT / 64; ++w) {
+    const uint32_t v = wsum[w];
+    base += w < wv ? v : 0u;
+    total += v;
+  }
+  base += inc - cnt;
+  // A3: append in frame order
+  uint32_t *list = clist + lo;
+  for (uint64_t m = mask; m; m &= m - 1) {
+    const int j = __ffsll((unsigned long long)m) - 1;
+    const uint32_t k = key_at(a, ckey, f0 + (uint64_t)j);
+    list[base++] = (uint32_t)(threadIdx.x * RPER + j) << 16 | k;
+  }
+  __syncthreads();   // (the list and rem[] are complete for the block)
+  // B: the ordered walk; wave w takes the buckets b with b % 16 == w (their
+  // candidates keep their order), so the per-bucket steps run 16 waves wide
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint32_t s0 = 0; s0 < total; s0 += 64) {
+    const uint32_t e = s0 + (uint32_t)lane < total ? list[s0 + lane] : NOSUBJ;
+    const uint32_t k = e & 0xffffu;
+    const bool on = e != NOSUBJ && (k & (HT / 64 - 1)) == (uint32_t)wv;
+    uint64_t todo = __ballot(on);
+    while (todo) {
+      const int leader = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t b = __shfl(k, leader);
+      const uint64_t m = __ballot(on && k == b);
+      const uint32_t r0 = tab[b];
+      const uint32_t pc = (uint32_t)__popcll(m);
+      if (r0 != 0) {
+        if (on && k == b && (uint32_t)__popcll(m & lt) + 1u == r0)
+          lim[b] = (uint32_t)(lo + (e >> 16)) + 1u;
+        if (lane == leader) tab[b] = (uint16_t)(r0 > pc ? r0 - pc : 0u);
+      }
+      todo &= ~m;
+    }
+  }
+}
+
+// V: verdicts in frame order, code[] staged in LDS per block (a persistent
+// grid: the 128 KB table is read once per CU, not once per 1024 frames):
+// key NOSUBJ -> 2; code ALL -> 1; NONE -> 0; else by the frame's block
+// against c*, and inside c* against lim[b] (the one global read left, only
+// for frames of a bucket's boundary block).  Four frames per thread and
+// step: one 4-byte verdict store when the verdict array's alignment allows.
+__device__ __forceinline__ uint32_t verdict_code(const PermitArgs &a, const uint16_t *tab,
+                                                 const uint32_t *lim, uint64_t i, uint32_t k) {
+  if (k == NOSUBJ) return 2u;
+  const uint32_t cd = tab[k];
+  if (cd == CODE_ALL) return 1u;
+  if (cd == CODE_NONE) return 0u;
+  const uint32_t blk = (uint32_t)(i / HB);
+  if (blk != cd) return blk < cd ? 1u : 0u;
+  return (uint32_t)i < lim[k] ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(HT) void permit_verdicts_tab(PermitArgs a, const uint32_t *ckey,
+                                                          const uint16_t *code,
+                                                          const uint32_t *lim) {
+  __shared__ uint16_t tab[HMAX];
+  stage_code(a, code, tab);
+  __syncthreads();
+  const bool aligned = ((uintptr_t)a.verdict & 3u) == 0;
+  const bool kvec = ((uintptr_t)(a.keys_in ? a.keys_in : ckey) & 15u) == 0;
+  // VU groups of four frames per thread and step, their key loads issued
+  // together (a step of one group waited on load latency: 22 us)
+  constexpr int VU = 4;
+  const uint64_t stride = 4 * (uint64_t)gridDim.x * HT;
+  for (uint64_t i0 = 4 * ((uint64_t)blockIdx.x * HT + threadIdx.x); i0 < a.n; i0 += VU * stride) {
+    uint32_t k[VU][4];
+#pragma unroll
+    for (int g = 0; g < VU; ++g) {
+      const uint64_t i = i0 + (uint64_t)g * stride;
+      if (i + 4 <= a.n) {
+        keys4(a, ckey, i, kvec, k[g]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) k[g][u] = i + u < a.n ? key_at(a, ckey, i + u) : NOSUBJ;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < VU; ++g) {
+      const uint64_t i = i0 + (uint64_t)g * stride;
+      if (i >= a.n) break;
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = verdict_code(a, tab, lim, i + u, k[g][u]);
+      if (aligned && i + 4 <= a.n) {
+        *(uint32_t *)(a.verdict + i) = v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24;
+      } else {
+        for (int u = 0; u < 4 && i + u < a.n; ++u) a.verdict[i + u] = (uint8_t)v[u];
       }
     }
   }
@@ -372,7 +536,8 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // sort-free path scratch: dense keys, the histogram table, per-bucket lim /
 // need / pend, per-block flags
 struct HistScratch {
-  uint32_t *ckey, *bh, *lim, *need, *pend, *blk_flag;
+  uint32_t *ckey, *bh, *lim, *need, *blk_flag, *clist;
+  uint16_t *code;
   uint32_t nblk;
   size_t total;
 };
@@ -391,8 +556,9 @@ void hist_layout(uint64_t n, uint32_t hash_size, void *base, HistScratch &s) {
   s.bh = take((size_t)s.nblk * words * 4);
   s.lim = take((size_t)hash_size * 4);
   s.need = take((size_t)hash_size * 4);
-  s.pend = take((size_t)hash_size * 4);
+  s.code = (uint16_t *)take((size_t)hash_size * 2 + 4);
   s.blk_flag = take((size_t)s.nblk * 4);
+  s.clist = take(n * 4);
   s.total = off;
 }
 
@@ -431,7 +597,7 @@ unsigned blocks(uint64_t n) { return (unsigned)((n + PT - 1) / PT); }
 }  // namespace
 
 size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
-  if (hash_size <= HMAX) {
+  if (hash_size <= HMAX && (n + HB - 1) / HB <= MAX_BLOCKS) {
     HistScratch h;
     hist_layout(n, hash_size, nullptr, h);
     return h.total;
@@ -443,16 +609,18 @@ size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
 
 hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   if (a.n == 0) return hipSuccess;
-  if (a.hash_size <= HMAX) {
+  if (a.hash_size <= HMAX && (a.n + HB - 1) / HB <= MAX_BLOCKS) {
     HistScratch h;
     hist_layout(a.n, a.hash_size, scratch, h);
     hipLaunchKernelGGL(permit_hist, dim3(h.nblk), dim3(HT), 0, st, a, h.ckey, h.bh, h.blk_flag);
     hipLaunchKernelGGL(permit_scan, dim3(blocks(a.hash_size)), dim3(PT), 0, st, a, h.bh, h.nblk,
-                       h.lim, h.need, h.pend, h.blk_flag);
-    hipLaunchKernelGGL(permit_resolve, dim3(h.nblk), dim3(HT), 0, st, a, h.ckey, h.need, h.pend,
-                       h.blk_flag, h.lim);
-    hipLaunchKernelGGL(permit_verdicts, dim3(blocks((a.n + 3) / 4)), dim3(PT), 0, st, a, h.ckey,
-                       h.lim);
+                       h.lim, h.need, h.code, h.blk_flag);
+    hipLaunchKernelGGL(permit_resolve, dim3(h.nblk), dim3(HT), 0, st, a, h.ckey, h.need, h.code,
+                       h.blk_flag, h.clist, h.lim);
+    // one block per CU holds the 128 KB table (a persistent grid)
+    const unsigned vb = (unsigned)std::min<uint64_t>((a.n + 4 * HT - 1) / (4 * HT),
+                                                     (uint64_t)std::max(1, a.ncu));
+    hipLaunchKernelGGL(permit_verdicts_tab, dim3(vb), dim3(HT), 0, st, a, h.ckey, h.code, h.lim);
     return hipGetLastError();
   }
   PermitScratch s;

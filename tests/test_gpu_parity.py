@@ -143,8 +143,21 @@ def test_binned_order_and_hash_out(name, dev):
 GROUP_MAX_LEN = [113, 1521]   # rx_internal.h kGroupMaxLen
 
 
+BIN_SHORT_PCT = 40            # rx_internal.h kBinShortPct
+
+
 def _group_of(lens):
     return np.searchsorted(np.array(GROUP_MAX_LEN), lens.astype(np.int64), side="left")
+
+
+def _mixed_perm(lens):
+    """The processing order pptk_rx_batch_device_mixed reports: binned
+    (stable by length group) when at least BIN_SHORT_PCT % of the frames are
+    in group 0, else batch order (the adaptive plan, rx_internal.h)."""
+    g = _group_of(lens)
+    if (g == 0).sum() * 100 >= BIN_SHORT_PCT * len(lens):
+        return np.argsort(g, kind="stable")
+    return np.arange(len(lens))
 
 
 def _run_mixed(ctx, z, dev, shift=0, max_len=0):
@@ -175,7 +188,7 @@ def test_mixed_length_groups(name, shift, max_len, dev):
     assert not d, d
     want = as_records(z["recs"])
     assert np.array_equal(h, np.where(want["flags"] & F_PARSED, want["flow_hash"], 0))
-    assert np.array_equal(perm, np.argsort(_group_of(z["len"]), kind="stable"))
+    assert np.array_equal(perm, _mixed_perm(z["len"]))
 
 
 class _HipBuf:
@@ -237,7 +250,7 @@ def test_mixed_empty_trailing_groups_perm_own_allocation(dev):
         perm.free()
     d = diff_records(recs.cpu().numpy().reshape(-1), want)
     assert not d, d
-    assert np.array_equal(got_perm, np.argsort(_group_of(lens), kind="stable"))
+    assert np.array_equal(got_perm, _mixed_perm(lens))
 
 
 def _frame_of_len(fg, rng, L):
@@ -280,7 +293,38 @@ def test_mixed_every_group_boundary(dev):
     got, _, perm = _run_mixed(_ctx(z), z, dev, shift=3)
     d = diff_records(got, want)
     assert not d, d
-    assert np.array_equal(perm, np.argsort(_group_of(lens), kind="stable"))
+    assert np.array_equal(perm, _mixed_perm(lens))
+
+
+@pytest.mark.parametrize("short_pct", [0, 39, 40, 100])
+def test_mixed_adaptive_plan(short_pct, dev):
+    """The adaptive plan at and around its threshold: 2 000 frames of which
+    short_pct % are at most 113 bytes (the rest 114-1500, in random order):
+    binned (stable by group) from kBinShortPct = 40 %, batch order below --
+    records bit-exact against the oracle either way."""
+    import framegen
+    from oracle.oracle import Oracle, make_opts
+    rng = np.random.default_rng(4000 + short_pct)
+    n = 2000
+    nshort = n * short_pct // 100
+    sizes = np.concatenate([rng.integers(60, 114, nshort), rng.integers(114, 1501, n - nshort)])
+    rng.shuffle(sizes)
+    frames = [_frame_of_len(framegen, rng, int(L)) for L in sizes]
+    off = np.cumsum([0] + [(len(f) + 3) & ~3 for f in frames[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(off[-1]) + len(frames[-1]) + 64, np.uint8)
+    for i, f in enumerate(frames):
+        buf[int(off[i]):int(off[i]) + len(f)] = np.frombuffer(f, np.uint8)
+    lens = np.array([len(f) for f in frames], np.uint16)
+    key = bytes(range(1, 17))
+    want = Oracle().rx_batch(buf, off, lens, opts=make_opts(key, 24, 48, 1 << 12))
+    z = {"buf": buf, "off": off, "len": lens, "key": np.frombuffer(key, np.uint8),
+         "iphash": np.array([24, 48, 1 << 12])}
+    got, h, perm = _run_mixed(_ctx(z), z, dev, max_len=1500)
+    d = diff_records(got, want)
+    assert not d, d
+    binned = short_pct >= BIN_SHORT_PCT
+    assert np.array_equal(perm, _mixed_perm(lens))
+    assert (perm != np.arange(n)).any() == (binned and 0 < short_pct < 100)
 
 
 @pytest.mark.parametrize("name", ["edge", "cmix"])

@@ -7,6 +7,8 @@
 //   C1500 1500 B IPv4/TCP (doff 5), 1446 B random payload
 //   CMIX  64..1500 B, 70 % IPv4 / 30 % IPv6, 50/50 TCP/UDP, 25 % 802.1Q,
 //         5 % IPv4 with IHL > 5, 2 % IPv6 with one hop-by-hop header
+//   IMIX  the classic 7:4:1 mix of 64 / 576 / 1500 B frames, otherwise as
+//         CMIX (a short frame grows to its headers' minimum, <= 102 B)
 // Checksums are computed here by a plain per-thread big-endian word sum
 // (independent of the product kernel).  About 1 % of frames are corrupted
 // (half in the IPv4 header, half in the L4 bytes); `expect` receives, per
@@ -53,7 +55,7 @@ __device__ uint64_t be_sum(const Writer &w, int a, int b) {
   return s;
 }
 
-enum { CFG_C64 = 0, CFG_C1500 = 1, CFG_CMIX = 2 };
+enum { CFG_C64 = 0, CFG_C1500 = 1, CFG_CMIX = 2, CFG_IMIX = 3 };
 
 // Shape of frame `gi`: everything that determines its length.
 struct Shape {
@@ -66,9 +68,13 @@ __device__ Shape shape_of(int cfg, uint64_t seed, uint64_t gi) {
   if (cfg == CFG_C1500) {
     sh.total = 1500;
     sh.proto = 6;
-  } else if (cfg == CFG_CMIX) {
+  } else if (cfg == CFG_CMIX || cfg == CFG_IMIX) {
     Rng r{mix64(seed ^ (gi * 0xd1b54a32d192ed03ULL)) ^ 0x51e5};
-    const uint32_t size = 64 + r.below(1437);
+    uint32_t size = 64 + r.below(1437);
+    if (cfg == CFG_IMIX) {
+      const uint32_t u = size % 12;   // (the same draw, reused)
+      size = u < 7 ? 64 : u < 11 ? 576 : 1500;
+    }
     sh.proto = r.chance(500) ? 6 : 17;
     sh.vlan = r.chance(250);
     sh.v6 = r.chance(300);

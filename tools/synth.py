@@ -5,7 +5,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libpptksynth.so")
-CFG = {"c64": 0, "c1500": 1, "cmix": 2, "c1500a": 1, "c1500g": 1}
+CFG = {"c64": 0, "c1500": 1, "cmix": 2, "imix": 3, "c1500a": 1, "c1500g": 1}
 # c1500a: 1536-byte slots; c1500g: C1500 frames described by off/len arrays
 SEED = 0x5EED
 
@@ -26,7 +26,7 @@ def lib():
 
 
 def make_batch(cfg, n, device, first=0, seed=SEED, stream=None):
-    """Frames [first, first+n) of config `cfg` ('c64' | 'c1500' | 'cmix') in
+    """Frames [first, first+n) of config `cfg` ('c64' | 'c1500' | 'cmix' | 'imix') in
     HBM.  Returns dict(frames, n, stride | off+lens, expect, max_len)."""
     import torch
     c = CFG[cfg]
