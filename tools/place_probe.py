@@ -334,6 +334,59 @@ def txside(args):
           flush=True)
 
 
+def bursts(args):
+    """Does a longer record-write burst rescue a slow (frames, records)
+    pair?  Frame batches (each behind a spacer) x record buffers (each behind
+    a spacer), as bench.placed_buffers allocates them; per pair the rx launch
+    and the trivial read/write kernel (tools/rwmix.hip rw_kernel, non-
+    temporal) moving the same bytes with the records written in bursts of
+    4 KB per 96 KB tile (the rx kernel's flush), 16 KB per 4 tiles and 64 KB
+    per 16 tiles.  One JSON line: per pair the medians."""
+    import ctypes
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.rwmix import _lib
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    L = _lib()
+    hold, bs, rs = [], [], []
+    for k in range(args.batches):
+        if k:
+            hold.append(torch.empty(8 << 30, dtype=torch.uint8, device=dev))
+        bs.append(make_batch("c1500", n, dev, first=k * n))
+    for _ in range(args.matrix or 4):
+        hold.append(torch.empty(4 << 30, dtype=torch.uint8, device=dev))
+        rs.append(torch.zeros((n, 64), dtype=torch.uint8, device=dev))
+    sink = torch.zeros(64, dtype=torch.int32, device=dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    s = torch.cuda.current_stream(dev)
+    modes = [("rx", 0, 0), ("mix4k", 96000, 4096), ("mix16k", 4 * 96000, 16384),
+             ("mix64k", 16 * 96000, 65536)]
+    t = {}
+    torch.cuda.synchronize()
+    for rep in range(args.reps + 1):
+        for bi, b in enumerate(bs):
+            for ri, r in enumerate(rs):
+                for name, rb, wb in modes:
+                    a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    if name == "rx":
+                        ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=r)
+                    else:
+                        L.rwmix_run(b["frames"].data_ptr(), r.data_ptr(), n * 1500 // rb, rb, wb, 1,
+                                    ncu * 2, sink.data_ptr(), ctypes.c_void_p(s.cuda_stream))
+                    z.record()
+                    torch.cuda.synchronize()
+                    if rep:
+                        t.setdefault((bi, ri, name), []).append(a.elapsed_time(z))
+    out = {}
+    for (bi, ri, name), v in sorted(t.items()):
+        out.setdefault(f"{bi},{ri}", {})[name] = round(sorted(v)[len(v) // 2], 3)
+    print(json.dumps({"pairs": out}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-mb", type=float, default=16)
@@ -349,11 +402,14 @@ def main():
     ap.add_argument("--benchpath", action="store_true")
     ap.add_argument("--txplace", action="store_true")
     ap.add_argument("--txside", action="store_true")
+    ap.add_argument("--bursts", action="store_true")
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--spacer-gb", type=float, default=0.0,
                     help="matrix: allocate this many GB before every batch after the first "
                          "and before every record buffer")
     args = ap.parse_args()
+    if args.bursts:
+        return bursts(args)
     if args.matrix:
         return matrix(args)
     if args.policies:
