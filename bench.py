@@ -470,16 +470,22 @@ def mix_sol(b, recs, n):
 
 
 def binned_bench(ctx, b, n, dev, steps, warmup, recs=None):
-    """The binned CMIX path BASELINE.json names (configs[3], "lanes binned
-    by length"): pptk_rx_batch_device_mixed -- the device length binning
-    plus one launch per length group -- timed per batch, whole call (into
-    `recs`, the batch-order run's placed record buffer, when given)."""
+    """The mixed-size call BASELINE.json's configs[3] names ("lanes binned
+    by length"): pptk_rx_batch_device_mixed, timed per batch, whole call
+    (into `recs`, the batch-order run's placed record buffer, when given),
+    without d_perm (the processing order is not needed here; an untimed call
+    with d_perm reports whether this batch was binned)."""
     import torch
     if recs is None:
         recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-    perm = torch.empty(n, dtype=torch.int32, device=dev)
     scratch = torch.empty(ctx._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8, device=dev)
-    kw = dict(max_len=b["max_len"], recs=recs, perm=perm, scratch=scratch)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], max_len=b["max_len"], recs=recs,
+                           perm=perm, scratch=scratch)
+    p = perm[:min(n, 1 << 20)].cpu()
+    binned = bool((p != torch.arange(p.numel(), dtype=p.dtype)).any().item())
+    del perm
+    kw = dict(max_len=b["max_len"], recs=recs, scratch=scratch)
     for _ in range(max(warmup, 3)):
         ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], **kw)
     torch.cuda.synchronize(dev)
@@ -492,12 +498,11 @@ def binned_bench(ctx, b, n, dev, steps, warmup, recs=None):
     torch.cuda.synchronize(dev)
     ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
     ach = b["bytes"] / (ms * 1e-3) / 1e9
-    p = perm[:min(n, 1 << 20)].cpu()
-    binned = bool((p != torch.arange(p.numel(), dtype=p.dtype)).any().item())
     return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "ms_per_batch": round(ms, 4),
-            "workload": f"{b['cfg'].upper()}, pptk_rx_batch_device_mixed: device length histogram; "
-                        "binned (one launch per length group) when >= 40 % of the frames are "
-                        "<= 113 B, else batch order; records at the frames' own indices",
+            "workload": f"{b['cfg'].upper()}, pptk_rx_batch_device_mixed (max_len hint "
+                        f"{b['max_len']}): binned into length groups only when jumbo frames "
+                        "(> 1521 B) mix with shorter ones, else batch order; records at the "
+                        "frames' own indices",
             "binned_by_plan": binned,
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
@@ -1037,7 +1042,7 @@ def main():
 
     secondary = {}
     if not args.no_secondary and args.only is None:
-        for cfg in ("c64", "cmix", "imix"):
+        for cfg in ("c64", "cmix", "imix", "jmix"):
             r = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None, check,
                            args.settle, first=first, place=place)
             secondary[cfg] = summary(r, n)
@@ -1046,7 +1051,7 @@ def main():
                 if sol:
                     secondary[cfg]["roofline"]["mix_sol_ms"] = sol[0]
                     secondary[cfg]["roofline"]["mix_sol_frac"] = round(sol[0] / r["kernel_ms"], 4)
-            if cfg in ("cmix", "imix"):
+            if cfg in ("cmix", "imix", "jmix"):
                 secondary[cfg]["binned"] = binned_bench(ctx, r["_batch"], n, dev, args.steps,
                                                         args.warmup, recs=r["_recs"])
             if cfg == "c64" and not args.no_rec32:

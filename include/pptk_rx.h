@@ -245,20 +245,23 @@ int pptk_rx_bin_device(struct pptk_rx_ctx *ctx, const uint16_t *d_len,
                        uint64_t n, uint32_t *d_perm, void *d_scratch,
                        void *stream);
 
-/* Mixed-size batch in one call: pptk_rx_bin_device() into d_perm/d_scratch,
- * then one launch per length group (..113, ..1521 bytes, longer), each
- * streamed by the kernel shape sized for that group instead of every frame
- * by the shape of the longest.  (On MI355X the batch-order call,
- * pptk_rx_batch_device with d_off/d_len, is faster on mixed traffic: every
- * finer grouping measured slower, DESIGN.md "Binned CMIX".)  Requires d_len;
- * b->d_perm is ignored (d_perm receives the processing order).  b->max_len
- * (when nonzero) is a hint: the groups above it are folded into the group
- * that holds it (one launch fewer each; a wrong hint changes speed only).
- * Records land at d_recs[i] for frame i.  d_perm holds n u32, d_scratch
- * pptk_rx_bin_scratch_bytes(n) bytes (the binning's counters and group table,
- * and the frames' descriptors laid out in binned order, which the group
- * launches stream); both stay in use until the stream reaches the end of
- * the call. */
+/* Mixed-size batch in one call.  Length binning pays on MI355X only when a
+ * batch mixes jumbo frames (> 1521 bytes, which batch order would stream
+ * with the 64-lane jumbo shape) with shorter ones; every split of 64..1521 B
+ * frames into groups measured slower than batch order (DESIGN.md "Binned
+ * order").  So: with b->max_len (a hint) at most 1521 the call runs the
+ * batch in batch order, as pptk_rx_batch_device; otherwise a device pass
+ * counts the length groups (..113, ..1521 bytes, longer) and, when the
+ * batch holds frames of the last group and shorter ones, bins it
+ * (pptk_rx_bin_device into the permutation) and runs one launch per group,
+ * each streamed by the kernel shape sized for it; else batch order by the
+ * launch of the highest non-empty group.  Results are identical either way.
+ * Requires d_len; b->d_perm is ignored.  d_perm (nullable) receives the
+ * processing order: the binned permutation, or the identity.  d_scratch:
+ * pptk_rx_bin_scratch_bytes(n) bytes (counters, group table, the binned
+ * descriptors the group launches stream, and the permutation when d_perm
+ * is NULL); both stay in use until the stream reaches the end of the call.
+ * Records land at d_recs[i] for frame i. */
 int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *ctx,
                                const struct pptk_rx_dev_batch *b, uint32_t *d_perm,
                                void *d_scratch, void *stream);

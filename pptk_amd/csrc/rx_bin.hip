@@ -9,6 +9,8 @@
 // Reads 2 x 2 bytes and writes 4 bytes per frame: <1 % of the frame bytes
 // the transform itself reads.  The scan also leaves the group start table
 // (kGroups + 1 entries) behind the counters for the group launches.
+#include <algorithm>
+
 #include "rx_internal.h"
 
 namespace pptk {
@@ -85,9 +87,16 @@ __global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, u
   const uint32_t g = m / NB;
   if (threadIdx.x <= (unsigned)NB)
     table[threadIdx.x] = threadIdx.x < (unsigned)NB ? counts[threadIdx.x * g] : part[1023];
-  if (threadIdx.x == 0) {   // group 0 holds [0, start of group 1)
-    const uint64_t total = part[1023], short0 = NB > 1 ? counts[g] : total;
-    table[NB + 1] = !adaptive || short0 * 100u >= (uint64_t)kBinShortPct * total ? 1u : 0u;
+  if (threadIdx.x == 0) {   // the plan (rx_internal.h launch_bin)
+    const uint32_t total = part[1023];
+    const uint32_t last0 = counts[(NB - 1) * g];   // start of the last group
+    uint32_t top = 0;                              // highest non-empty group
+    for (int k = 0; k < NB; ++k) {
+      const uint32_t lo = counts[k * g], hi = k + 1 < NB ? counts[(k + 1) * g] : total;
+      if (hi > lo) top = (uint32_t)k;
+    }
+    const bool bin = !adaptive || (last0 < total && last0 > 0);
+    table[NB + 1] = bin ? 1u : top << 8;
   }
 }
 
@@ -103,7 +112,7 @@ __global__ __launch_bounds__(BT) void bin_scatter(const uint16_t *len, uint64_t 
   __shared__ uint32_t cursor[NB];
   __shared__ uint32_t wcnt[NWARP][NB];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (*plan == 0) {   // not binned: the identity order, no binned descriptors
+  if (!(*plan & 1u)) {   // not binned: the identity order, no binned descriptors
     const uint64_t lo = blockIdx.x * per_block, hi = min(lo + per_block, n);
     for (uint64_t i = lo + threadIdx.x; i < hi; i += BT) perm[i] = (uint32_t)i;
     return;
@@ -155,7 +164,29 @@ static size_t table_end(int grid) {
 }
 
 size_t bin_scratch_bytes(uint64_t n, int grid) {
-  return table_end(grid) + (size_t)n * (sizeof(uint64_t) + sizeof(uint16_t));
+  // + the permutation of a mixed call made without d_perm (16-byte aligned)
+  return table_end(grid) + (size_t)n * (sizeof(uint64_t) + sizeof(uint16_t)) + 16 +
+         (size_t)n * sizeof(uint32_t);
+}
+
+uint32_t *bin_perm(void *scratch, int grid, uint64_t n) {
+  const uintptr_t p = (uintptr_t)((uint8_t *)scratch + table_end(grid) +
+                                  (size_t)n * (sizeof(uint64_t) + sizeof(uint16_t)));
+  return (uint32_t *)((p + 15) & ~(uintptr_t)15);
+}
+
+namespace {
+__global__ __launch_bounds__(BT) void iota_kernel(uint32_t *perm, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BT)
+    perm[i] = (uint32_t)i;
+}
+}  // namespace
+
+hipError_t launch_iota(uint32_t *perm, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((n + BT - 1) / BT, 4096);
+  hipLaunchKernelGGL(iota_kernel, dim3((unsigned)blocks), dim3(BT), 0, s, perm, n);
+  return hipGetLastError();
 }
 
 uint64_t *bin_desc_off(void *scratch, int grid) {

@@ -786,20 +786,30 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
                                uint32_t *d_perm, void *d_scratch, void *stream) {
   int rc = check_batch(c, b);
   if (rc || b->n == 0) return rc;
-  if (!b->d_len || !d_perm || !d_scratch) return -EINVAL;
+  if (!b->d_len || !d_scratch) return -EINVAL;
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   const hipStream_t s = (hipStream_t)stream;
-  // the binning also lays the descriptors out in binned order (scratch), so
-  // the group launches stream them instead of gathering them through d_perm
-  BinDesc bd{b->d_off, b->stride, bin_desc_off(d_scratch, kBinGrid),
-             bin_desc_len(d_scratch, kBinGrid, b->n)};
   const BinBounds &bb = bin_bounds();
   const bool dflt = default_bounds(bb);
-  hipError_t e = launch_bin(b->d_len, b->n, d_perm, d_scratch, s, kBinGrid, bd, bb, true);
+  if (b->max_len && b->max_len <= bb.b[kGroups - 2]) {
+    // Every frame fits the 1536-byte shape (by the hint; a wrong hint costs
+    // speed, never results): no length group is worth a launch of its own
+    // (DESIGN.md "Binned order"), so batch order, as pptk_rx_batch_device.
+    pptk_rx_dev_batch t = *b;
+    t.d_perm = nullptr;
+    if ((rc = pptk_rx_batch_device(c, &t, stream)) != 0) return rc;
+    return d_perm ? hip_err(launch_iota(d_perm, b->n, s)) : 0;
+  }
+  uint32_t *perm = d_perm ? d_perm : bin_perm(d_scratch, kBinGrid, b->n);
+  // the binning also lays the descriptors out in binned order (scratch), so
+  // the group launches stream them instead of gathering them through perm
+  BinDesc bd{b->d_off, b->stride, bin_desc_off(d_scratch, kBinGrid),
+             bin_desc_len(d_scratch, kBinGrid, b->n)};
+  hipError_t e = launch_bin(b->d_len, b->n, perm, d_scratch, s, kBinGrid, bd, bb, true);
   if (e != hipSuccess) return -EIO;
   RxKArgs a = batch_args(c, b);
-  a.perm = d_perm;
+  a.perm = perm;
   a.off = bd.boff;
   a.len = bd.blen;
   a.by_pos = 1;
@@ -817,11 +827,11 @@ int pptk_rx_batch_device_mixed(struct pptk_rx_ctx *c, const struct pptk_rx_dev_b
     int variant = fv >= 0 && fv != RX_L4 ? fv
                   : dflt || g == kGroups - 1 ? kGroupVariant[g]
                                              : pick_variant(bb.b[g] + 15);
-    // (the last launch also runs the whole batch when it is not binned:
+    // (a launch may run the whole batch when it is not binned:
     // pptk_rx_autotune's choice for its shape applies, as in batch order)
-    if (last && fv < 0 && c->tuned[1][variant] >= 0 && c->tuned[1][variant] != RX_L4)
+    if (fv < 0 && c->tuned[1][variant] >= 0 && c->tuned[1][variant] != RX_L4)
       variant = c->tuned[1][variant];
-    a.plan_all = last ? 1u : 0u;
+    a.plan_group = (uint32_t)g;
     a.range_lo = tab + g;
     a.range_hi = tab + (last ? kGroups : g + 1);
     a.tune = pick_tune(c, variant, true);

@@ -93,13 +93,13 @@ struct RxKArgs {
   // the per-frame status goes to rw_status
   uint32_t mss, mss_flags;
   // binned launches of pptk_rx_batch_device_mixed: the binning's plan word
-  // (device; 0 = the batch is not worth binning: batch order), the caller's
-  // own descriptors for that case (off0 nullable: stride), and whether this
-  // launch is the one that then takes every frame
+  // (device; bit 0 = binned; else bits 8-15 = the group whose launch runs
+  // the whole batch in batch order), the caller's own descriptors for that
+  // case (off0 nullable: stride), and this launch's group
   const uint32_t *plan;
   const uint64_t *off0;
   const uint16_t *len0;
-  uint32_t plan_all;
+  uint32_t plan_group;
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S
@@ -140,12 +140,12 @@ int rx_variant_blocks_per_cu(int variant);
 // bin_table(scratch, grid)[g] is the first position of group g in perm,
 // [kGroups] = n and [kGroups + 1] the plan word (device memory, written by
 // the launch).  With `adaptive` the binning first decides whether the batch
-// is worth binning at all: only if at least kBinShortPct % of its frames are
-// in group 0 (the short frames a small kernel shape streams many per round;
-// CMIX's uniform 64-1500 B has 3 %, IMIX 58 %).  Otherwise the plan word is
-// 0, perm is the identity and the group launches run the batch in batch
-// order (every split of a uniform mix measured slower: DESIGN.md).
-constexpr uint32_t kBinShortPct = 40;
+// is worth binning at all: only when it mixes frames of the last group
+// (> 1521 bytes: batch order would stream every frame with the jumbo shape)
+// with shorter ones.  Splitting 64..1521 B frames into groups was measured
+// slower than batch order for every mix tried (CMIX, IMIX; DESIGN.md "Binned
+// order"), so otherwise the plan word sends the whole batch, in batch order,
+// to the launch of its highest non-empty group (perm = identity).
 constexpr int kBinGrid = 2048;   // blocks of the binning sort (scratch layout)
 // Optional binned copy of the descriptors (boff/blen null: perm only).
 struct BinDesc {
@@ -162,6 +162,10 @@ struct BinBounds {
 hipError_t launch_bin(const uint16_t *len, uint64_t n, uint32_t *perm,
                       void *scratch, hipStream_t s, int grid, const BinDesc &bdesc,
                       const BinBounds &bounds, bool adaptive);
+// perm[i] = i (the processing order of a mixed call that runs batch order)
+hipError_t launch_iota(uint32_t *perm, uint64_t n, hipStream_t s);
+// the permutation inside the scratch (mixed calls without d_perm)
+uint32_t *bin_perm(void *scratch, int grid, uint64_t n);
 size_t bin_scratch_bytes(uint64_t n, int grid);
 const uint32_t *bin_table(const void *scratch, int grid);
 uint64_t *bin_desc_off(void *scratch, int grid);

@@ -874,11 +874,12 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // length-group launch (pptk_rx_batch_device_mixed): this launch owns
     // positions [*range_lo, *range_hi) of the binned order, known on the
     // device only
-    if (a.range_lo && a.plan && *a.plan == 0) {
-      // the binning found the batch not worth binning: the launch marked
-      // plan_all runs every frame in batch order from the caller's own
-      // descriptors (records in whole 4 KB runs), the others nothing
-      if (!a.plan_all) return;
+    if (a.range_lo && a.plan && !(*a.plan & 1u)) {
+      // the binning found the batch not worth binning: the launch of the
+      // group the plan names runs every frame in batch order from the
+      // caller's own descriptors (records in whole 4 KB runs), the others
+      // nothing
+      if (((*a.plan >> 8) & 0xffu) != a.plan_group) return;
       a.perm = nullptr;
       a.perm_ld = (const uint32_t *)a.zero;
       a.perm_msk = 0u;

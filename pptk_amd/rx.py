@@ -349,13 +349,13 @@ class RxContext:
 
     def batch_device_mixed(self, frames, n, off, lens, recs=None, hash_out=None, max_len=0,
                            perm=None, scratch=None, stream=None, frag_out=None):
-        """Mixed-size batch: device binning + one launch per length group
-        (asynchronous).  perm/scratch: optional preallocated device buffers."""
+        """Mixed-size batch (pptk_rx_batch_device_mixed, asynchronous): batch
+        order, or device binning + one launch per length group when the batch
+        mixes jumbo frames with shorter ones.  perm: optional device buffer
+        that receives the processing order; scratch: optional preallocated."""
         import torch
         if recs is None:
             recs = torch.empty((n, 64), dtype=torch.uint8, device=frames.device)
-        if perm is None:
-            perm = torch.empty(n, dtype=torch.int32, device=frames.device)
         if scratch is None:
             scratch = torch.empty(self._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
                                   device=frames.device)

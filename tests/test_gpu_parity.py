@@ -143,21 +143,22 @@ def test_binned_order_and_hash_out(name, dev):
 GROUP_MAX_LEN = [113, 1521]   # rx_internal.h kGroupMaxLen
 
 
-BIN_SHORT_PCT = 40            # rx_internal.h kBinShortPct
-
-
 def _group_of(lens):
     return np.searchsorted(np.array(GROUP_MAX_LEN), lens.astype(np.int64), side="left")
 
 
-def _mixed_perm(lens):
-    """The processing order pptk_rx_batch_device_mixed reports: binned
-    (stable by length group) when at least BIN_SHORT_PCT % of the frames are
-    in group 0, else batch order (the adaptive plan, rx_internal.h)."""
+def _mixed_perm(lens, max_len=0):
+    """The processing order pptk_rx_batch_device_mixed reports
+    (include/pptk_rx.h): batch order when the max_len hint is at most 1521;
+    otherwise binned (stable by length group) when the batch mixes frames
+    over 1521 bytes with shorter ones, else batch order."""
+    n = len(lens)
+    if max_len and max_len <= GROUP_MAX_LEN[-1]:
+        return np.arange(n)
     g = _group_of(lens)
-    if (g == 0).sum() * 100 >= BIN_SHORT_PCT * len(lens):
+    if (g == 2).any() and (g < 2).any():
         return np.argsort(g, kind="stable")
-    return np.arange(len(lens))
+    return np.arange(n)
 
 
 def _run_mixed(ctx, z, dev, shift=0, max_len=0):
@@ -188,7 +189,7 @@ def test_mixed_length_groups(name, shift, max_len, dev):
     assert not d, d
     want = as_records(z["recs"])
     assert np.array_equal(h, np.where(want["flags"] & F_PARSED, want["flow_hash"], 0))
-    assert np.array_equal(perm, _mixed_perm(z["len"]))
+    assert np.array_equal(perm, _mixed_perm(z["len"], max_len))
 
 
 class _HipBuf:
@@ -296,19 +297,25 @@ def test_mixed_every_group_boundary(dev):
     assert np.array_equal(perm, _mixed_perm(lens))
 
 
-@pytest.mark.parametrize("short_pct", [0, 39, 40, 100])
-def test_mixed_adaptive_plan(short_pct, dev):
-    """The adaptive plan at and around its threshold: 2 000 frames of which
-    short_pct % are at most 113 bytes (the rest 114-1500, in random order):
-    binned (stable by group) from kBinShortPct = 40 %, batch order below --
-    records bit-exact against the oracle either way."""
+@pytest.mark.parametrize("case", ["hint_1500", "no_jumbo", "few_jumbo", "all_jumbo",
+                                  "jumbo_no_perm"])
+def test_mixed_plan(case, dev):
+    """The mixed call's choice between batch order and binning (include/
+    pptk_rx.h): 2 000 frames of 60..1500 bytes, plus jumbo frames (1522..
+    9018 B) in some cases; records bit-exact against the oracle whatever the
+    choice, and the reported processing order is the one the rule names
+    (binned only for a mix of jumbo and shorter frames without a low max_len
+    hint; with d_perm NULL the binned permutation lives in the scratch)."""
     import framegen
     from oracle.oracle import Oracle, make_opts
-    rng = np.random.default_rng(4000 + short_pct)
+    rng = np.random.default_rng(sum(case.encode()))
     n = 2000
-    nshort = n * short_pct // 100
-    sizes = np.concatenate([rng.integers(60, 114, nshort), rng.integers(114, 1501, n - nshort)])
-    rng.shuffle(sizes)
+    sizes = rng.integers(60, 1501, n)
+    if case in ("few_jumbo", "jumbo_no_perm"):
+        sizes[rng.choice(n, 40, replace=False)] = rng.integers(1522, 9019, 40)
+    elif case == "all_jumbo":
+        sizes = rng.integers(1522, 9019, n)
+    max_len = 1500 if case == "hint_1500" else 0
     frames = [_frame_of_len(framegen, rng, int(L)) for L in sizes]
     off = np.cumsum([0] + [(len(f) + 3) & ~3 for f in frames[:-1]]).astype(np.uint64)
     buf = np.zeros(int(off[-1]) + len(frames[-1]) + 64, np.uint8)
@@ -319,12 +326,21 @@ def test_mixed_adaptive_plan(short_pct, dev):
     want = Oracle().rx_batch(buf, off, lens, opts=make_opts(key, 24, 48, 1 << 12))
     z = {"buf": buf, "off": off, "len": lens, "key": np.frombuffer(key, np.uint8),
          "iphash": np.array([24, 48, 1 << 12])}
-    got, h, perm = _run_mixed(_ctx(z), z, dev, max_len=1500)
+    ctx = _ctx(z)
+    if case == "jumbo_no_perm":
+        _keep, fr = _upload(buf, dev)
+        recs = ctx.batch_device_mixed(fr, n, torch.from_numpy(off.view(np.int64)).to(dev),
+                                      torch.from_numpy(lens.view(np.int16)).to(dev))
+        torch.cuda.synchronize()
+        d = diff_records(recs.cpu().numpy().reshape(-1), want)
+        assert not d, d
+        return
+    got, h, perm = _run_mixed(ctx, z, dev, max_len=max_len)
     d = diff_records(got, want)
     assert not d, d
-    binned = short_pct >= BIN_SHORT_PCT
-    assert np.array_equal(perm, _mixed_perm(lens))
-    assert (perm != np.arange(n)).any() == (binned and 0 < short_pct < 100)
+    expect = _mixed_perm(lens, max_len)
+    assert np.array_equal(perm, expect)
+    assert (perm != np.arange(n)).any() == (case == "few_jumbo")
 
 
 @pytest.mark.parametrize("name", ["edge", "cmix"])

@@ -363,7 +363,9 @@ def bursts(args):
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     s = torch.cuda.current_stream(dev)
     modes = [("rx", 0, 0), ("mix4k", 96000, 4096), ("mix16k", 4 * 96000, 16384),
-             ("mix64k", 16 * 96000, 65536)]
+             ("mix32k", 8 * 96000, 32768), ("mix64k", 16 * 96000, 65536),
+             ("mix128k", 32 * 96000, 131072), ("mix256k", 64 * 96000, 262144),
+             ("defer4", 96000, 4096), ("defer16", 96000, 4096)]
     t = {}
     torch.cuda.synchronize()
     for rep in range(args.reps + 1):
@@ -374,6 +376,10 @@ def bursts(args):
                     a.record()
                     if name == "rx":
                         ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=r)
+                    elif name.startswith("defer"):
+                        L.rwdefer_run(b["frames"].data_ptr(), r.data_ptr(), n * 1500 // rb, rb,
+                                      wb, int(name[5:]), ncu * 2, sink.data_ptr(),
+                                      ctypes.c_void_p(s.cuda_stream))
                     else:
                         L.rwmix_run(b["frames"].data_ptr(), r.data_ptr(), n * 1500 // rb, rb, wb, 1,
                                     ncu * 2, sink.data_ptr(), ctypes.c_void_p(s.cuda_stream))

@@ -119,6 +119,62 @@ extern "C" int sol_run(const void *in, const void *off, const void *len, uint64_
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// Deferred record writes: each wave reads G strided tiles (tile t, t +
+// nwaves, ...: the rx kernel's tile order) of rb bytes, keeping one 16-byte
+// value per tile, and only then writes the G tiles' wb-byte outputs, each at
+// its own tile's position (what an rx kernel that staged G tiles' records
+// before flushing them would write: clustered in time, not contiguous).
+template <int G>
+__global__ __launch_bounds__(256) void rw_defer_kernel(const u32x4 *in, u32x4 *out,
+                                                       uint64_t ntiles, uint32_t rb16,
+                                                       uint32_t wb16, uint32_t *sink) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  const uint64_t wid = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  u32x4 tot = {0, 0, 0, 0};
+  for (uint64_t t0 = wid; t0 < ntiles; t0 += nwaves * G) {
+    u32x4 acc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      acc[g] = (u32x4){0, 0, 0, 0};
+      const uint64_t t = t0 + (uint64_t)g * nwaves;
+      if (t >= ntiles) continue;
+      const u32x4 *p = in + t * rb16;
+      uint32_t k = lane;
+      for (; k + 7 * 64 < rb16; k += 8 * 64) {
+        u32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + k + u * 64);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[g] ^= v[u];
+      }
+      for (; k < rb16; k += 64) acc[g] ^= __builtin_nontemporal_load(p + k);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint64_t t = t0 + (uint64_t)g * nwaves;
+      if (t >= ntiles) continue;
+      u32x4 *q = out + t * (uint64_t)wb16;
+      for (uint32_t e = lane; e < wb16; e += 64) __builtin_nontemporal_store(acc[g], q + e);
+      tot ^= acc[g];
+    }
+  }
+  const uint32_t x = tot.x ^ tot.y ^ tot.z ^ tot.w;
+  if (x == 0x9e3779b9u) sink[lane] = x;
+}
+
+extern "C" int rwdefer_run(const void *in, void *out, uint64_t ntiles, uint32_t rb, uint32_t wb,
+                           int g, int grid, uint32_t *sink, void *stream) {
+  const hipStream_t s = (hipStream_t)stream;
+  if (g == 4)
+    hipLaunchKernelGGL(rw_defer_kernel<4>, dim3(grid), dim3(256), 0, s, (const u32x4 *)in,
+                       (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else
+    hipLaunchKernelGGL(rw_defer_kernel<16>, dim3(grid), dim3(256), 0, s, (const u32x4 *)in,
+                       (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int rwmix_run(const void *in, void *out, uint64_t ntiles, uint32_t rb, uint32_t wb,
                          int nt, int grid, uint32_t *sink, void *stream) {
   if (nt == 13)

@@ -25,6 +25,9 @@ def _lib():
     L.sol_run.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32,
                           ctypes.c_uint32, ctypes.c_int, ctypes.c_int, vp, vp]
     L.sol_run.restype = ctypes.c_int
+    L.rwdefer_run.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                              ctypes.c_int, ctypes.c_int, vp, vp]
+    L.rwdefer_run.restype = ctypes.c_int
     return L
 
 

@@ -9,6 +9,7 @@
 //         5 % IPv4 with IHL > 5, 2 % IPv6 with one hop-by-hop header
 //   IMIX  the classic 7:4:1 mix of 64 / 576 / 1500 B frames, otherwise as
 //         CMIX (a short frame grows to its headers' minimum, <= 102 B)
+//   JMIX  CMIX with 2 % of the frames 9000-byte jumbo frames
 // Checksums are computed here by a plain per-thread big-endian word sum
 // (independent of the product kernel).  About 1 % of frames are corrupted
 // (half in the IPv4 header, half in the L4 bytes); `expect` receives, per
@@ -55,7 +56,7 @@ __device__ uint64_t be_sum(const Writer &w, int a, int b) {
   return s;
 }
 
-enum { CFG_C64 = 0, CFG_C1500 = 1, CFG_CMIX = 2, CFG_IMIX = 3 };
+enum { CFG_C64 = 0, CFG_C1500 = 1, CFG_CMIX = 2, CFG_IMIX = 3, CFG_JMIX = 4 };
 
 // Shape of frame `gi`: everything that determines its length.
 struct Shape {
@@ -68,12 +69,14 @@ __device__ Shape shape_of(int cfg, uint64_t seed, uint64_t gi) {
   if (cfg == CFG_C1500) {
     sh.total = 1500;
     sh.proto = 6;
-  } else if (cfg == CFG_CMIX || cfg == CFG_IMIX) {
+  } else if (cfg == CFG_CMIX || cfg == CFG_IMIX || cfg == CFG_JMIX) {
     Rng r{mix64(seed ^ (gi * 0xd1b54a32d192ed03ULL)) ^ 0x51e5};
     uint32_t size = 64 + r.below(1437);
     if (cfg == CFG_IMIX) {
       const uint32_t u = size % 12;   // (the same draw, reused)
       size = u < 7 ? 64 : u < 11 ? 576 : 1500;
+    } else if (cfg == CFG_JMIX && size % 50 == 7) {   // (the same draw: 2 %)
+      size = 9000;
     }
     sh.proto = r.chance(500) ? 6 : 17;
     sh.vlan = r.chance(250);

@@ -5,7 +5,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libpptksynth.so")
-CFG = {"c64": 0, "c1500": 1, "cmix": 2, "imix": 3, "c1500a": 1, "c1500g": 1}
+CFG = {"c64": 0, "c1500": 1, "cmix": 2, "imix": 3, "jmix": 4, "c1500a": 1, "c1500g": 1}
 # c1500a: 1536-byte slots; c1500g: C1500 frames described by off/len arrays
 SEED = 0x5EED
 
@@ -26,7 +26,7 @@ def lib():
 
 
 def make_batch(cfg, n, device, first=0, seed=SEED, stream=None):
-    """Frames [first, first+n) of config `cfg` ('c64' | 'c1500' | 'cmix' | 'imix') in
+    """Frames [first, first+n) of config `cfg` ('c64' | 'c1500' | 'cmix' | 'imix' | 'jmix') in
     HBM.  Returns dict(frames, n, stride | off+lens, expect, max_len)."""
     import torch
     c = CFG[cfg]
@@ -58,7 +58,8 @@ def make_batch(cfg, n, device, first=0, seed=SEED, stream=None):
         frames = torch.empty(total, dtype=torch.uint8, device=device)
         rc = lib().synth_frames(c, seed, first, n, frames.data_ptr(), off.data_ptr(), 0,
                                 expect.data_ptr(), sp)
-        out.update(frames=frames, off=off, lens=lens, max_len=1500, bytes=int(ln.sum().item()))
+        out.update(frames=frames, off=off, lens=lens, max_len=9000 if cfg == "jmix" else 1500,
+                   bytes=int(ln.sum().item()))
     assert rc == 0, rc
     out["expect"] = expect
     return out
