@@ -345,7 +345,7 @@ def bursts(args):
     import ctypes
     import torch
     from pptk_amd.rx import RxContext
-    from tools.rwmix import _lib
+    from tools.rwmix import _lib, sol_ms
     from tools.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
@@ -365,8 +365,10 @@ def bursts(args):
     modes = [("rx", 0, 0), ("mix4k", 96000, 4096), ("mix16k", 4 * 96000, 16384),
              ("mix32k", 8 * 96000, 32768), ("mix64k", 16 * 96000, 65536),
              ("mix128k", 32 * 96000, 131072), ("mix256k", 64 * 96000, 262144),
-             ("defer4", 96000, 4096), ("defer16", 96000, 4096)]
-    t = {}
+             ("defer4", 96000, 4096), ("defer16", 96000, 4096),
+             ("stage1", 96000, 4096), ("stage2", 96000, 4096), ("stage4", 96000, 4096),
+             ("stage2s", 96000, 4096), ("sol", 96000, 4096)]
+    t, sol_how = {}, {}
     torch.cuda.synchronize()
     for rep in range(args.reps + 1):
         for bi, b in enumerate(bs):
@@ -376,6 +378,21 @@ def bursts(args):
                     a.record()
                     if name == "rx":
                         ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=r)
+                    elif name == "sol":
+                        if rep == 1:
+                            ms, how = sol_ms(b["frames"], n, r, 4096, rb=96000, reps=2)
+                            t[(bi, ri, name)] = [ms]
+                            sol_how[f"{bi},{ri}"] = how
+                        continue
+                    elif name.startswith("stage"):
+                        # stageN: 36 KB of header-image LDS as in the rx kernel;
+                        # stage2s: the same burst with no pad (occupancy bound by
+                        # the staging alone)
+                        if L.rwstage_run(b["frames"].data_ptr(), r.data_ptr(), n * 1500 // rb,
+                                         rb, wb, int(name[5]), 0 if name.endswith("s") else 36864,
+                                         ncu * 2, sink.data_ptr(),
+                                         ctypes.c_void_p(s.cuda_stream)):
+                            continue
                     elif name.startswith("defer"):
                         L.rwdefer_run(b["frames"].data_ptr(), r.data_ptr(), n * 1500 // rb, rb,
                                       wb, int(name[5:]), ncu * 2, sink.data_ptr(),
@@ -390,7 +407,7 @@ def bursts(args):
     out = {}
     for (bi, ri, name), v in sorted(t.items()):
         out.setdefault(f"{bi},{ri}", {})[name] = round(sorted(v)[len(v) // 2], 3)
-    print(json.dumps({"pairs": out}), flush=True)
+    print(json.dumps({"pairs": out, "sol_setting": sol_how}), flush=True)
 
 
 def main():

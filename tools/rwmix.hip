@@ -175,6 +175,65 @@ extern "C" int rwdefer_run(const void *in, void *out, uint64_t ntiles, uint32_t 
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// Workgroup-staged record writes: a workgroup (4 waves) owns runs of 4*TPW
+// consecutive tiles; each wave reads TPW of them (96 KB-style tiles of rb
+// bytes) and parks each tile's wb-byte output in LDS; after a barrier the
+// whole workgroup flushes the run's 4*TPW*wb bytes as one contiguous burst.
+// `pad` bytes of extra dynamic LDS emulate the rx kernel's header images
+// (occupancy).  This is the shape an rx kernel staging records in LDS would
+// have: bursts of 4*TPW tiles' records instead of one tile's.
+template <int TPW>
+__global__ __launch_bounds__(256) void rw_stage_kernel(const u32x4 *in, u32x4 *out,
+                                                       uint64_t ntiles, uint32_t rb16,
+                                                       uint32_t wb16, uint32_t *sink) {
+  extern __shared__ u32x4 stage[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  const uint64_t runs = ntiles / (4 * TPW);
+  u32x4 tot = {0, 0, 0, 0};
+  for (uint64_t run = blockIdx.x; run < runs; run += gridDim.x) {
+#pragma unroll
+    for (int g = 0; g < TPW; ++g) {
+      const uint32_t lt = (uint32_t)g * 4 + w;  // tile within the run
+      const u32x4 *p = in + (run * 4 * TPW + lt) * rb16;
+      u32x4 acc = {0, 0, 0, 0};
+      uint32_t k = lane;
+      for (; k + 7 * 64 < rb16; k += 8 * 64) {
+        u32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + k + u * 64);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= v[u];
+      }
+      for (; k < rb16; k += 64) acc ^= __builtin_nontemporal_load(p + k);
+      for (uint32_t e = lane; e < wb16; e += 64) stage[lt * wb16 + e] = acc;
+      tot ^= acc;
+    }
+    __syncthreads();
+    u32x4 *q = out + run * 4 * TPW * (uint64_t)wb16;
+    for (uint32_t e = threadIdx.x; e < 4 * TPW * wb16; e += 256)
+      __builtin_nontemporal_store(stage[e], q + e);
+    __syncthreads();
+  }
+  const uint32_t x = tot.x ^ tot.y ^ tot.z ^ tot.w;
+  if (x == 0x9e3779b9u) sink[lane] = x;
+}
+
+extern "C" int rwstage_run(const void *in, void *out, uint64_t ntiles, uint32_t rb, uint32_t wb,
+                           int tpw, uint32_t pad, int grid, uint32_t *sink, void *stream) {
+  const hipStream_t s = (hipStream_t)stream;
+  const size_t lds = (size_t)4 * tpw * wb + pad;
+  if (tpw == 1)
+    hipLaunchKernelGGL(rw_stage_kernel<1>, dim3(grid), dim3(256), lds, s, (const u32x4 *)in,
+                       (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else if (tpw == 2)
+    hipLaunchKernelGGL(rw_stage_kernel<2>, dim3(grid), dim3(256), lds, s, (const u32x4 *)in,
+                       (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else
+    hipLaunchKernelGGL(rw_stage_kernel<4>, dim3(grid), dim3(256), lds, s, (const u32x4 *)in,
+                       (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int rwmix_run(const void *in, void *out, uint64_t ntiles, uint32_t rb, uint32_t wb,
                          int nt, int grid, uint32_t *sink, void *stream) {
   if (nt == 13)

@@ -28,6 +28,9 @@ def _lib():
     L.rwdefer_run.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                               ctypes.c_int, ctypes.c_int, vp, vp]
     L.rwdefer_run.restype = ctypes.c_int
+    L.rwstage_run.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                              ctypes.c_int, ctypes.c_uint32, ctypes.c_int, vp, vp]
+    L.rwstage_run.restype = ctypes.c_int
     return L
 
 
