@@ -789,7 +789,8 @@ def mss_bench(ctx, n, dev, steps, warmup, stride=80):
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}}
 
 
-def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
+def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
+                 runs=("records", "keys", "keys_denying")):
     """Batched ip_permitted over a C64 batch: buckets of
     the /24 source prefixes in 2^16 buckets, every IPv4 frame a subject, one
     token array carried across the timed batches.  Three runs:
@@ -802,7 +803,9 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
     Roofline: the algorithmic bytes of a verdict are its 4-byte key read and
     1-byte verdict written (records: the 16-byte slice of the record the key
     is in -- a DRAM burst of 64 bytes is what the memory moves for it), plus
-    the token array read and written."""
+    the token array read and written; `traffic` is the committed PMC
+    summary's HBM bytes for that run (tools/opbench.py permit_<run>).
+    `runs` selects the runs (profiling: one run per PMC pass)."""
     import torch
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch
@@ -837,27 +840,36 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16):
         return ms, {"permitted": int((v == 1).sum()), "denied": int((v == 0).sum()),
                     "not_subject": int((v == 2).sum())}
 
-    def line(ms, per_frame_bytes, what, counts):
+    def line(ms, per_frame_bytes, what, counts, run):
         alg = n * per_frame_bytes + 2 * 4 * hash_size
         ach = alg / (ms * 1e-3) / 1e9
+        traffic, src = pmc_traffic("op_permit_" + run, n)
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": alg,
+                "traffic": traffic}
+        if src:
+            roof["traffic_source"] = src
         return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "ms_per_batch": round(ms, 4),
                 "frames": n, "hash_size": hash_size, "workload": what, "verdicts": counts,
-                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                             "algorithmic_bytes_per_launch": alg, "traffic": None}}
+                "roofline": roof}
 
     out = {}
-    ms, c = timed(lambda tok: ctx.permit_device(recs, 4, tok, verdict=verdict, scratch=scratch))
-    out = line(ms, 64 + 1, "C64 records (64 B each), IPv4 /24 buckets, all frames subject", c)
-    ms, c = timed(lambda tok: ctx.permit_keys_device(keys, 4, tok, verdict=verdict,
-                                                     scratch=scratch))
-    out["keys"] = line(ms, 4 + 1, "dense 4-byte keys of the same batch (d_key)", c)
-    ms, c = timed(lambda tok: ctx.permit_keys_device(keys, 4, tok, verdict=verdict,
-                                                     scratch=scratch),
-                  refill=lambda tok: tok.fill_(128))
-    out["keys_denying"] = line(ms, 4 + 1, "dense keys, 128 tokens per bucket before each batch "
-                                          "(~half the frames denied: resolve pass in every block)",
-                               c)
+    if "records" in runs:
+        ms, c = timed(lambda tok: ctx.permit_device(recs, 4, tok, verdict=verdict,
+                                                    scratch=scratch))
+        out = line(ms, 64 + 1, "C64 records (64 B each), IPv4 /24 buckets, all frames subject",
+                   c, "records")
+    if "keys" in runs:
+        ms, c = timed(lambda tok: ctx.permit_keys_device(keys, 4, tok, verdict=verdict,
+                                                         scratch=scratch))
+        out["keys"] = line(ms, 4 + 1, "dense 4-byte keys of the same batch (d_key)", c, "keys")
+    if "keys_denying" in runs:
+        ms, c = timed(lambda tok: ctx.permit_keys_device(keys, 4, tok, verdict=verdict,
+                                                         scratch=scratch),
+                      refill=lambda tok: tok.fill_(128))
+        out["keys_denying"] = line(ms, 4 + 1, "dense keys, 128 tokens per bucket before each "
+                                   "batch (~half the frames denied: resolve pass in every block)",
+                                   c, "keys_denying")
     del recs, keys, verdict, scratch
     torch.cuda.empty_cache()
     return out
@@ -884,7 +896,7 @@ def gather_bench(ctx, gb, ws, dev, steps):
 
 # the newest round's committed PMC summary (tools/pmc_summary.py)
 PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json")
-                                for r in ("r02", "r01")) if os.path.exists(p)),
+                                for r in ("r03", "r02", "r01")) if os.path.exists(p)),
                    os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"))
 
 
@@ -897,7 +909,7 @@ def pmc_traffic(cfg, frames):
     try:
         with open(PMC_SUMMARY) as f:
             e = json.load(f)[cfg]
-        return (int(e["traffic_bytes"] * frames / N_PER_GPU),
+        return (int(e.get("traffic_bytes_per_call", e["traffic_bytes"]) * frames / N_PER_GPU),
                 os.path.relpath(PMC_SUMMARY, ROOT))
     except (OSError, KeyError, ValueError):
         return None, None

@@ -142,6 +142,11 @@ def main():
     elif op == "permit":
         r = bench.permit_bench(n, dev, 1, 0, args.steps, args.warmup)
         r["changed_bytes_per_launch"] = n          # one verdict byte per frame
+    elif op.startswith("permit_"):   # one run of the rate limiter alone (PMC passes)
+        run = op[len("permit_"):]
+        r = bench.permit_bench(n, dev, 1, 0, args.steps, args.warmup, runs=(run,))
+        r = r.get(run, r)
+        r["changed_bytes_per_launch"] = n
     elif op == "binned":
         b = make_batch("cmix", n, dev)
         r = bench.binned_bench(ctx, b, n, dev, args.steps, args.warmup)

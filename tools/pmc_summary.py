@@ -86,12 +86,14 @@ def op_counter(d, cname, regex):
 
 
 def op_entry(spec):
-    """op:REGEX:CHANGED_BYTES=DIR_FETCH,DIR_WRITE -- a secondary op's HBM
-    traffic per launch and its write amplification (WRITE_SIZE bytes /
-    bytes the op must change)."""
+    """op:NAME:REGEX:CHANGED_BYTES[:CALLS]=DIR_FETCH,DIR_WRITE -- a secondary
+    op's HBM traffic per launch and its write amplification (WRITE_SIZE
+    bytes / bytes the op must change).  With CALLS (the op calls the run
+    made: an op may be several kernels), also the traffic per call."""
     head, dirs = spec.rsplit("=", 1)
-    head, changed = head.rsplit(":", 1)
-    regex = head.split(":", 2)[2]
+    parts = head.split(":")
+    calls = int(parts[4]) if len(parts) > 4 else 0
+    changed, regex = parts[3], parts[2]
     dirs = dirs.split(",")
     f, fd, names = op_counter(dirs[0], "FETCH_SIZE", regex)
     w, wd, _ = op_counter(dirs[1], "WRITE_SIZE", regex)
@@ -119,6 +121,9 @@ def op_entry(spec):
                            "read_bytes_per_launch": v["read"] / max(1, v["launches"]),
                            "write_bytes_per_launch": v["write"] / max(1, v["launches"])}
                        for k, v in per.items()}
+    if calls:
+        e["calls"] = calls
+        e["traffic_bytes_per_call"] = (sum(f) * 2 + sum(w)) * 1024 / calls
     e["changed_bytes"] = int(changed)
     e["write_amplification"] = round(e["hbm_write_bytes"] / int(changed), 2)
     return e
