@@ -461,13 +461,14 @@ int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
 // read/write-mix speed of light ~4.8 ms for C1500) T32S3D7 ran C1500 6 %
 // faster than T16S6; T16S6 was chosen where the mix costs ~4.0 ms.  The
 // 1536-byte class is the one measured.
-static int autotune_candidates(int variant, int cand[8]) {
+static int autotune_candidates(int variant, bool gather, int cand[8]) {
   int n = 0;
   cand[n++] = variant;
   if (variant == RX_T16S6) {
     cand[n++] = RX_T32S3;
     cand[n++] = RX_T32S3D7;
     cand[n++] = RX_T16S7L;
+    if (gather) cand[n++] = RX_M6;   // mixed lengths: lanes binned inside the tile
   }
   return n;
 }
@@ -482,7 +483,7 @@ int pptk_rx_autotune(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b, i
   const int base = auto_variant(b, nullptr);
   const int g = b->d_off || b->d_len || b->d_perm ? 1 : 0;
   int cand[8];
-  const int nc = autotune_candidates(base, cand);
+  const int nc = autotune_candidates(base, g == 1, cand);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
     (void)hipEventDestroy(e0);

@@ -111,6 +111,7 @@ enum RxVariant {
   RX_T32S3D7, RX_T16S6D1, // prefetch-depth experiments
   RX_T8S2, RX_T16S4,      // length-group shapes (256 and 1024 bytes)
   RX_L4,                  // lane kernel: fixed stride, 16-byte aligned frames <= 64 bytes
+  RX_M6,                  // mixed shapes: lanes binned by length inside each tile
   RX_NVARIANTS
 };
 

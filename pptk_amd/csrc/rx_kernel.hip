@@ -29,6 +29,8 @@
 //     2.(B)), which is bit-exact (DESIGN.md "Checksum invariants").
 #include "rx_internal.h"
 
+#include <type_traits>
+
 namespace pptk {
 
 namespace {
@@ -868,39 +870,44 @@ constexpr int min_waves() { return D == 1 && S * T >= 32 ? PPTK_RX_D1_WAVES : mi
 // D = rounds in flight; (D + 1) must divide T so that the prefetch ring is
 // back in its starting registers at the tile boundary (no moves of in-flight
 // load destinations, which would force vmcnt waits).
+// Length-group launch (pptk_rx_batch_device_mixed): this launch owns
+// positions [*range_lo, *range_hi) of the binned order, known on the device
+// only.  Returns false when the launch has nothing to do.
+__device__ __forceinline__ bool group_range(RxKArgs &a) {
+  if (a.range_lo && a.plan && !(*a.plan & 1u)) {
+    // the binning found the batch not worth binning: the launch of the
+    // group the plan names runs every frame in batch order from the
+    // caller's own descriptors (records in whole 4 KB runs), the others
+    // nothing
+    if (((*a.plan >> 8) & 0xffu) != a.plan_group) return false;
+    a.perm = nullptr;
+    a.perm_ld = (const uint32_t *)a.zero;
+    a.perm_msk = 0u;
+    a.off_ld = a.off0 ? a.off0 : (const uint64_t *)a.zero;
+    a.off_msk = a.off0 ? ~0u : 0u;
+    a.stride_g = a.off0 ? 0u : a.stride;
+    a.len_ld = a.len0;
+    a.len_msk = ~0u;
+    a.by_pos = 0;
+  } else if (a.range_lo) {
+    const uint32_t lo = *a.range_lo, hi = *a.range_hi;
+    a.perm_ld += lo;
+    if (a.by_pos) {
+      a.off_ld += lo;
+      a.len_ld += lo;
+    }
+    a.n = hi > lo ? hi - lo : 0;
+    // an empty group: perm_ld points one past the permutation, and even
+    // the clamped descriptor loads below would read it
+    if (a.n == 0) return false;
+  }
+  return true;
+}
+
 template <int T, int S, int D, int AL, bool NT, bool GATHER>
 __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(RxKArgs a) {
   if constexpr (GATHER) {
-    // length-group launch (pptk_rx_batch_device_mixed): this launch owns
-    // positions [*range_lo, *range_hi) of the binned order, known on the
-    // device only
-    if (a.range_lo && a.plan && !(*a.plan & 1u)) {
-      // the binning found the batch not worth binning: the launch of the
-      // group the plan names runs every frame in batch order from the
-      // caller's own descriptors (records in whole 4 KB runs), the others
-      // nothing
-      if (((*a.plan >> 8) & 0xffu) != a.plan_group) return;
-      a.perm = nullptr;
-      a.perm_ld = (const uint32_t *)a.zero;
-      a.perm_msk = 0u;
-      a.off_ld = a.off0 ? a.off0 : (const uint64_t *)a.zero;
-      a.off_msk = a.off0 ? ~0u : 0u;
-      a.stride_g = a.off0 ? 0u : a.stride;
-      a.len_ld = a.len0;
-      a.len_msk = ~0u;
-      a.by_pos = 0;
-    } else if (a.range_lo) {
-      const uint32_t lo = *a.range_lo, hi = *a.range_hi;
-      a.perm_ld += lo;
-      if (a.by_pos) {
-        a.off_ld += lo;
-        a.len_ld += lo;
-      }
-      a.n = hi > lo ? hi - lo : 0;
-      // an empty group: perm_ld points one past the permutation, and even
-      // the clamped descriptor loads below would read it
-      if (a.n == 0) return;
-    }
+    if (!group_range(a)) return;
   }
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * IMG_STRIDE];
   constexpr int IMGC = (S * T < IMG_CHUNKS) ? S * T : IMG_CHUNKS;  // chunks parked
@@ -1050,6 +1057,265 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     dc = dn;
     dn = d2;
     idx2 = idx3;
+  }
+}
+
+// ---- Mixed-shape kernel (RX_M6): lanes binned by length inside each tile.
+//
+// rx_kernel gives every frame of a tile a team round sized for the longest
+// frame the batch may hold (T16S6: 4 frames per round, 6 chunk loads per
+// lane), so a 64-byte frame of an IMIX tile costs as many load and sum
+// instructions as a 1500-byte one.  Here each tile's 64 frames are binned by
+// their chunk count into three classes, each run with rounds of the same
+// register shape -- 6 chunk loads per lane -- but a different team width:
+//   class 0: <= 24 chunks (<= 384-byte span), teams of 4 lanes, 16 frames/round
+//   class 1: <= 48 chunks (<= 768 bytes),     teams of 8 lanes,  8 frames/round
+//   class 2: anything longer,                 teams of 16 lanes, 4 frames/round
+// (longer than 96 chunks: the rest is summed in the lane phase, as the
+// unrolled team variants do).  The binning is a ballot per class and a
+// rank by mbcnt: the tile's frame indices are listed class by class in a
+// 64-byte LDS list (no global permutation, no extra HBM traffic); round r of
+// the tile runs list entries of one class.  Every round issues the same six
+// loads, so the prefetch ring of rx_kernel carries over unchanged: D = 3
+// rounds in flight in fixed register slots, the round count padded to a
+// multiple of 4 with empty rounds, and the next tile's schedule (built from
+// its descriptors, which run a tile ahead) known before the last round
+// group issues that tile's first rounds.  A round's team sum goes to the
+// frame's LDS slot (bytes 128..131 of its image), where the owning lane
+// reads it in the lane phase.  Frame i's record stays at its own index,
+// written in the tile's 4 KB run.  IMIX (7:4:1 of 64/576/1500 B) needs ~10
+// rounds per tile instead of 16.
+constexpr int M_S = 6;        // chunk loads per lane per round
+constexpr int M_D = 3;        // rounds in flight
+constexpr int M_SUM = 128;    // byte offset of a frame's team sum in its image slot
+static_assert(IMG_STRIDE >= M_SUM + 4, "the team sum lives past the 128-byte image");
+
+// A tile's schedule (wave-uniform): frames per class, and the round
+// boundaries -- class 0 runs rounds [0, e0), class 1 [e0, e1), class 2
+// [e1, e2), rounds [e2, P) are empty.
+struct MSched {
+  uint32_t n0, n1, n2, e0, e1, e2;
+};
+
+__device__ __forceinline__ uint32_t m_rank(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Bin the tile's frames (descriptor d per lane) and list their lanes class
+// by class in `list` (64 bytes of LDS).  Lanes past the batch are not
+// listed.  (Listing whole descriptors, 16 bytes each, read by one broadcast
+// LDS load per round instead of the lane index plus three shuffles,
+// measured slower: IMIX 1.62 vs 1.54 ms, CMIX +11 % vs +1.5 % against the
+// team kernel.)
+__device__ __forceinline__ MSched m_schedule(const Desc &d, int lane, LDS_AS uint8_t *list) {
+  const bool valid = d.idx != 0xffffffffu;
+  const uint32_t nch = ((uint32_t)(d.base & 15u) + d.len + 15u) >> 4;
+  const uint64_t b0 = __ballot(valid && nch <= 24u);
+  const uint64_t b1 = __ballot(valid && nch > 24u && nch <= 48u);
+  const uint64_t b2 = __ballot(valid && nch > 48u);
+  MSched s;
+  s.n0 = (uint32_t)__popcll(b0);
+  s.n1 = (uint32_t)__popcll(b1);
+  s.n2 = (uint32_t)__popcll(b2);
+  s.e0 = (s.n0 + 15u) >> 4;
+  s.e1 = s.e0 + ((s.n1 + 7u) >> 3);
+  s.e2 = s.e1 + ((s.n2 + 3u) >> 2);
+  const uint32_t pos = nch <= 24u ? m_rank(b0)
+                       : nch <= 48u ? s.n0 + m_rank(b1)
+                                    : s.n0 + s.n1 + m_rank(b2);
+  if (valid) list[pos] = (uint8_t)lane;
+  return s;
+}
+
+// Rounds the tile runs: the schedule's, padded to whole groups of D + 1,
+// and at least two groups -- the group loop then runs at least once, so the
+// compiler has no zero-trip path on which it would copy the ring's in-flight
+// registers (a vmcnt(0) drain at every such tile).
+__device__ __forceinline__ uint32_t m_rounds(const MSched &s) {
+  return s.e2 <= (uint32_t)(2 * (M_D + 1)) ? (uint32_t)(2 * (M_D + 1))
+                                           : (s.e2 + (uint32_t)M_D) & ~(uint32_t)M_D;
+}
+
+// log2 of the team width of round r (wave-uniform).
+__device__ __forceinline__ int m_tl(const MSched &s, uint32_t r) {
+  return r < s.e0 ? 2 : r < s.e1 ? 3 : 4;
+}
+
+// Team sum of a round, complete in the team's LAST lane (lane T - 1 of the
+// team), by DPP adds inside each row of 16 lanes -- no LDS crossbar traffic:
+// quad_perm [1,0,3,2] and [2,3,0,1] sum each quad (every lane of it), then
+// row_shr:4 and row_shr:8 fold the quads of an 8- or 16-lane team into its
+// last lane (lanes whose source lies outside the row add 0).
+template <int CTRL>
+__device__ __forceinline__ uint32_t m_dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t m_team_sum(uint32_t x, int tl) {
+  x += m_dpp<0xb1>(x);   // quad_perm [1,0,3,2]
+  x += m_dpp<0x4e>(x);   // quad_perm [2,3,0,1]
+  const uint32_t x8 = x + m_dpp<0x114>(x);    // row_shr:4
+  x = tl >= 3 ? x8 : x;
+  const uint32_t x16 = x + m_dpp<0x118>(x);   // row_shr:8
+  return tl >= 4 ? x16 : x;
+}
+
+struct MBuf {
+  u32x4 v[M_S];
+  // packed: bits 0-7 the frame's lane in the tile (0xff: no frame, an empty
+  // team), 8-11 the frame start inside its chunk, 16-31 the frame length
+  uint32_t qml;
+};
+
+template <bool NT>
+__device__ __forceinline__ MBuf m_load_round(const RxKArgs &a, const Desc &d, const MSched &s,
+                                             const LDS_AS uint8_t *list, uint32_t r, int lane) {
+  const int tl = m_tl(s, r);
+  const uint32_t first = r < s.e0 ? 0u : r < s.e1 ? s.n0 : s.n0 + s.n1;
+  const uint32_t cnt = r < s.e0 ? s.n0 : r < s.e1 ? s.n1 : s.n2;
+  const uint32_t r0 = r < s.e0 ? 0u : r < s.e1 ? s.e0 : s.e1;
+  // this team's entry of the class: (r - r0) * (64 >> tl) + team
+  const uint32_t k = ((r - r0) << (6 - tl)) + ((uint32_t)lane >> tl);
+  const bool real = k < cnt;
+  // (an empty team reads some lane's frame: every lane describes a valid
+  // frame, lanes past the batch frame 0)
+  const uint32_t q = (uint32_t)list[real ? first + k : 0u] & (WAVE - 1);
+  MBuf b;
+  // both shuffles unconditional: a ds_bpermute executed under a lane mask
+  // reads 0 from every source lane outside the mask
+  const uint64_t pb = __shfl(d.base, (int)q);
+  const uint32_t pl = __shfl(d.len, (int)q) & (0u - (uint32_t)real);
+  const int m = (int)(pb & 15u);
+  b.qml = (real ? q : 0xffu) | ((uint32_t)m << 8) | (pl << 16);
+  const u32x4 *c0 = (const u32x4 *)(a.frames + (pb - (uint64_t)m));
+  const int nch = (m + (int)pl + 15) >> 4;
+  const int clast = nch > 0 ? nch - 1 : 0;
+  const int j = lane & ((1 << tl) - 1);
+#pragma unroll
+  for (int i = 0; i < M_S; ++i)
+    b.v[i] = ldc<NT>(c0 + min((i << tl) + j, clast));   // unconditional (see load_round)
+  return b;
+}
+
+template <bool NT, bool GATHER>
+__global__ __launch_bounds__(WAVE * WPB, 2) void rx_kernel_mixed(RxKArgs a) {
+  if constexpr (GATHER) {
+    if (!group_range(a)) return;
+  }
+  __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * IMG_STRIDE];
+  __shared__ uint8_t lists[WPB][2][WAVE];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = threadIdx.x / WAVE;
+  LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * IMG_STRIDE;
+  LDS_AS uint8_t *lst[2] = {(LDS_AS uint8_t *)lists[wv][0], (LDS_AS uint8_t *)lists[wv][1]};
+  const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
+  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+  const bool blocked = a.tune & 256u;
+  const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
+  const uint64_t per = (ntiles + nwaves - 1) / nwaves;
+  const uint64_t step = blocked ? 1 : nwaves;
+  const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
+
+  uint64_t tile = blocked ? wid * per : wid;
+  Desc dc = load_desc<GATHER>(a, tile, lane);
+  Desc dn = load_desc<GATHER>(a, tile + step, lane);
+  uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * step, lane);
+  int cur = 0;
+  MSched sc = m_schedule(dc, lane, lst[0]);
+  MBuf b[M_D + 1];
+#pragma unroll
+  for (int k = 0; k < M_D; ++k) {
+    b[k] = m_load_round<NT>(a, dc, sc, lst[0], (uint32_t)k, lane);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  while (tile < tend) {
+    const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
+    u32x4 tailc = (u32x4){0u, 0u, 0u, 0u};
+    if constexpr (GATHER)
+      tailc = *(const u32x4 *)(a.frames + ((dc.base + (uint64_t)max(dc.len, 1u) - 1u) &
+                                           ~(uint64_t)15));
+    // the next tile's schedule, into the other list (the previous tile's,
+    // whose rounds are all consumed)
+    const MSched sn = m_schedule(dn, lane, lst[cur ^ 1]);
+    const uint32_t P = m_rounds(sc);
+    // Round r lives in slot r % (D + 1); P is a multiple of D + 1, so the
+    // ring is back in slot 0 at every tile boundary.  LAST: the group's
+    // prefetches past this tile issue the next tile's first D rounds.
+    auto group = [&](const uint32_t r0, auto last_tag) __attribute__((always_inline)) {
+      constexpr bool LAST = decltype(last_tag)::value;
+#pragma unroll
+      for (int u = 0; u <= M_D; ++u) {
+        const uint32_t r = r0 + (uint32_t)u;
+        if (LAST && u > 0)
+          b[(u + M_D) % (M_D + 1)] =
+              m_load_round<NT>(a, dn, sn, lst[cur ^ 1], (uint32_t)(u - 1), lane);
+        else
+          b[(u + M_D) % (M_D + 1)] = m_load_round<NT>(a, dc, sc, lst[cur], r + M_D, lane);
+        const MBuf &cb = b[u];
+        const int tl = m_tl(sc, r);
+        const int j = lane & ((1 << tl) - 1);
+        const uint32_t q = cb.qml & 0xffu;
+        const bool real = q != 0xffu;
+        const int m = (int)((cb.qml >> 8) & 15u);
+        const int pl = (int)(cb.qml >> 16);
+        LDS_AS uint8_t *img = wimg + (q & (WAVE - 1)) * IMG_STRIDE;
+        // the image: chunks 0..7 of the frame (every team width is >= 4,
+        // so only the first two load slots can hold them)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int c = (i << tl) + j;
+          if (real && c < IMG_CHUNKS) *(LDS_AS u32x4 *)(img + 16 * c) = cb.v[i];
+        }
+        uint32_t acc = 0;
+        const int ts = team_start_of(m);
+#pragma unroll
+        for (int i = 0; i < M_S; ++i)
+          acc = sum_chunk_from<!GATHER>(cb.v[i], 16 * ((i << tl) + j) - m, ts, pl, acc);
+        acc = m_team_sum(acc, tl);
+        if (real && j == (1 << tl) - 1) *(LDS_AS uint32_t *)(img + M_SUM) = acc;
+      }
+    };
+    uint32_t r0 = 0;
+#pragma unroll 1
+    do {   // P >= 2 (D + 1): at least once
+      group(r0, std::false_type{});
+      r0 += M_D + 1;
+    } while (r0 < P - (M_D + 1));
+    const Desc d2 = desc_fill<GATHER>(a, idx2, tile + 2 * step, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    group(P - (M_D + 1), std::true_type{});
+
+    // ---- lane phase: frame `lane` -> record
+    __builtin_amdgcn_wave_barrier();
+    const bool stage = !(a.tune & 2u);
+    const bool scatter = GATHER && a.perm;
+    if (dc.idx != 0xffffffffu && !(kDiag && (a.tune & 16u))) {
+      const int m = (int)(dc.base & 15);
+      uint32_t my_sum = *(const LDS_AS uint32_t *)(wimg + lane * IMG_STRIDE + M_SUM);
+      const int nch = (m + (int)dc.len + 15) >> 4;
+      if (nch > 16 * M_S) {   // longer than a 16-lane round holds (jumbo): rare
+        const u32x4 *c0 = (const u32x4 *)(a.frames + (dc.base - (uint64_t)m));
+        for (int c = 16 * M_S; c < nch; ++c)
+          my_sum = settle(sum_chunk_from<!GATHER>(ldc<NT>(c0 + c), 16 * c - m, 0, (int)dc.len,
+                                                  my_sum));
+      }
+      const FrameView v = {wimg + lane * IMG_STRIDE, (const GLB_AS uint8_t *)a.frames + dc.base, m,
+                           16 * IMG_CHUNKS - m};
+      LaneRec o;
+      lane_generic(a, v, dc.len, dc.base, my_sum, tailc, o);
+      if (a.txside)
+        a.txside[dc.idx] = o.tx;
+      emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
+    }
+    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32))
+      flush_records(a, wimg, tile, lane, dc.idx, scatter);
+    tile += step;
+    dc = dn;
+    dn = d2;
+    idx2 = idx3;
+    sc = sn;
+    cur ^= 1;
   }
 }
 
@@ -1432,6 +1698,19 @@ __global__ __launch_bounds__(256) void rx_mss_kernel(RxKArgs a) {
   }
 }
 
+// Descriptor sources of an offset-described (GATHER) launch: absent arrays
+// read the context's zeroed stand-in buffer (RxKArgs::zero).
+void gather_args(RxKArgs &a) {
+  a.perm_ld = a.perm ? a.perm : (const uint32_t *)a.zero;
+  a.perm_msk = a.perm ? ~0u : 0u;
+  a.off_ld = a.off ? a.off : (const uint64_t *)a.zero;
+  a.off_msk = a.off ? ~0u : 0u;
+  a.stride_g = a.off ? 0u : a.stride;
+  a.len_ld = a.len ? a.len : (const uint16_t *)a.zero;
+  a.len_msk = a.len ? ~0u : 0u;
+  a.fixed_g = a.len ? 0u : a.fixed_len;
+}
+
 template <int T, int S, int D, int AL>
 hipError_t launch_variant(const RxKArgs &a0, int grid, hipStream_t s) {
   const dim3 gd(grid), bd(WAVE * WPB);
@@ -1439,16 +1718,7 @@ hipError_t launch_variant(const RxKArgs &a0, int grid, hipStream_t s) {
   const bool nt = a.tune & 1u;
   const bool gather = a.off || a.len || a.perm;
   if (gather) {
-    a.perm_ld = a.perm ? a.perm : (const uint32_t *)a.zero;
-    a.perm_msk = a.perm ? ~0u : 0u;
-    a.off_ld = a.off ? a.off : (const uint64_t *)a.zero;
-    a.off_msk = a.off ? ~0u : 0u;
-    a.stride_g = a.off ? 0u : a.stride;
-    a.len_ld = a.len ? a.len : (const uint16_t *)a.zero;
-    a.len_msk = a.len ? ~0u : 0u;
-    a.fixed_g = a.len ? 0u : a.fixed_len;
-  }
-  if (gather) {
+    gather_args(a);
     if (nt) hipLaunchKernelGGL((rx_kernel<T, S, D, AL, true, true>), gd, bd, 0, s, a);
     else hipLaunchKernelGGL((rx_kernel<T, S, D, AL, false, true>), gd, bd, 0, s, a);
   } else {
@@ -1521,6 +1791,20 @@ hipError_t launch_tx_apply(const uint64_t *txside, uint8_t *frames, const uint64
 }
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s) {
+  if (variant == RX_M6) {
+    const dim3 gd(grid), bd(WAVE * WPB);
+    RxKArgs m = a;
+    const bool nt = m.tune & 1u;
+    if (m.off || m.len || m.perm) {
+      gather_args(m);
+      if (nt) hipLaunchKernelGGL((rx_kernel_mixed<true, true>), gd, bd, 0, s, m);
+      else hipLaunchKernelGGL((rx_kernel_mixed<false, true>), gd, bd, 0, s, m);
+    } else {
+      if (nt) hipLaunchKernelGGL((rx_kernel_mixed<true, false>), gd, bd, 0, s, m);
+      else hipLaunchKernelGGL((rx_kernel_mixed<false, false>), gd, bd, 0, s, m);
+    }
+    return hipGetLastError();
+  }
   if (variant == RX_L4) {
     const dim3 gd(grid), bd(WAVE * WPB);
     if (a.tune & 1u) hipLaunchKernelGGL(rx_kernel_lane<true>, gd, bd, 0, s, a);
@@ -1547,6 +1831,13 @@ hipError_t launch_mss_clamp(const RxKArgs &a, int grid, hipStream_t s) {
 }
 
 int rx_variant_blocks_per_cu(int variant) {
+  if (variant == RX_M6) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel_mixed<false, true>, WAVE * WPB,
+                                                     0) != hipSuccess)
+      return 1;
+    return nb > 0 ? nb : 1;
+  }
   if (variant == RX_L4) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel_lane<false>, WAVE * WPB, 0) !=

@@ -65,7 +65,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
 
 # Kernel variants, in the order of enum RxVariant (pptk_amd/csrc/rx_internal.h).
 VARIANTS = ("T4S1", "T4S2", "T16S2", "T16S6", "T32S3", "T64S2", "T16S7L", "T32S4L",
-            "T32S3D7", "T16S6D1", "T8S2", "T16S4", "L4")
+            "T32S3D7", "T16S6D1", "T8S2", "T16S4", "L4", "M6")
 RX_L4 = VARIANTS.index("L4")
 
 _libs = {}

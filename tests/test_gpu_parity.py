@@ -763,6 +763,50 @@ def test_large_fresh_batches_vs_oracle(seed, oracle_lib, dev):
     got32 = _run(ctx, z, dev, shift=3, compact=True)
     d = diff_records(got32, to_rec32(want), dtype=REC32_DTYPE)
     assert not d, d
+    from pptk_amd.rx import VARIANTS
+    ctx.set_tuning(VARIANTS.index("M6"), -1)   # lanes binned by length inside the tile
+    got = _run(ctx, z, dev, shift=5)
+    d = diff_records(got, want)
+    assert not d, d
+
+
+@pytest.mark.parametrize("cfg", ["imix", "cmix", "jmix"])
+def test_mixed_shape_kernel_vs_oracle(cfg, oracle_lib, dev):
+    """RX_M6 (each tile's frames binned by chunk count into 4-, 8- and
+    16-lane team rounds) on 2^17-frame synthetic batches of every mixed
+    config: records, dense flow hashes and compact records bit-exact against
+    the CPU oracle, in batch order and in a binned processing order."""
+    from oracle.oracle import make_opts
+    from pptk_amd.rx import RxContext, VARIANTS
+    from tools.synth import make_batch
+    n = 1 << 17
+    b = make_batch(cfg, n, dev)
+    host = b["frames"].cpu().numpy()
+    off = b["off"].cpu().numpy().view(np.uint64)
+    lens = b["lens"].cpu().numpy().view(np.uint16)
+    key = bytes(range(1, 17))
+    want = oracle_lib.rx_batch(host, off, lens, opts=make_opts(key, 24, 48, 1 << 12), nthreads=8)
+    ctx = RxContext(0, key, 24, 48, 1 << 12)
+    ctx.set_tuning(VARIANTS.index("M6"), -1)
+    kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
+    h = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    recs = ctx.batch_device(b["frames"], n, hash_out=h, **kw)
+    torch.cuda.synchronize()
+    assert ctx.last_variant() == VARIANTS.index("M6")
+    got = recs.cpu().numpy().reshape(-1)
+    d = diff_records(got, want)
+    assert not d, d
+    assert np.array_equal(h.cpu().numpy().view(np.uint64), want["flow_hash"])
+    r32 = ctx.batch_device(b["frames"], n, compact=True, **kw)
+    torch.cuda.synchronize()
+    d = diff_records(r32.cpu().numpy().reshape(-1), to_rec32(want), dtype=REC32_DTYPE)
+    assert not d, d
+    p = ctx.bin_device(b["lens"], n)
+    recs = ctx.batch_device(b["frames"], n, perm=p, **kw)
+    torch.cuda.synchronize()
+    d = diff_records(recs.cpu().numpy().reshape(-1), want)
+    assert not d, d
+    ctx.close()
 
 
 @pytest.mark.parametrize("layout", ["fixed", "offsets"])
@@ -788,7 +832,8 @@ def test_autotune_keeps_records(layout, dev):
     want = torch.from_numpy(w.view(np.uint8).reshape(n, 64).copy())
     ctx = RxContext(0, bytes(range(1, 17)))
     name = ctx.autotune(b["frames"], n, reps=2, **kw)
-    assert name in ("T16S6", "T32S3", "T32S3D7", "T16S7L")
+    assert name in (("T16S6", "T32S3", "T32S3D7", "T16S7L") +
+                    (("M6",) if layout == "offsets" else ()))
     got = ctx.batch_device(b["frames"], n, **kw)
     torch.cuda.synchronize()
     assert VARIANTS[ctx._L.pptk_rx_last_variant(ctx._ctx)] == name
