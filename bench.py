@@ -915,6 +915,52 @@ def pmc_traffic(cfg, frames):
         return None, None
 
 
+def live_pmc(cfg, variant, n, timeout_s=120):
+    """Same-run HBM traffic of this config's rx kernel: one FETCH_SIZE pass
+    and one WRITE_SIZE pass (separate rocprofv3 runs, MI355X_MICROARCH.md
+    HBM section), each a child process `bench.py --only cfg` of n frames
+    with the kernel shape this run chose (PPTK_RX_VARIANT), killed after
+    timeout_s.  Per launch, median over the child's launches; FETCH_SIZE x2
+    (gfx950 counts half of 16-byte/lane streaming reads), both in KiB.
+    Returns (traffic bytes, detail dict) or (None, reason)."""
+    import shutil
+    import subprocess
+    import tempfile
+    from pptk_amd.rx import VARIANTS
+    from tools.pmc_summary import counter
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rp):
+        return None, "rocprofv3 not found"
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return None, "already under rocprofv3"
+    base = tempfile.mkdtemp(prefix="pptk_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ, PPTK_RX_VARIANT=str(VARIANTS.index(variant)))
+    got = {}
+    t0 = time.perf_counter()
+    try:
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(base, c)
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), rp, "--pmc", c,
+                   "--kernel-include-regex", "rx_kernel", "-d", d, "-o", "run",
+                   "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__),
+                   "--only", cfg, "--frames", str(n), "--steps", "3", "--warmup", "1",
+                   "--no-cpu", "--no-check", "--no-membench", "--no-rec32", "--no-place",
+                   "--settle", "0.3", "--no-live-pmc"]
+            r = subprocess.run(cmd, env=env, cwd=base, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, timeout=timeout_s + 30)
+            if r.returncode != 0:
+                return None, f"{c} pass exited {r.returncode}: {r.stderr.decode()[-200:]}"
+            vals, _, kname = counter(d, c)
+            got[c] = float(np.median(vals))
+    except Exception as e:          # the committed summary stays the fallback
+        return None, f"{type(e).__name__}: {e}"
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+    rd, wr = got["FETCH_SIZE"] * 2 * 1024, got["WRITE_SIZE"] * 1024
+    return int(rd + wr), {"read_bytes": int(rd), "write_bytes": int(wr), "kernel": kname,
+                          "seconds": round(time.perf_counter() - t0, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -937,6 +983,9 @@ def main():
                     help="seconds of untimed launches before the warmup steps")
     ap.add_argument("--no-place", action="store_true",
                     help="one record buffer as allocated, no placement probe")
+    ap.add_argument("--no-live-pmc", action="store_true",
+                    help="no same-run rocprofv3 FETCH_SIZE/WRITE_SIZE passes (roofline.traffic "
+                         "then comes from the committed summary)")
     args = ap.parse_args()
     launch_ranks(sys.argv[1:], args.gpus)
 
@@ -1088,6 +1137,27 @@ def main():
         if args.steps + args.warmup < 64:
             rewrite = rewrite_bench(ctx, n, dev, rank, args.steps, args.warmup)
             log(f"[rank {rank}] rewrite: {rewrite}")
+
+    # roofline.traffic from this run: rocprofv3 PMC passes over the same
+    # workload and kernel shape, in child processes (rank 0 of a one-GPU
+    # run; the committed summary is the fallback)
+    if rank == 0 and ws == 1 and not args.no_live_pmc:
+        t, info = live_pmc(primary_cfg, prim["variant"], n)
+        if t is not None:
+            roofline["traffic"] = t
+            roofline["traffic_source"] = "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, this run"
+            roofline["traffic_detail"] = info
+        else:
+            roofline["traffic_live_error"] = info
+        log(f"live pmc {primary_cfg}: {t} {info}")
+        for cfg, sec in secondary.items():
+            t, info = live_pmc(cfg, sec["kernel_variant"], n)
+            if t is not None:
+                sec["roofline"]["traffic"] = t
+                sec["roofline"]["traffic_detail"] = info
+            else:
+                sec["roofline"]["traffic_live_error"] = info
+            log(f"live pmc {cfg}: {t} {info}")
 
     if rank == 0:
         line = {
