@@ -931,7 +931,8 @@ def live_pmc(cfg, variant, n, timeout_s=120):
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None, "rocprofv3 not found"
-    if any(k.startswith("ROCPROF") for k in os.environ):
+    if (any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+            or "rocprof" in os.environ.get("LD_PRELOAD", "")):
         return None, "already under rocprofv3"
     base = tempfile.mkdtemp(prefix="pptk_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     env = dict(os.environ, PPTK_RX_VARIANT=str(VARIANTS.index(variant)))

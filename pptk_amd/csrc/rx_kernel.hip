@@ -1102,12 +1102,15 @@ __device__ __forceinline__ uint32_t m_rank(uint64_t mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Bin the tile's frames (descriptor d per lane) and list their lanes class
-// by class in `list` (64 bytes of LDS).  Lanes past the batch are not
-// listed.  (Listing whole descriptors, 16 bytes each, read by one broadcast
-// LDS load per round instead of the lane index plus three shuffles,
-// measured slower: IMIX 1.62 vs 1.54 ms, CMIX +11 % vs +1.5 % against the
-// team kernel.)
+// Bin the tile's frames (descriptor d per lane) and list them round by
+// round in `list`: row r (16 bytes) holds the lanes of the frames round r's
+// teams sum, 0xff for an empty team, so a round finds its team's frame with
+// one LDS byte load and no per-class arithmetic.  Lanes past the batch are
+// not listed.  (Listing whole descriptors, 16 bytes each, read by one
+// broadcast LDS load per round instead of the lane index plus three
+// shuffles, measured slower: IMIX 1.62 vs 1.54 ms, CMIX +11 % vs +1.5 %
+// against the team kernel.)
+constexpr int M_RMAX = 24;   // list rows (a tile needs at most 20: 1 + 1 + 16 rounds, padded)
 __device__ __forceinline__ MSched m_schedule(const Desc &d, int lane, LDS_AS uint8_t *list) {
   const bool valid = d.idx != 0xffffffffu;
   const uint32_t nch = ((uint32_t)(d.base & 15u) + d.len + 15u) >> 4;
@@ -1121,10 +1124,15 @@ __device__ __forceinline__ MSched m_schedule(const Desc &d, int lane, LDS_AS uin
   s.e0 = (s.n0 + 15u) >> 4;
   s.e1 = s.e0 + ((s.n1 + 7u) >> 3);
   s.e2 = s.e1 + ((s.n2 + 3u) >> 2);
-  const uint32_t pos = nch <= 24u ? m_rank(b0)
-                       : nch <= 48u ? s.n0 + m_rank(b1)
-                                    : s.n0 + s.n1 + m_rank(b2);
-  if (valid) list[pos] = (uint8_t)lane;
+  LDS_AS uint32_t *lw = (LDS_AS uint32_t *)list;   // every row empty first
+  lw[lane] = 0xffffffffu;
+  if (lane < M_RMAX * 4 - WAVE) lw[WAVE + lane] = 0xffffffffu;
+  // class c: rows from its first round on, 16 >> c frames per row
+  const uint32_t c = nch <= 24u ? 0u : nch <= 48u ? 1u : 2u;
+  const uint32_t rho = c == 0u ? m_rank(b0) : c == 1u ? m_rank(b1) : m_rank(b2);
+  const uint32_t er = c == 0u ? 0u : c == 1u ? s.e0 : s.e1;
+  const uint32_t sh = 4u - c;
+  if (valid) list[(er + (rho >> sh)) * 16u + (rho & ((1u << sh) - 1u))] = (uint8_t)lane;
   return s;
 }
 
@@ -1171,15 +1179,11 @@ template <bool NT>
 __device__ __forceinline__ MBuf m_load_round(const RxKArgs &a, const Desc &d, const MSched &s,
                                              const LDS_AS uint8_t *list, uint32_t r, int lane) {
   const int tl = m_tl(s, r);
-  const uint32_t first = r < s.e0 ? 0u : r < s.e1 ? s.n0 : s.n0 + s.n1;
-  const uint32_t cnt = r < s.e0 ? s.n0 : r < s.e1 ? s.n1 : s.n2;
-  const uint32_t r0 = r < s.e0 ? 0u : r < s.e1 ? s.e0 : s.e1;
-  // this team's entry of the class: (r - r0) * (64 >> tl) + team
-  const uint32_t k = ((r - r0) << (6 - tl)) + ((uint32_t)lane >> tl);
-  const bool real = k < cnt;
-  // (an empty team reads some lane's frame: every lane describes a valid
+  const uint32_t e = list[r * 16u + ((uint32_t)lane >> tl)];
+  const bool real = e != 0xffu;
+  // (an empty team reads lane 63's frame: every lane describes a valid
   // frame, lanes past the batch frame 0)
-  const uint32_t q = (uint32_t)list[real ? first + k : 0u] & (WAVE - 1);
+  const uint32_t q = e & (WAVE - 1);
   MBuf b;
   // both shuffles unconditional: a ds_bpermute executed under a lane mask
   // reads 0 from every source lane outside the mask
@@ -1203,7 +1207,7 @@ __global__ __launch_bounds__(WAVE * WPB, 2) void rx_kernel_mixed(RxKArgs a) {
     if (!group_range(a)) return;
   }
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * IMG_STRIDE];
-  __shared__ uint8_t lists[WPB][2][WAVE];
+  __shared__ __attribute__((aligned(16))) uint8_t lists[WPB][2][M_RMAX * 16];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * IMG_STRIDE;
@@ -1269,9 +1273,25 @@ __global__ __launch_bounds__(WAVE * WPB, 2) void rx_kernel_mixed(RxKArgs a) {
         }
         uint32_t acc = 0;
         const int ts = team_start_of(m);
+        if constexpr (GATHER) {
+          // unmasked sums of the chunks c in [c_lo, nch): o = 16c - m >= ts
+          // and o < len; one unsigned compare per chunk
+          const int c_lo = (ts + m + 15) >> 4;
+          const uint32_t span = (uint32_t)max(((m + pl + 15) >> 4) - c_lo, 0);
+          const uint32_t jc = (uint32_t)(j - c_lo);
 #pragma unroll
-        for (int i = 0; i < M_S; ++i)
-          acc = sum_chunk_from<!GATHER>(cb.v[i], 16 * ((i << tl) + j) - m, ts, pl, acc);
+          for (int i = 0; i < M_S; ++i) {
+            uint32_t t = dot16(cb.v[i].x, 0);
+            t = dot16(cb.v[i].y, t);
+            t = dot16(cb.v[i].z, t);
+            t = dot16(cb.v[i].w, t);
+            acc += jc + ((uint32_t)i << tl) < span ? t : 0u;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < M_S; ++i)
+            acc = sum_chunk_from<true>(cb.v[i], 16 * ((i << tl) + j) - m, ts, pl, acc);
+        }
         acc = m_team_sum(acc, tl);
         if (real && j == (1 << tl) - 1) *(LDS_AS uint32_t *)(img + M_SUM) = acc;
       }

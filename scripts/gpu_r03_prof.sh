@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-3 evidence, one box, one tree (profiles/r03):
 #  * smoke;
-#  * the default bench command under rocprofv3 kernel tracing;
+#  * the default bench command under rocprofv3 kernel tracing (its own
+#    same-run PMC passes off: no profiler nesting);
 #  * FETCH_SIZE / WRITE_SIZE passes (separate runs, MI355X_MICROARCH.md) of
 #    the C1500 / C64 / CMIX / IMIX / JMIX rx kernels and of the three rate
 #    limiter runs alone (tools/opbench.py permit_<run>).
@@ -10,7 +11,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r03p
 mkdir -p $O
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench_prof 900 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python bench.py
+step bench_prof 900 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python bench.py --no-live-pmc
 variant() {
   python - "$1" <<'PY'
 import json, sys
@@ -25,8 +26,8 @@ PY
 for c in c1500 c64 cmix imix jmix; do
   export PPTK_RX_VARIANT=$(variant $c)
   echo "$c PPTK_RX_VARIANT=$PPTK_RX_VARIANT" >> gpurun_out/steps.log
-  step fetch_$c 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rx_kernel -d $O/fetch_$c -o run --output-format csv -- python bench.py --only $c --steps 3 --warmup 1 --no-cpu --no-check --no-membench --no-rec32 --settle 0.3
-  step write_$c 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rx_kernel -d $O/write_$c -o run --output-format csv -- python bench.py --only $c --steps 3 --warmup 1 --no-cpu --no-check --no-membench --no-rec32 --settle 0.3
+  step fetch_$c 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rx_kernel -d $O/fetch_$c -o run --output-format csv -- python bench.py --only $c --steps 3 --warmup 1 --no-cpu --no-check --no-membench --no-rec32 --settle 0.3 --no-live-pmc
+  step write_$c 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex rx_kernel -d $O/write_$c -o run --output-format csv -- python bench.py --only $c --steps 3 --warmup 1 --no-cpu --no-check --no-membench --no-rec32 --settle 0.3 --no-live-pmc
 done
 unset PPTK_RX_VARIANT
 for op in permit_records permit_keys permit_keys_denying; do
