@@ -374,11 +374,30 @@ __device__ __forceinline__ u32x4 ldc(const u32x4 *p) {
   else return *p;
 }
 
+// Sum over a team of T lanes, complete in every lane of the team.  Teams
+// inside a row of 16 lanes by DPP adds (no LDS crossbar traffic): quad_perm
+// [1,0,3,2] and [2,3,0,1] (quads), row_half_mirror (lane i <-> 7 - i: the
+// two quads of an 8-lane half), row_mirror (i <-> 15 - i: the two halves):
+// CMIX T16S6 2.743 -> 2.717 ms, IMIX 1.696 -> 1.653 ms, C1500 T16S6 4.330
+// -> 4.312 ms (in-process A/B, profiles/r03/dpp).  Teams of 32 and 64 lanes
+// keep xor shuffles for every step (C1500 T32S3 4.184 vs 4.208 ms with the
+// row steps as DPP).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t x) {
+  return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, true);
+}
 template <int T>
 __device__ __forceinline__ uint32_t team_sum(uint32_t x) {
+  if constexpr (T >= 32) {
 #pragma unroll
-  for (int d = T / 2; d >= 1; d >>= 1)
-    x += __shfl_xor(x, d, T);
+    for (int d = T / 2; d >= 1; d >>= 1)
+      x += __shfl_xor(x, d, T);
+    return x;
+  }
+  if constexpr (T >= 2) x = dpp_add<0xb1>(x);    // quad_perm [1,0,3,2]
+  if constexpr (T >= 4) x = dpp_add<0x4e>(x);    // quad_perm [2,3,0,1]
+  if constexpr (T >= 8) x = dpp_add<0x141>(x);   // row_half_mirror
+  if constexpr (T >= 16) x = dpp_add<0x140>(x);  // row_mirror
   return x;
 }
 
