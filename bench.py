@@ -915,14 +915,21 @@ def pmc_traffic(cfg, frames):
         return None, None
 
 
-def live_pmc(cfg, variant, n, timeout_s=120):
+_LIVE_PMC_FAILED = []   # after one failed pass the later configs skip theirs
+
+
+def live_pmc(cfg, variant, n, timeout_s=60):
     """Same-run HBM traffic of this config's rx kernel: one FETCH_SIZE pass
     and one WRITE_SIZE pass (separate rocprofv3 runs, MI355X_MICROARCH.md
     HBM section), each a child process `bench.py --only cfg` of n frames
     with the kernel shape this run chose (PPTK_RX_VARIANT), killed after
-    timeout_s.  Per launch, median over the child's launches; FETCH_SIZE x2
-    (gfx950 counts half of 16-byte/lane streaming reads), both in KiB.
-    Returns (traffic bytes, detail dict) or (None, reason)."""
+    timeout_s (a pass takes 5-10 s).  Per launch, median over the child's
+    launches; FETCH_SIZE x2 (gfx950 counts half of 16-byte/lane streaming
+    reads), both in KiB.  Returns (traffic bytes, detail dict) or (None,
+    reason); once a pass has failed, every later call returns at once, so a
+    profiler that hangs costs the bench one time limit, not one per config."""
+    if _LIVE_PMC_FAILED:
+        return None, f"skipped: an earlier pass failed ({_LIVE_PMC_FAILED[0]})"
     import shutil
     import subprocess
     import tempfile
@@ -950,10 +957,12 @@ def live_pmc(cfg, variant, n, timeout_s=120):
             r = subprocess.run(cmd, env=env, cwd=base, stdout=subprocess.DEVNULL,
                                stderr=subprocess.PIPE, timeout=timeout_s + 30)
             if r.returncode != 0:
+                _LIVE_PMC_FAILED.append(f"{cfg} {c} exit {r.returncode}")
                 return None, f"{c} pass exited {r.returncode}: {r.stderr.decode()[-200:]}"
             vals, _, kname = counter(d, c)
             got[c] = float(np.median(vals))
     except Exception as e:          # the committed summary stays the fallback
+        _LIVE_PMC_FAILED.append(f"{cfg}: {type(e).__name__}")
         return None, f"{type(e).__name__}: {e}"
     finally:
         shutil.rmtree(base, ignore_errors=True)
