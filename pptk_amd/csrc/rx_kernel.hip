@@ -1095,9 +1095,9 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
 // rank by mbcnt: the tile's frame indices are listed class by class in a
 // 64-byte LDS list (no global permutation, no extra HBM traffic); round r of
 // the tile runs list entries of one class.  Every round issues the same six
-// loads, so the prefetch ring of rx_kernel carries over unchanged: D = 3
-// rounds in flight in fixed register slots, the round count padded to a
-// multiple of 4 with empty rounds, and the next tile's schedule (built from
+// loads, so the prefetch ring of rx_kernel carries over unchanged: D rounds
+// in flight in fixed register slots, the round count padded to a multiple
+// of D + 1 with empty rounds, and the next tile's schedule (built from
 // its descriptors, which run a tile ahead) known before the last round
 // group issues that tile's first rounds.  A round's team sum goes to the
 // frame's LDS slot (bytes 128..131 of its image), where the owning lane
@@ -1105,7 +1105,17 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
 // written in the tile's 4 KB run.  IMIX (7:4:1 of 64/576/1500 B) needs ~10
 // rounds per tile instead of 16.
 constexpr int M_S = 6;        // chunk loads per lane per round
-constexpr int M_D = 3;        // rounds in flight
+// Rounds in flight and waves per SIMD: one round in flight at 3 waves/SIMD
+// (141 VGPRs) beat three at 2 waves/SIMD (195) and two at 2 or 3 (168):
+// IMIX 1.537 / 1.475 / 1.451 ms for D = 3 / 2 / 1, CMIX 2.891 / 2.864 /
+// 2.865 ms (in-process A/B, profiles/r03/m6/m6d_ab_*.json).
+#ifndef PPTK_RX_M_D
+#define PPTK_RX_M_D 1
+#endif
+#ifndef PPTK_RX_M_WAVES
+#define PPTK_RX_M_WAVES 3
+#endif
+constexpr int M_D = PPTK_RX_M_D;   // rounds in flight
 constexpr int M_SUM = 128;    // byte offset of a frame's team sum in its image slot
 static_assert(IMG_STRIDE >= M_SUM + 4, "the team sum lives past the 128-byte image");
 
@@ -1160,8 +1170,8 @@ __device__ __forceinline__ MSched m_schedule(const Desc &d, int lane, LDS_AS uin
 // compiler has no zero-trip path on which it would copy the ring's in-flight
 // registers (a vmcnt(0) drain at every such tile).
 __device__ __forceinline__ uint32_t m_rounds(const MSched &s) {
-  return s.e2 <= (uint32_t)(2 * (M_D + 1)) ? (uint32_t)(2 * (M_D + 1))
-                                           : (s.e2 + (uint32_t)M_D) & ~(uint32_t)M_D;
+  constexpr uint32_t G = M_D + 1;
+  return s.e2 <= 2 * G ? 2 * G : (s.e2 + G - 1) / G * G;
 }
 
 // log2 of the team width of round r (wave-uniform).
@@ -1221,7 +1231,7 @@ __device__ __forceinline__ MBuf m_load_round(const RxKArgs &a, const Desc &d, co
 }
 
 template <bool NT, bool GATHER>
-__global__ __launch_bounds__(WAVE * WPB, 2) void rx_kernel_mixed(RxKArgs a) {
+__global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(RxKArgs a) {
   if constexpr (GATHER) {
     if (!group_range(a)) return;
   }
