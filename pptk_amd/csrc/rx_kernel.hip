@@ -1092,9 +1092,9 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
 //   class 2: anything longer,                 teams of 16 lanes, 4 frames/round
 // (longer than 96 chunks: the rest is summed in the lane phase, as the
 // unrolled team variants do).  The binning is a ballot per class and a
-// rank by mbcnt: the tile's frame indices are listed class by class in a
-// 64-byte LDS list (no global permutation, no extra HBM traffic); round r of
-// the tile runs list entries of one class.  Every round issues the same six
+// rank by mbcnt: the tile's frame lanes are listed round by round in LDS
+// (m_schedule; no global permutation, no extra HBM traffic); round r of the
+// tile runs frames of one class.  Every round issues the same six
 // loads, so the prefetch ring of rx_kernel carries over unchanged: D rounds
 // in flight in fixed register slots, the round count padded to a multiple
 // of D + 1 with empty rounds, and the next tile's schedule (built from
@@ -1102,8 +1102,8 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
 // group issues that tile's first rounds.  A round's team sum goes to the
 // frame's LDS slot (bytes 128..131 of its image), where the owning lane
 // reads it in the lane phase.  Frame i's record stays at its own index,
-// written in the tile's 4 KB run.  IMIX (7:4:1 of 64/576/1500 B) needs ~10
-// rounds per tile instead of 16.
+// written in the tile's 4 KB run.  IMIX (7:4:1 of 64/576/1500 B) needs ~8
+// rounds per tile instead of 16 (DESIGN.md section 5).
 constexpr int M_S = 6;        // chunk loads per lane per round
 // Rounds in flight and waves per SIMD: one round in flight at 3 waves/SIMD
 // (141 VGPRs) beat three at 2 waves/SIMD (195) and two at 2 or 3 (168):
