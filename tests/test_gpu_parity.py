@@ -809,6 +809,34 @@ def test_mixed_shape_kernel_vs_oracle(cfg, oracle_lib, dev):
     ctx.close()
 
 
+@pytest.mark.parametrize("cfg", ["imix", "cmix"])
+def test_mixed_shape_kernel_full_size(cfg, dev):
+    """BASELINE sizes (16 M frames): M6 and the team kernel T16S6 write
+    byte-identical records for the whole batch, every frame parses, and
+    every IP / L4 verdict equals what the generator planted (its own
+    checksums, ~1 % of frames corrupted) -- size-independent properties."""
+    from pptk_amd.records import F_IP_OK, F_L4_OK, F_PARSED
+    from pptk_amd.rx import RxContext, VARIANTS
+    from tools.synth import make_batch
+    n = 1 << 24
+    b = make_batch(cfg, n, dev)
+    kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
+    ctx = RxContext(0, bytes(range(1, 17)))
+    ctx.set_tuning(VARIANTS.index("M6"), -1)
+    got = ctx.batch_device(b["frames"], n, **kw)
+    ctx.set_tuning(VARIANTS.index("T16S6"), -1)
+    ref = ctx.batch_device(b["frames"], n, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    r = got.view(torch.int16)[:, 27].to(torch.int32) & 0xFFFF      # flags @54
+    exp = b["expect"].to(torch.int32)
+    assert bool(((r & F_PARSED) != 0).all().item())
+    assert bool((((r & F_IP_OK) != 0).to(torch.int32) == (exp & 1)).all().item())
+    assert bool((((r & F_L4_OK) != 0).to(torch.int32) == ((exp >> 1) & 1)).all().item())
+    assert int((exp != 3).sum().item()) > n // 200                 # corrupted frames present
+    ctx.close()
+
+
 @pytest.mark.parametrize("layout", ["fixed", "offsets"])
 def test_autotune_keeps_records(layout, dev):
     """pptk_rx_autotune picks one of the interchangeable shapes for a
