@@ -1,4 +1,5 @@
 #!/bin/bash
+# (abl/libpptkrx_exp.so: make abvariant NAME=exp DEFS="-DPPTK_RX_EXPERIMENTS -DPPTK_RX_DIAG"; cp build/ab_exp/libpptkrx.so abl/libpptkrx_exp.so -- build/ is not sent to the GPU box)
 # Round 3: where the C64 lane kernel's time goes (exp = diagnostics build:
 # bit 16 no per-frame phase, bit 8 no record stores; output invalid).
 cd $GRAFT_REPO_ROOT

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (abl/libpptkrx_exp.so: make abvariant NAME=exp DEFS="-DPPTK_RX_EXPERIMENTS -DPPTK_RX_DIAG"; cp build/ab_exp/libpptkrx.so abl/libpptkrx_exp.so -- build/ is not sent to the GPU box)
 # Round 3: where IMIX / CMIX time goes -- streaming shapes (same records) and
 # diagnostic bits of the experiment build (16 = no lane phase, 8 = no record
 # stores; output invalid), in-process interleaved A/B.

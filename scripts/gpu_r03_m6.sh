@@ -1,4 +1,5 @@
 #!/bin/bash
+# (abl/libpptkrx_exp.so: make abvariant NAME=exp DEFS="-DPPTK_RX_EXPERIMENTS -DPPTK_RX_DIAG"; cp build/ab_exp/libpptkrx.so abl/libpptkrx_exp.so -- build/ is not sent to the GPU box)
 # Round 3: the mixed-shape kernel (RX_M6): parity tests, then in-process A/B
 # against the automatic team shape on the mixed configs (exp = diagnostics
 # build: bit 16 no lane phase, bit 8 no record stores; output invalid).
