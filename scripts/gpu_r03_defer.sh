@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the PPTK_RX_DEFER_FLUSH variant was measured and removed from the source: DESIGN.md section 10)
 # Round 3: deferred record flush (abl/libpptkrx_defer.so = make abvariant
 # NAME=defer DEFS=-DPPTK_RX_DEFER_FLUSH) against the product library,
 # in-process interleaved A/B on placed buffers.

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the PPTK_RX_LANE_UNROLL2 / PPTK_RX_LANE_WAVES variant was measured and removed from the source: DESIGN.md section 10)
 # Round 3: C64 lane kernel -- register sets used in turn (no copy of the
 # prefetch registers, no vmcnt(0) per tile) at 3 waves/SIMD (abl/libpptkrx_lane3.so
 # = make abvariant NAME=lane3 DEFS="-DPPTK_RX_LANE_UNROLL2 -DPPTK_RX_LANE_WAVES=3")
