@@ -422,7 +422,10 @@ int pptk_rx_last_variant(const struct pptk_rx_ctx *ctx);
  * (fixed-stride or offset-described) use the fastest (another shape must
  * beat the automatic one by 1 % to replace it).  The best shape
  * depends on how expensive the record writes are (which follows where the
- * record buffer sits, see pptk_rx_place_records);
+ * record buffer sits, see pptk_rx_place_records) and, for
+ * offset-described batches, on the length mix (the candidates include the
+ * kernel that bins each tile's frames by length into 4-, 8- and 16-lane
+ * rounds, fastest on IMIX-like streams of mostly small frames);
  * results never change.  Synchronous; reps 1..100.
  * pptk_rx_set_tuning's forced variant still takes precedence. */
 int pptk_rx_autotune(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *batch, int reps,
