@@ -10,7 +10,7 @@ CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wextra -Iinclude
 
 LIB := pptk_amd/libpptkrx.so
 HIP_SRCS := pptk_amd/csrc/rx_kernel.hip pptk_amd/csrc/rx_bin.hip pptk_amd/csrc/rx_permit.hip \
-            pptk_amd/csrc/rx_capi.hip pptk_amd/csrc/rx_comm.hip
+            pptk_amd/csrc/rx_capi.hip pptk_amd/csrc/rx_comm.hip pptk_amd/csrc/rx_ring.hip
 C_SRCS := pptk_amd/csrc/host/ipcksum.c pptk_amd/csrc/host/hashseed.c pptk_amd/csrc/host/tcpopt.c \
           pptk_amd/csrc/host/iphash.c pptk_amd/csrc/host/timerlink.c
 HDRS := $(wildcard include/*.h) pptk_amd/csrc/rx_internal.h

@@ -220,6 +220,31 @@ def placed_buffers(ctx, b, n, dev, compact, kw, frames=True, nf=PLACE_FRAMES,
     return recs, report
 
 
+def ring_buffers(ctx, b, n, dev, compact):
+    """The product's default device rings (pptk_rx_ring_alloc): the library
+    allocates frame and record candidates spread apart in HBM, probes every
+    pair with a synthetic batch of the ring's geometry and keeps the fastest
+    (DESIGN.md section 7 "Placement"); the batch is then written into the
+    frame ring, as an rx queue fills its ring.  b["frames"] is replaced by
+    the ring's frame buffer.  Returns (recs, report)."""
+    fbytes = b["frames"].numel() - 64
+    probe = b.get("fixed_len") or 1500
+    ring = ctx.ring_alloc(fbytes, n, 32 if compact else 64, probe_len=min(1536, max(64, probe)))
+    ring.frames.copy_(b["frames"])
+    b["frames"] = ring.frames
+    report = dict(ring.report)
+    report["alloc"] = "pptk_rx_ring_alloc"
+    report["plain_alloc_ms"] = report.pop("first_ms")
+    # the probe is the batch's own launch only for fixed-stride batches of
+    # the probe's frame length (C1500, C64); for offset-described mixes it is
+    # a C1500-stride probe over the same bytes (placement, not a CMIX time)
+    report["probe_is_batch"] = "off" not in b and report["probe_frames"] == n
+    freed, at = release(dev)          # the batch as generated, now copied into the ring
+    report["freed_bytes"] += freed
+    report["_freed_at"] = at
+    return ring.recs, report
+
+
 def placed_gather(ctx, b, recs, kw, n_total, ws, rank, dev, ncand=8, steps=4):
     """The two gather buffers, placed.  The all-gather lands (ws - 1) shards
     of hashes in this GPU's HBM while the next batch streams its frames, and
@@ -305,8 +330,11 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
         # charges for the record writes by up to 25 %:
         # pick a well-placed pair, untimed, as a long-lived rx ring would be
         # set up once (a reused batch keeps its frames: records only)
-        recs, placement = placed_buffers(ctx, b, n, dev, compact, kw, frames=batch is None,
-                                         autotune=autotune)
+        if batch is None:
+            recs, placement = ring_buffers(ctx, b, n, dev, compact)
+        else:
+            recs, placement = placed_buffers(ctx, b, n, dev, compact, kw, frames=False,
+                                             autotune=autotune)
     else:
         recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
     gplace = None
@@ -529,16 +557,26 @@ def summary(r, n):
 
 
 def as_allocated(r):
-    """{"frac_as_allocated": ...}: the read-roofline fraction of the same
-    launch into the buffers as first allocated (the placement probe's pair
-    0), beside the placed pair's `frac` -- what a caller that does not place
-    its rings gets on this GPU."""
+    """What a caller gets from the default allocation.  With the product's
+    device rings (pptk_rx_ring_alloc, the default here) that is the timed
+    run itself: "frac_as_allocated" = frac, and "frac_plain_alloc" is the
+    same launch on a plain hipMalloc pair (the ring probe's candidate pair
+    0: what a caller that allocates its own buffers and does not place them
+    gets on this GPU).  With caller-placed buffers (records-only placement
+    of a reused batch) "frac_as_allocated" is the probe's pair 0, as before."""
     p = r.get("placement") or {}
+    frac = lambda ms: round(r["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if p.get("alloc") == "pptk_rx_ring_alloc":
+        out = {"as_allocated": "pptk_rx_ring_alloc", "frac_as_allocated": frac(r["kernel_ms"]),
+               "as_allocated_ms": round(r["kernel_ms"], 4)}
+        if p.get("plain_alloc_ms") and p.get("probe_is_batch"):
+            out["frac_plain_alloc"] = frac(p["plain_alloc_ms"])
+            out["plain_alloc_ms"] = p["plain_alloc_ms"]
+        return out
     ms = p.get("as_allocated_ms")
     if not ms:
         return {}
-    return {"frac_as_allocated": round(r["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "as_allocated_ms": ms}
+    return {"frac_as_allocated": frac(ms), "as_allocated_ms": ms}
 
 
 def oracle_sample(b, recs, n, dev, k=4096, compact=False):

@@ -18,9 +18,10 @@
  * fail_all(), which aborts every context's communicator
  * (pptk_rx_comm_abort): siblings waiting for a gather it will never join
  * get -ECANCELED from pptk_rx_comm_sync (never hipStreamSynchronize on a
- * gather stream) and the process exits non-zero instead of hanging.  A rank
- * that never joins at all makes the others' pptk_rx_comm_create return
- * -ETIMEDOUT after opts.comm_timeout_ms.
+ * gather stream), siblings still inside (or not yet in) pptk_rx_comm_create
+ * get -ECANCELED from it at once, and the process exits non-zero instead of
+ * hanging.  A rank that never joins without failing makes the others'
+ * pptk_rx_comm_create return -ETIMEDOUT after opts.comm_timeout_ms.
  *
  *   gcc -O2 -pthread -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude \
  *       examples/rx_multigpu.c -Lpptk_amd -lpptkrx -L/opt/rocm/lib -lamdhip64 -o rx_multigpu
@@ -80,7 +81,7 @@ static void fail_all(void)
   if (atomic_exchange(&g_failed, 1))
     return;
   for (int i = 0; i < g_nranks; i++) {
-    int rc = pptk_rx_comm_abort(g_ctx[i]);   /* -EINVAL if it has none (yet) */
+    int rc = pptk_rx_comm_abort(g_ctx[i]);   /* also cancels a creation in progress or to come */
     trace("fail_all: abort rank %d: %d", i, rc);
   }
 }

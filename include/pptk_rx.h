@@ -464,31 +464,40 @@ int pptk_rx_comm_uid(uint8_t uid[PPTK_RX_COMM_UID_BYTES]);
 /* Join `ctx` (one context per GPU) to communicator `uid` as rank `rank` of
  * `nranks`.  Collective: blocks until every rank has called it, at most
  * opts.comm_timeout_ms (then -ETIMEDOUT and the context has no
- * communicator, so it may try again with a new uid).  -EINVAL if the
- * context already has a communicator. */
+ * communicator, so it may try again with a new uid).  -ECANCELED if
+ * pptk_rx_comm_abort was called on the context while this ran, or before
+ * it (a pending abort, consumed by this call).  -EAGAIN if kMaxAbandoned
+ * (4) earlier creations of this process that gave up are still stuck inside
+ * RCCL (a rank that never joined).  -EINVAL if the context already has a
+ * communicator or a creation in progress. */
 int pptk_rx_comm_create(struct pptk_rx_ctx *ctx, int nranks, int rank,
                         const uint8_t uid[PPTK_RX_COMM_UID_BYTES]);
 
 /* Single process, one thread per GPU: one communicator over ctxs[0..n)
  * (each on a different device), rank i = ctxs[i].  Call from one thread;
  * afterwards each rx thread uses its own context concurrently.  Bounded by
- * ctxs[0]'s opts.comm_timeout_ms; on any failure no context keeps one. */
+ * ctxs[0]'s opts.comm_timeout_ms; an abort of any of the contexts cancels
+ * it (-ECANCELED, as pptk_rx_comm_create); on any failure no context keeps
+ * one. */
 int pptk_rx_comm_create_all(struct pptk_rx_ctx *const *ctxs, int n);
 
 /* Orderly teardown (flushes enqueued gathers, bounded; an abort if the
- * flush does not finish).  The context may then create a new one. */
+ * flush does not finish).  Also drops a pending abort.  The context may then
+ * create a new one.  -EBUSY while the context's creation is in progress. */
 int pptk_rx_comm_destroy(struct pptk_rx_ctx *ctx);
 
 /* Cancel the context's communicator now, from any thread: RCCL's kernels
  * of pending gathers return (so their streams drain, with wrong gathered
  * data), waits in pptk_rx_comm_sync / pptk_rx_allgather_hash on it return
  * -ECANCELED, and so does every later call on it until
- * pptk_rx_comm_destroy.  An rx thread that fails calls this on every
- * context of the job, so no sibling waits for a gather it will never join
- * (examples/rx_multigpu.c).  -EINVAL without a communicator (also while
- * the context's pptk_rx_comm_create is still running: that call ends at its
- * own deadline).  It must not race with pptk_rx_comm_destroy or
- * pptk_rx_ctx_destroy of the same context. */
+ * pptk_rx_comm_destroy.  A creation still in progress on the context
+ * (pptk_rx_comm_create / _create_all) returns -ECANCELED promptly and keeps
+ * nothing; on a context with no communicator yet the abort is kept pending
+ * and cancels its next creation.  An rx thread that fails calls this on
+ * every context of the job, so no sibling waits for a gather -- or a
+ * creation -- it will never join (examples/rx_multigpu.c).  0 in every
+ * case.  It must not race with pptk_rx_comm_destroy or pptk_rx_ctx_destroy
+ * of the same context. */
 int pptk_rx_comm_abort(struct pptk_rx_ctx *ctx);
 
 /* Wait until everything enqueued on `stream` (gathers included) is done,
@@ -553,6 +562,63 @@ int pptk_rx_place_buffers(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batc
 int pptk_rx_place_records(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *b,
                           void *const *d_cands, int ncand, int reps, int *best, float *ms,
                           void *stream);
+
+/* ---- Device rings owned by the library -----------------------------------
+ * The default way to get the device frame ring and record ring of a
+ * long-lived rx queue (an LDP/netmap ring lives for the process, reference
+ * ldp/ldpnetmap.c:163-185): the library allocates frame and record
+ * candidates spread apart in HBM, fills every frame candidate with a
+ * synthetic batch of the ring's geometry (fixed-stride IPv4/TCP frames of
+ * probe_len bytes, as many as fit, at most nrec), runs the receive
+ * transform on every (frames, records) pair as pptk_rx_place_buffers does,
+ * keeps the fastest pair and frees everything else -- so an application
+ * that takes its rings from here gets the placed pair without managing
+ * candidates (placement measured: C1500 4.03 ms placed against 4.80 ms on a
+ * plain allocation of the same box).  The frame ring's
+ * contents after the call are the probe batch: the application writes its
+ * frames over it.  Synchronous (uses `stream` for the probe).
+ * frame_cands 1..8 (0 = 3), rec_cands 1..16 (0 = 8), reps 1..20 (0 = 3),
+ * probe_len 64..1536 (0 = 1500); candidates beyond the first pair are
+ * allocated only as far as 60 % of the free device memory.  Freeing the
+ * candidates not kept makes the driver scrub that memory in the background
+ * (~20-30 GB/s; batches beside it run up to 9 % slower): with
+ * PPTK_RX_RING_SETTLE the call sleeps until it is over (settle_ms), else
+ * freed_bytes says how much was freed.  -EINVAL for a bad spec, -ENOMEM if
+ * not even one pair fits.  Release with pptk_rx_ring_free. */
+#define PPTK_RX_RING_SETTLE 0x1
+struct pptk_rx_ring_spec {
+  uint64_t frame_bytes;   /* frame ring bytes (the ring stays readable 64 B past it) */
+  uint64_t nrec;          /* records the record ring holds (<= 2^32 - 1) */
+  uint32_t rec_bytes;     /* 64 (struct pptk_rx_rec) or 32 (struct pptk_rx_rec32) */
+  uint32_t probe_len;     /* probe frame length, 0 = 1500 */
+  uint32_t frame_cands;   /* 0 = 3 */
+  uint32_t rec_cands;     /* 0 = 8 */
+  uint32_t reps;          /* timed probe launches per pair, 0 = 3 */
+  uint32_t flags;         /* PPTK_RX_RING_SETTLE */
+};
+struct pptk_rx_ring {
+  uint8_t *d_frames;      /* frame_bytes (+ 64 readable) */
+  void *d_recs;           /* nrec * rec_bytes */
+  uint64_t frame_bytes;
+  uint64_t nrec;
+  uint32_t rec_bytes;
+  int32_t device;         /* the context's device */
+  uint32_t frame_cands;   /* candidates actually probed */
+  uint32_t rec_cands;
+  int32_t chosen_frames;  /* the pair kept (candidate indices) */
+  int32_t chosen_recs;
+  float chosen_ms;        /* probe median launch time on the pair kept */
+  float first_ms;         /* ... on candidate pair (0, 0): a plain allocation */
+  uint64_t probe_frames;  /* frames in the probe batch */
+  uint64_t freed_bytes;   /* candidates and spacers freed */
+  uint32_t settle_ms;     /* slept for the scrub (PPTK_RX_RING_SETTLE) */
+  uint32_t reserved;
+};
+int pptk_rx_ring_alloc(struct pptk_rx_ctx *ctx, const struct pptk_rx_ring_spec *spec,
+                       struct pptk_rx_ring *ring, void *stream);
+/* Frees both rings (on ring->device; the context need not exist any more)
+ * and zeroes *ring.  Every batch using them must have completed. */
+int pptk_rx_ring_free(struct pptk_rx_ring *ring);
 
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);

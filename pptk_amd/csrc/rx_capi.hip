@@ -159,6 +159,7 @@ struct pptk_rx_ctx {
   // ordered pool (allocated and freed on the call's stream, so concurrent
   // tx calls on different streams never share one), or the caller's buffer
   hipMemPool_t txpool = nullptr;
+  std::mutex txpool_mu;   // tx calls of one context may run on several threads
   uint64_t *d_txuser = nullptr;   // pptk_tx_set_side_buffer
   uint64_t txuser_n = 0;
   int ncu = 256;
@@ -663,20 +664,26 @@ int pptk_tx_cksum_device(struct pptk_rx_ctx *c, uint8_t *d_frames, const uint64_
     uint64_t *side = c->d_txuser && c->txuser_n >= n ? c->d_txuser : nullptr;
     const bool pooled = side == nullptr;
     if (pooled) {   // stream-ordered: this call's own array, freed behind it
-      if (!c->txpool) {
-        hipMemPoolProps pp;
-        memset(&pp, 0, sizeof(pp));
-        pp.allocType = hipMemAllocationTypePinned;
-        pp.location.type = hipMemLocationTypeDevice;
-        pp.location.id = c->device;
-        if (hipMemPoolCreate(&c->txpool, &pp) != hipSuccess) {
-          c->txpool = nullptr;
-          return -ENOMEM;
+      hipMemPool_t pool;
+      {
+        // created once, by whichever tx call comes first (two threads'
+        // first calls may race)
+        std::lock_guard<std::mutex> g(c->txpool_mu);
+        if (!c->txpool) {
+          hipMemPoolProps pp;
+          memset(&pp, 0, sizeof(pp));
+          pp.allocType = hipMemAllocationTypePinned;
+          pp.location.type = hipMemLocationTypeDevice;
+          pp.location.id = c->device;
+          hipMemPool_t np = nullptr;
+          if (hipMemPoolCreate(&np, &pp) != hipSuccess) return -ENOMEM;
+          uint64_t keep = UINT64_MAX;   // keep freed blocks for the next call
+          (void)hipMemPoolSetAttribute(np, hipMemPoolAttrReleaseThreshold, &keep);
+          c->txpool = np;
         }
-        uint64_t keep = UINT64_MAX;   // keep freed blocks for the next call
-        (void)hipMemPoolSetAttribute(c->txpool, hipMemPoolAttrReleaseThreshold, &keep);
+        pool = c->txpool;
       }
-      if (hipMallocFromPoolAsync((void **)&side, n * 8, c->txpool, s) != hipSuccess)
+      if (hipMallocFromPoolAsync((void **)&side, n * 8, pool, s) != hipSuccess)
         return -ENOMEM;
     }
     a.txside = side;

@@ -38,9 +38,12 @@
 // RCCL argument errors -EINVAL, every other RCCL or HIP failure -EIO.
 #include <dlfcn.h>
 #include <errno.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
+#include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -58,7 +61,6 @@ using namespace pptk;
 // Experiment builds: PPTK_RX_COMM_TRACE=1 traces the communicator calls.
 #ifdef PPTK_RX_EXPERIMENTS
 #include <stdio.h>
-#include <stdlib.h>
 #define COMM_TRACE(...)                                              \
   do {                                                               \
     static const bool on_ = getenv("PPTK_RX_COMM_TRACE") != nullptr; \
@@ -143,16 +145,40 @@ struct Backoff {
   }
 };
 
+struct InitJob;
+
+// A context's communicator slot.  Besides a live (or aborted) communicator
+// it holds, while pptk_rx_comm_create runs, the creation in progress (so an
+// abort from another thread can cancel it), and, when an abort arrives at a
+// context that has no communicator yet, that pending abort (its next
+// pptk_rx_comm_create returns -ECANCELED at once).
+enum class CommState { kCreating, kReady, kPendingAbort };
+
 struct RxComm {
-  std::mutex mu;          // guards comm against a concurrent abort
+  std::mutex mu;          // guards comm and state against a concurrent abort
+  CommState state = CommState::kReady;
   ncclComm_t comm = nullptr;
   int nranks = 0;
   int rank = 0;
   bool aborted = false;   // comm is gone (aborted); only the struct remains
+  std::shared_ptr<InitJob> job;   // kCreating: the creation to cancel
 };
+
+// Slot reads that go on to lock an RxComm (abort) and slot clears that
+// delete one (a failed or cancelled creation, a consumed pending abort,
+// destroy) are serialised by this lock, so an abort from another thread
+// never touches a deleted RxComm.
+std::mutex g_slots;
 
 RxComm *comm_of(const pptk_rx_ctx *c) {
   return (RxComm *)ctx_comm_slot((pptk_rx_ctx *)c)->load(std::memory_order_acquire);
+}
+
+// The context's communicator, if it has one (live or aborted): not a
+// creation in progress, not a pending abort.
+RxComm *live_comm_of(const pptk_rx_ctx *c) {
+  RxComm *m = comm_of(c);
+  return m && m->state == CommState::kReady ? m : nullptr;
 }
 
 void set_comm(pptk_rx_ctx *c, RxComm *m) {
@@ -223,12 +249,44 @@ struct InitJob {
   std::mutex mu;
   std::condition_variable cv;
   bool done = false, abandoned = false;
+  bool cancelled = false;   // pptk_rx_comm_abort on a context being created
   ncclResult_t r = ncclSuccess;
   std::vector<ncclComm_t> comms;
 };
 
+// Helper threads the caller gave up on (deadline or abort) that have not
+// finished yet: one stuck inside RCCL's synchronous init stays until the
+// missing rank appears or the process exits, so a caller retrying creation
+// could pile them up; beyond kMaxAbandoned creation returns -EAGAIN.
+constexpr int kMaxAbandoned = 4;
+std::atomic<int> g_abandoned{0};
+
+bool job_abandoned(const std::shared_ptr<InitJob> &job) {
+  std::lock_guard<std::mutex> g(job->mu);
+  return job->abandoned;
+}
+
+// Fault injection for the failure-containment tests (a rank that inits but
+// never issues the warm-up gather cannot be staged on a one-GPU box):
+// PPTK_RX_COMM_TEST_WARMUP_STALL_MS=t holds the warm-up stream behind a
+// kernel that spins for t ms (bounded: at most 60 s) before the gather, as a
+// peer that never arrives would.  Read at each creation; unset in production.
+__global__ void warmup_stall_kernel(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+uint32_t warmup_stall_ms() {
+  const char *e = getenv("PPTK_RX_COMM_TEST_WARMUP_STALL_MS");
+  const long v = e ? atol(e) : 0;
+  return v <= 0 ? 0u : (uint32_t)std::min(v, 60000L);
+}
+
 void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
-              std::vector<int> devs, std::vector<int> ranks, int nranks) {
+              std::vector<int> devs, std::vector<int> ranks, int nranks, uint32_t timeout_ms) {
+  // the helper's own bound (the caller's deadline plus a margin): even if
+  // nobody marks the job abandoned, no wait here is unbounded
+  const Deadline until(timeout_ms + 1000);
   const size_t k = devs.size();
   std::vector<ncclComm_t> comms(k, nullptr);
   std::vector<ncclConfig_t> cfg(k, nonblocking_config());
@@ -254,9 +312,9 @@ void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
       ++i;
       continue;
     }
-    {
-      std::lock_guard<std::mutex> g(job->mu);
-      if (job->abandoned) break;
+    if (job_abandoned(job) || until.passed()) {
+      r = ncclInProgress;
+      break;
     }
     b.pause();
   }
@@ -267,31 +325,68 @@ void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
   if (r == ncclSuccess) {
     std::vector<hipStream_t> st(k, nullptr);
     std::vector<uint64_t *> buf(k, nullptr);
+    const uint32_t stall = warmup_stall_ms();
     for (size_t i = 0; i < k && r == ncclSuccess; ++i)
       if (hipSetDevice(devs[i]) != hipSuccess ||
           hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess ||
           hipMalloc((void **)&buf[i], (size_t)nranks * 8) != hipSuccess ||
           hipMemsetAsync(buf[i], 0, (size_t)nranks * 8, st[i]) != hipSuccess)
         r = ncclUnhandledCudaError;
+    for (size_t i = 0; i < k && r == ncclSuccess && stall; ++i) {
+      (void)hipSetDevice(devs[i]);
+      hipLaunchKernelGGL(warmup_stall_kernel, dim3(1), dim3(64), 0, st[i], (uint64_t)stall * 100000u);
+    }
     if (r == ncclSuccess && k > 1) r = R->GroupStart();
     for (size_t i = 0; i < k && going(r); ++i) {
       (void)hipSetDevice(devs[i]);
       r = R->AllGather(buf[i] + ranks[i], buf[i], 1, ncclUint64, comms[i], st[i]);
     }
     if (k > 1 && going(r)) r = R->GroupEnd();
-    for (size_t i = 0; i < k && going(r); ++i) {   // enqueued; now let it finish
+    // Enqueued; now let it finish -- polled, never a blocking wait: a peer
+    // that inits but never issues its part of the gather would otherwise
+    // keep this thread (and RCCL's kernel) waiting for ever.  Given up on
+    // (abandoned by the caller, or this thread's own deadline), the new
+    // communicators are aborted, so RCCL's kernels return and the streams
+    // drain before the buffers are freed.
+    bool quit = false;
+    for (size_t i = 0; i < k && going(r) && !quit;) {
       ncclResult_t st2 = ncclInProgress;
-      while (R->CommGetAsyncError(comms[i], &st2) == ncclSuccess && st2 == ncclInProgress)
-        b.pause();
-      r = st2;
+      if (R->CommGetAsyncError(comms[i], &st2) != ncclSuccess) st2 = ncclInternalError;
       (void)hipSetDevice(devs[i]);
-      if (r == ncclSuccess && hipStreamSynchronize(st[i]) != hipSuccess)
+      const hipError_t q = hipStreamQuery(st[i]);
+      if (st2 != ncclSuccess && st2 != ncclInProgress) {
+        r = st2;
+      } else if (q == hipSuccess && st2 == ncclSuccess) {
+        ++i;
+      } else if (q != hipSuccess && q != hipErrorNotReady) {
         r = ncclUnhandledCudaError;
+      } else if (job_abandoned(job) || until.passed()) {
+        quit = true;
+        r = ncclInProgress;
+      } else {
+        b.pause();
+      }
     }
+    if (r != ncclSuccess) {
+      for (size_t i = 0; i < k; ++i)
+        if (comms[i] && hipSetDevice(devs[i]) == hipSuccess) (void)R->CommAbort(comms[i]);
+      comms.assign(k, nullptr);
+    }
+    // (an aborted gather returns; a stream still busy after 10 s keeps its
+    // buffer: leaked rather than freed under a running kernel)
+    const Deadline drain(10000);
+    Backoff b2;
     for (size_t i = 0; i < k; ++i) {
       (void)hipSetDevice(devs[i]);
-      if (buf[i]) (void)hipFree(buf[i]);
-      if (st[i]) (void)hipStreamDestroy(st[i]);
+      bool idle = !st[i];
+      while (!idle) {
+        const hipError_t q = hipStreamQuery(st[i]);
+        idle = q != hipErrorNotReady;
+        if (!idle && drain.passed()) break;
+        if (!idle) b2.pause();
+      }
+      if (idle && buf[i]) (void)hipFree(buf[i]);
+      if (idle && st[i]) (void)hipStreamDestroy(st[i]);
     }
     COMM_TRACE("init job: warm-up gather %d", (int)r);
   }
@@ -305,10 +400,11 @@ void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
       job->done = true;
     }
   }
-  if (abandoned) {   // the caller returned -ETIMEDOUT: nobody owns these
+  if (abandoned) {   // the caller returned -ETIMEDOUT / -ECANCELED: nobody owns these
     COMM_TRACE("init job: abandoned, aborting");
     for (size_t i = 0; i < k; ++i)
       if (comms[i] && hipSetDevice(devs[i]) == hipSuccess) (void)R->CommAbort(comms[i]);
+    g_abandoned.fetch_sub(1);
   } else {
     job->cv.notify_all();
   }
@@ -317,33 +413,114 @@ void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
 // Start the init of ranks[i] on devs[i] (i < devs.size()) of an
 // nranks-rank communicator and wait for it, at most timeout_ms.  0 with
 // comms filled, or -errno with nothing left behind for the caller.
-int bounded_init(const Rccl *R, const ncclUniqueId &id, const std::vector<int> &devs,
-                 const std::vector<int> &ranks, int nranks, uint32_t timeout_ms,
-                 std::vector<ncclComm_t> &comms) {
-  std::shared_ptr<InitJob> job;
+// `job` is created by the caller (and published in the contexts' slots,
+// so that pptk_rx_comm_abort can cancel it: -ECANCELED).  -EAGAIN when too
+// many earlier helpers are still stuck (kMaxAbandoned).
+int bounded_init(const Rccl *R, const std::shared_ptr<InitJob> &job, const ncclUniqueId &id,
+                 const std::vector<int> &devs, const std::vector<int> &ranks, int nranks,
+                 uint32_t timeout_ms, std::vector<ncclComm_t> &comms) {
+  if (g_abandoned.load() >= kMaxAbandoned) return -EAGAIN;
   try {
-    job = std::make_shared<InitJob>();
-    std::thread(init_run, R, job, id, devs, ranks, nranks).detach();
+    std::thread(init_run, R, job, id, devs, ranks, nranks, timeout_ms).detach();
   } catch (...) {
     return -EAGAIN;
   }
   const auto until = Clock::now() + std::chrono::milliseconds(timeout_ms);
   std::unique_lock<std::mutex> g(job->mu);
-  if (!job->cv.wait_until(g, until, [&] { return job->done; })) {
-    job->abandoned = true;
-    COMM_TRACE("create: deadline passed, init abandoned");
-    return -ETIMEDOUT;
+  const bool done = job->cv.wait_until(g, until, [&] { return job->done || job->cancelled; });
+  if (!job->done) {
+    job->abandoned = true;   // the helper aborts what it builds and counts itself out
+    g_abandoned.fetch_add(1);
+    COMM_TRACE("create: %s, init abandoned", done ? "cancelled" : "deadline passed");
+    return done ? -ECANCELED : -ETIMEDOUT;
   }
   const ncclResult_t r = job->r;
+  const bool cancelled = job->cancelled;
   comms = job->comms;
   g.unlock();
-  if (r == ncclSuccess) return 0;
+  if (r == ncclSuccess && !cancelled) return 0;
   int prev = -1;
   (void)hipGetDevice(&prev);
   for (size_t i = 0; i < comms.size(); ++i)
     if (comms[i] && hipSetDevice(devs[i]) == hipSuccess) (void)R->CommAbort(comms[i]);
   if (prev >= 0) (void)hipSetDevice(prev);
+  comms.clear();
+  if (cancelled) return -ECANCELED;
   return r == ncclInProgress ? -ETIMEDOUT : nccl_err(r);
+}
+
+// Publish a creation in progress in each context's slot.  -ECANCELED (and
+// the pending aborts consumed) if an abort is pending on any of them,
+// -EINVAL if one already has a communicator or a creation in progress.
+int begin_create(pptk_rx_ctx *const *ctxs, int n, const std::shared_ptr<InitJob> &job,
+                 std::vector<RxComm *> &ms) {
+  std::lock_guard<std::mutex> g(g_slots);
+  bool pending = false;
+  for (int i = 0; i < n; ++i) {
+    RxComm *m = comm_of(ctxs[i]);
+    if (m && m->state != CommState::kPendingAbort) return -EINVAL;
+    pending = pending || m != nullptr;
+  }
+  if (pending) {
+    for (int i = 0; i < n; ++i)
+      if (RxComm *m = comm_of(ctxs[i])) {
+        set_comm(ctxs[i], nullptr);
+        delete m;
+      }
+    return -ECANCELED;
+  }
+  ms.assign((size_t)n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    RxComm *m = new (std::nothrow) RxComm();
+    if (!m) {
+      for (int k = 0; k < i; ++k) {
+        set_comm(ctxs[k], nullptr);
+        delete ms[(size_t)k];
+      }
+      return -ENOMEM;
+    }
+    m->state = CommState::kCreating;
+    m->job = job;
+    ms[(size_t)i] = m;
+    set_comm(ctxs[i], m);
+  }
+  return 0;
+}
+
+// End a creation: on success the contexts' communicators go live (unless an
+// abort arrived after the init finished: then they are aborted and the
+// call fails with -ECANCELED); on failure the slots are cleared.
+int end_create(const Rccl *R, pptk_rx_ctx *const *ctxs, int n, std::vector<RxComm *> &ms,
+               const std::vector<ncclComm_t> &comms, int rc) {
+  std::lock_guard<std::mutex> g(g_slots);
+  if (rc == 0) {
+    bool cancelled = false;
+    for (int i = 0; i < n; ++i) {
+      std::lock_guard<std::mutex> gm(ms[(size_t)i]->mu);
+      std::lock_guard<std::mutex> gj(ms[(size_t)i]->job->mu);
+      cancelled = cancelled || ms[(size_t)i]->job->cancelled;
+    }
+    if (!cancelled) {
+      for (int i = 0; i < n; ++i) {
+        RxComm *m = ms[(size_t)i];
+        std::lock_guard<std::mutex> gm(m->mu);
+        m->comm = comms[(size_t)i];
+        m->state = CommState::kReady;
+        m->job.reset();
+      }
+      return 0;
+    }
+    for (int i = 0; i < n; ++i) {
+      DeviceScope ds(ctx_device(ctxs[i]));
+      (void)R->CommAbort(comms[(size_t)i]);
+    }
+    rc = -ECANCELED;
+  }
+  for (int i = 0; i < n; ++i) {
+    set_comm(ctxs[i], nullptr);
+    delete ms[(size_t)i];
+  }
+  return rc;
 }
 
 }  // namespace
@@ -353,7 +530,9 @@ namespace pptk {
 void comm_release(pptk_rx_ctx *c) {
   RxComm *m = comm_of(c);
   if (!m) return;
-  if (const Rccl *R = rccl()) teardown(R, m, ctx_comm_timeout_ms(c));
+  if (m->state == CommState::kReady)
+    if (const Rccl *R = rccl()) teardown(R, m, ctx_comm_timeout_ms(c));
+  std::lock_guard<std::mutex> g(g_slots);
   set_comm(c, nullptr);
   delete m;
 }
@@ -382,33 +561,33 @@ int pptk_rx_comm_uid(uint8_t uid[PPTK_RX_COMM_UID_BYTES]) {
 int pptk_rx_comm_create(struct pptk_rx_ctx *c, int nranks, int rank,
                         const uint8_t uid[PPTK_RX_COMM_UID_BYTES]) {
   if (!c || !uid || nranks < 1 || rank < 0 || rank >= nranks) return -EINVAL;
-  if (comm_of(c)) return -EINVAL;   // one communicator per context
   const Rccl *R = rccl();
   if (!R) return -ENOSYS;
-  RxComm *m = new (std::nothrow) RxComm();
-  if (!m) return -ENOMEM;
+  std::shared_ptr<InitJob> job;
+  try {
+    job = std::make_shared<InitJob>();
+  } catch (...) {
+    return -ENOMEM;
+  }
+  std::vector<RxComm *> ms;
+  int rc = begin_create(&c, 1, job, ms);
+  if (rc != 0) return rc;
+  ms[0]->nranks = nranks;
+  ms[0]->rank = rank;
   ncclUniqueId id;
   memcpy(&id, uid, sizeof(id));
   COMM_TRACE("create: init rank %d of %d", rank, nranks);
   std::vector<ncclComm_t> comms;
-  const int rc = bounded_init(R, id, {ctx_device(c)}, {rank}, nranks, ctx_comm_timeout_ms(c), comms);
+  rc = bounded_init(R, job, id, {ctx_device(c)}, {rank}, nranks, ctx_comm_timeout_ms(c), comms);
   COMM_TRACE("create: %d", rc);
-  if (rc == 0) m->comm = comms[0];
-  if (rc != 0) {
-    delete m;
-    return rc;
-  }
-  m->nranks = nranks;
-  m->rank = rank;
-  set_comm(c, m);
-  return 0;
+  return end_create(R, &c, 1, ms, comms, rc);
 }
 
 int pptk_rx_comm_create_all(struct pptk_rx_ctx *const *ctxs, int n) {
   if (!ctxs || n < 1) return -EINVAL;
   std::vector<int> devs((size_t)n);
   for (int i = 0; i < n; ++i) {
-    if (!ctxs[i] || comm_of(ctxs[i])) return -EINVAL;
+    if (!ctxs[i]) return -EINVAL;
     devs[(size_t)i] = ctx_device(ctxs[i]);
     for (int k = 0; k < i; ++k)   // one rank per GPU
       if (devs[(size_t)k] == devs[(size_t)i] || ctxs[k] == ctxs[i]) return -EINVAL;
@@ -418,55 +597,66 @@ int pptk_rx_comm_create_all(struct pptk_rx_ctx *const *ctxs, int n) {
   ncclUniqueId id;
   int rc = nccl_err(R->GetUniqueId(&id));
   if (rc != 0) return rc;
+  std::shared_ptr<InitJob> job;
+  try {
+    job = std::make_shared<InitJob>();
+  } catch (...) {
+    return -ENOMEM;
+  }
+  std::vector<RxComm *> ms;
+  if ((rc = begin_create(ctxs, n, job, ms)) != 0) return rc;
+  for (int i = 0; i < n; ++i) {
+    ms[(size_t)i]->nranks = n;
+    ms[(size_t)i]->rank = i;
+  }
   // one group of per-device inits (what ncclCommInitAll does), bounded
   std::vector<int> ranks((size_t)n);
   for (int i = 0; i < n; ++i) ranks[(size_t)i] = i;
   std::vector<ncclComm_t> comms;
-  rc = bounded_init(R, id, devs, ranks, n, ctx_comm_timeout_ms(ctxs[0]), comms);
-  if (rc != 0) return rc;
-  std::vector<RxComm *> ms((size_t)n, nullptr);
-  for (int i = 0; i < n && rc == 0; ++i)
-    if (!(ms[(size_t)i] = new (std::nothrow) RxComm())) rc = -ENOMEM;
-  if (rc != 0) {
-    for (int i = 0; i < n; ++i) {
-      DeviceScope ds(devs[(size_t)i]);
-      (void)R->CommAbort(comms[(size_t)i]);
-      delete ms[(size_t)i];
-    }
-    return rc;
-  }
-  for (int i = 0; i < n; ++i) {
-    RxComm *m = ms[(size_t)i];
-    m->comm = comms[(size_t)i];
-    m->nranks = n;
-    m->rank = i;
-    set_comm(ctxs[i], m);
-  }
-  return 0;
+  rc = bounded_init(R, job, id, devs, ranks, n, ctx_comm_timeout_ms(ctxs[0]), comms);
+  return end_create(R, ctxs, n, ms, comms, rc);
 }
 
 int pptk_rx_comm_destroy(struct pptk_rx_ctx *c) {
   if (!c) return -EINVAL;
+  RxComm *m = comm_of(c);
+  if (m && m->state == CommState::kCreating) return -EBUSY;
   DeviceScope ds(ctx_device(c));
-  comm_release(c);
+  comm_release(c);   // (also drops a pending abort)
   return 0;
 }
 
 int pptk_rx_comm_abort(struct pptk_rx_ctx *c) {
   if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(g_slots);
   RxComm *m = comm_of(c);
-  if (!m) return -EINVAL;
+  if (!m) {   // nothing to cancel yet: the context's next creation is
+    m = new (std::nothrow) RxComm();
+    if (!m) return -ENOMEM;
+    m->state = CommState::kPendingAbort;
+    set_comm(c, m);
+    return 0;
+  }
+  std::lock_guard<std::mutex> gm(m->mu);
+  if (m->state == CommState::kPendingAbort) return 0;
+  if (m->state == CommState::kCreating) {
+    {
+      std::lock_guard<std::mutex> gj(m->job->mu);
+      m->job->cancelled = true;
+    }
+    m->job->cv.notify_all();
+    return 0;
+  }
   const Rccl *R = rccl();
   if (!R) return -ENOSYS;
   DeviceScope ds(ctx_device(c));
-  std::lock_guard<std::mutex> g(m->mu);
   abort_locked(R, m);
   return 0;
 }
 
 int pptk_rx_comm_info(const struct pptk_rx_ctx *c, int *nranks, int *rank) {
   if (!c) return -EINVAL;
-  const RxComm *m = comm_of(c);
+  const RxComm *m = live_comm_of(c);
   if (!m) return -EINVAL;
   if (nranks) *nranks = m->nranks;
   if (rank) *rank = m->rank;
@@ -490,7 +680,7 @@ void pptk_rx_shard_range(uint64_t n, int nranks, int rank, uint64_t *first, uint
 int pptk_rx_allgather_hash(struct pptk_rx_ctx *c, const uint64_t *d_hash, uint64_t n,
                            uint64_t *d_out, void *stream) {
   if (!c) return -EINVAL;
-  RxComm *m = comm_of(c);
+  RxComm *m = live_comm_of(c);
   if (!m) return -EINVAL;
   if (n == 0) return 0;
   if (!d_hash || !d_out) return -EINVAL;
@@ -529,7 +719,7 @@ int pptk_rx_allgather_hash(struct pptk_rx_ctx *c, const uint64_t *d_hash, uint64
 
 int pptk_rx_comm_sync(struct pptk_rx_ctx *c, void *stream, uint32_t timeout_ms) {
   if (!c) return -EINVAL;
-  RxComm *m = comm_of(c);
+  RxComm *m = live_comm_of(c);
   const Rccl *R = m ? rccl() : nullptr;
   DeviceScope ds(ctx_device(c));
   if (!ds.ok) return -EIO;

@@ -34,6 +34,75 @@ class RxDevBatch(ctypes.Structure):
                 ("d_key", ctypes.c_void_p)]
 
 
+class RxRingSpec(ctypes.Structure):
+    """struct pptk_rx_ring_spec (include/pptk_rx.h "Device rings")."""
+    _fields_ = [("frame_bytes", ctypes.c_uint64), ("nrec", ctypes.c_uint64),
+                ("rec_bytes", ctypes.c_uint32), ("probe_len", ctypes.c_uint32),
+                ("frame_cands", ctypes.c_uint32), ("rec_cands", ctypes.c_uint32),
+                ("reps", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class RxRingC(ctypes.Structure):
+    """struct pptk_rx_ring."""
+    _fields_ = [("d_frames", ctypes.c_void_p), ("d_recs", ctypes.c_void_p),
+                ("frame_bytes", ctypes.c_uint64), ("nrec", ctypes.c_uint64),
+                ("rec_bytes", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("frame_cands", ctypes.c_uint32), ("rec_cands", ctypes.c_uint32),
+                ("chosen_frames", ctypes.c_int32), ("chosen_recs", ctypes.c_int32),
+                ("chosen_ms", ctypes.c_float), ("first_ms", ctypes.c_float),
+                ("probe_frames", ctypes.c_uint64), ("freed_bytes", ctypes.c_uint64),
+                ("settle_ms", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+RING_SETTLE = 0x1
+
+
+class _RingOwner:
+    """Frees a pptk_rx_ring when the last tensor over it is gone."""
+
+    def __init__(self, L, ring):
+        self.L, self.ring = L, ring
+
+    def __del__(self):
+        try:
+            if self.ring is not None:
+                self.L.pptk_rx_ring_free(ctypes.byref(self.ring))
+        except Exception:
+            pass
+        self.ring = None
+
+
+class _DevMem:
+    """A device range as a __cuda_array_interface__ object: torch.as_tensor
+    wraps it without copying and keeps it (and so the ring) alive."""
+
+    def __init__(self, owner, ptr, nbytes):
+        self.owner = owner
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1",
+                                         "data": (ptr, False), "version": 3, "strides": None}
+
+
+class DeviceRing:
+    """Library-owned placed device rings (pptk_rx_ring_alloc): .frames (torch
+    uint8, frame_bytes + 64), .recs (torch uint8 (nrec, rec_bytes)) and the
+    probe .report.  The rings are freed (pptk_rx_ring_free) once neither
+    tensor (nor a view of one) is referenced any more."""
+
+    def __init__(self, ctx, ring):
+        import torch
+        dev = torch.device("cuda", ctx.device)
+        own = _RingOwner(ctx._L, ring)
+        self.frames = torch.as_tensor(_DevMem(own, ring.d_frames, ring.frame_bytes + 64),
+                                      device=dev)
+        self.recs = torch.as_tensor(_DevMem(own, ring.d_recs, ring.nrec * ring.rec_bytes),
+                                    device=dev).view(ring.nrec, ring.rec_bytes)
+        self.report = {k: getattr(ring, k) for k in (
+            "frame_cands", "rec_cands", "chosen_frames", "chosen_recs", "settle_ms",
+            "probe_frames", "freed_bytes")}
+        self.report["chosen_ms"] = round(ring.chosen_ms, 4)
+        self.report["first_ms"] = round(ring.first_ms, 4)
+
+
 class LdpPacket(ctypes.Structure):
     """struct ldp_packet (include/ldp_packet.h; reference ldp/ldp.h:98-108)."""
     _fields_ = [("data", ctypes.c_void_p), ("sz", ctypes.c_uint32),
@@ -52,7 +121,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_set_side_buffer",
            "pptk_tx_rewrite_device",
            "pptk_tcp_mss_clamp_device", "pptk_rx_autotune", "pptk_rx_place_records",
-           "pptk_rx_place_buffers",
+           "pptk_rx_place_buffers", "pptk_rx_ring_alloc", "pptk_rx_ring_free",
            # multi-GPU (RCCL)
            "pptk_rx_device_count", "pptk_rx_comm_uid", "pptk_rx_comm_create",
            "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
@@ -121,6 +190,12 @@ def lib(path=None):
                                                 ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_float), vp]
             L.pptk_rx_place_buffers.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_ring_alloc"):           # absent from older A/B builds
+            L.pptk_rx_ring_alloc.argtypes = [vp, ctypes.POINTER(RxRingSpec),
+                                             ctypes.POINTER(RxRingC), vp]
+            L.pptk_rx_ring_alloc.restype = ctypes.c_int
+            L.pptk_rx_ring_free.argtypes = [ctypes.POINTER(RxRingC)]
+            L.pptk_rx_ring_free.restype = ctypes.c_int
         if hasattr(L, "pptk_tcp_mss_clamp_device"):    # absent from older A/B builds
             L.pptk_tcp_mss_clamp_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64,
                                                     ctypes.c_uint32, ctypes.c_uint64,
@@ -336,6 +411,21 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_place_buffers failed ({rc})")
         return bf.value, br.value, [round(x, 4) for x in ms[:nf * nr]]
+
+    def ring_alloc(self, frame_bytes, nrec, rec_bytes=64, probe_len=0, frame_cands=0,
+                   rec_cands=0, reps=0, settle=False, stream=None):
+        """pptk_rx_ring_alloc: placed device frame and record rings (a
+        DeviceRing; its .report carries the probe)."""
+        import torch
+        spec = RxRingSpec(frame_bytes, nrec, rec_bytes, probe_len, frame_cands, rec_cands, reps,
+                          RING_SETTLE if settle else 0)
+        ring = RxRingC()
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = self._L.pptk_rx_ring_alloc(self._ctx, ctypes.byref(spec), ctypes.byref(ring),
+                                        ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_ring_alloc failed ({rc})")
+        return DeviceRing(self, ring)
 
     def tuned_variant(self, frames, n, off=None, lens=None, stride=0, fixed_len=0, max_len=0,
                       compact=False):

@@ -531,6 +531,11 @@ def test_entry_points_reject_bad_arguments(lib):
     assert lib.pptk_rx_place_records(None, ctypes.byref(b), None, 1, 1, None, None, None) == EINVAL
     assert lib.pptk_rx_place_buffers(None, ctypes.byref(b), None, 1, None, 1, 1, None, None, None,
                                      None) == EINVAL
+    from pptk_amd.rx import RxRingC, RxRingSpec
+    spec, ring = RxRingSpec(1 << 20, 16, 64), RxRingC()
+    assert lib.pptk_rx_ring_alloc(None, ctypes.byref(spec), ctypes.byref(ring), None) == EINVAL
+    assert lib.pptk_rx_ring_free(None) == EINVAL
+    assert lib.pptk_rx_ring_free(ctypes.byref(ring)) == 0   # an empty ring: nothing to free
     lib.pptk_rx_ctx_destroy(None)                           # a no-op
 
 

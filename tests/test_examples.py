@@ -124,9 +124,11 @@ def test_rx_multigpu_thread_join_bit_exact(tmp_path):
 def test_rx_multigpu_failed_thread_exits_nonzero(tmp_path, join, ranks):
     """Failure containment: the last rank's thread fails (RX_MULTIGPU_FAIL).
     create_all form: it fails before its first gather and aborts every
-    communicator.  Thread-join form, two ranks: it never joins, so rank 0's
-    pptk_rx_comm_create must give up at the deadline (ETIMEDOUT, -110)
-    instead of blocking forever.  Either way the process exits 1, promptly."""
+    communicator.  Thread-join form, two ranks: it fails instead of joining
+    and aborts every context, so rank 0's pptk_rx_comm_create -- whether
+    already waiting or not yet called -- returns ECANCELED (-125) at once
+    instead of waiting for the 3 s deadline.  Either way the process exits 1,
+    promptly."""
     import time
     p = str(tmp_path / "s.rxq")
     write_rxq(p, ("edge",))
@@ -139,7 +141,7 @@ def test_rx_multigpu_failed_thread_exits_nonzero(tmp_path, join, ranks):
     assert out.returncode == 1, out.stdout + out.stderr
     assert "FAILED" in out.stdout and took < 60, (took, out.stdout)
     if join == "threads":
-        assert "rc -110" in out.stdout, out.stdout          # rank 0: ETIMEDOUT
+        assert "rc -125" in out.stdout, out.stdout          # rank 0: ECANCELED
 
 
 @pytest.mark.gpu

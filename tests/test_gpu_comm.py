@@ -275,11 +275,97 @@ def test_comm_sync_and_abort(dev):
     assert e.value.errno == ECANCELED
     assert ctx.comm_info() == (1, 0)
     ctx.comm_destroy()
-    with pytest.raises(OSError) as e:                       # no communicator
-        ctx.comm_abort()
-    assert e.value.errno == EINVAL
     assert ctx.comm_sync(s, 1000) == 0                      # plain bounded stream wait
     ctx.comm_create(1, 0, comm_uid())
     got, _ = _gather_set(ctx, z, dev)
     assert np.array_equal(got, want)
+    ctx.close()
+
+
+def _timed_create(ctx, nranks, rank, uid):
+    import time
+    t0 = time.monotonic()
+    try:
+        ctx.comm_create(nranks, rank, uid)
+        rc = 0
+    except OSError as e:
+        rc = -e.errno
+    return rc, time.monotonic() - t0
+
+
+def test_comm_abort_during_create_cancels(dev):
+    """pptk_rx_comm_abort from another thread while pptk_rx_comm_create is
+    still waiting (a 2-rank communicator whose rank 1 never joins, 30 s
+    deadline): the create returns ECANCELED well inside its deadline, the
+    context is left without a communicator, and then builds a 1-rank one
+    whose gather equals the golden flow hashes (reference model: the queue
+    threads of ldp/ldprecvmt.c:174-182 share nothing)."""
+    import threading
+    import time
+    from pptk_amd.rx import RxContext, comm_uid
+    z = load_golden("edge")
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_frame=65535, comm_timeout_ms=30000)
+    res = {}
+    th = threading.Thread(target=lambda: res.update(r=_timed_create(ctx, 2, 0, comm_uid())))
+    th.start()
+    time.sleep(1.0)
+    ctx.comm_abort()
+    th.join(20)
+    assert not th.is_alive()
+    rc, took = res["r"]
+    assert rc == -ECANCELED, rc
+    assert took < 10, took
+    assert ctx.comm_info() is None
+    ctx.comm_create(1, 0, comm_uid())
+    got, _ = _gather_set(ctx, z, dev)
+    assert np.array_equal(got, as_records(z["recs"])["flow_hash"])
+    assert ctx.comm_sync() == 0
+    ctx.close()
+
+
+def test_comm_pending_abort(dev):
+    """An abort that reaches a context before its pptk_rx_comm_create (a
+    sibling failed first) is kept: that create returns ECANCELED at once
+    instead of waiting for ranks that will never come; the next create
+    works.  comm_destroy drops a pending abort."""
+    from pptk_amd.rx import comm_uid
+    z = load_golden("cmix")
+    ctx = _ctx(z)
+    ctx.comm_abort()
+    ctx.comm_abort()                                        # still one pending abort
+    rc, took = _timed_create(ctx, 2, 0, comm_uid())
+    assert rc == -ECANCELED and took < 1.0, (rc, took)
+    assert ctx.comm_info() is None
+    ctx.comm_abort()
+    ctx.comm_destroy()                                      # drops it
+    ctx.comm_create(1, 0, comm_uid())
+    got, _ = _gather_set(ctx, z, dev)
+    assert np.array_equal(got, as_records(z["recs"])["flow_hash"])
+    ctx.close()
+
+
+def test_comm_warmup_gather_stall_is_bounded(dev, monkeypatch):
+    """A peer that inits but never issues its part of the creation's
+    warm-up gather (staged on one GPU by PPTK_RX_COMM_TEST_WARMUP_STALL_MS,
+    which holds the warm-up stream behind a 6 s spin): the create returns
+    ETIMEDOUT at its 1.5 s deadline, the helper aborts the new communicator
+    so the stream drains, a new communicator on the same context gathers the
+    golden hashes, and a device-wide synchronize then returns (nothing of
+    the abandoned creation is left running)."""
+    import time
+    from pptk_amd.rx import RxContext, comm_uid
+    z = load_golden("fuzz")
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_frame=65535, comm_timeout_ms=1500)
+    monkeypatch.setenv("PPTK_RX_COMM_TEST_WARMUP_STALL_MS", "6000")
+    rc, took = _timed_create(ctx, 1, 0, comm_uid())
+    assert rc == -ETIMEDOUT and 1.2 < took < 5, (rc, took)
+    monkeypatch.delenv("PPTK_RX_COMM_TEST_WARMUP_STALL_MS")
+    ctx.comm_create(1, 0, comm_uid())
+    got, _ = _gather_set(ctx, z, dev)
+    assert np.array_equal(got, as_records(z["recs"])["flow_hash"])
+    t0 = time.monotonic()
+    torch.cuda.synchronize()
+    assert time.monotonic() - t0 < 15
     ctx.close()

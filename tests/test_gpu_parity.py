@@ -970,3 +970,60 @@ def test_place_buffers(dev):
     with pytest.raises(OSError):
         ctx.place_buffers([], n, recs, off=off, lens=lens)
     ctx.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_ring_alloc(compact, dev):
+    """pptk_rx_ring_alloc: the library allocates and probes candidate (frames,
+    records) pairs and keeps the fastest; the rings it returns are sized as
+    asked, the report is consistent, the golden batch written into the frame
+    ring gives the exact records in the record ring, and the rings are freed
+    when the last tensor over them goes (the device memory comes back)."""
+    import gc
+    z = load_golden("cmix")
+    n = len(z["off"])
+    ctx = _ctx(z)
+    rb = 32 if compact else 64
+    fbytes = max(z["buf"].size, 1500 * 4096)
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(dev)
+    ring = ctx.ring_alloc(fbytes, n, rb, frame_cands=2, rec_cands=3, reps=2)
+    rep = ring.report
+    assert ring.frames.numel() == fbytes + 64 and tuple(ring.recs.shape) == (n, rb)
+    assert rep["frame_cands"] == 2 and rep["rec_cands"] == 3
+    assert 0 <= rep["chosen_frames"] < 2 and 0 <= rep["chosen_recs"] < 3
+    assert 0 < rep["chosen_ms"] <= rep["first_ms"] or rep["chosen_frames"] + rep["chosen_recs"] == 0
+    assert rep["probe_frames"] == min(n, fbytes // 1500) and rep["freed_bytes"] > 0
+    ring.frames[:z["buf"].size].copy_(torch.from_numpy(z["buf"]).to(dev))
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    ctx.batch_device(ring.frames, n, off=off, lens=lens, max_len=1500, recs=ring.recs,
+                     compact=compact)
+    torch.cuda.synchronize()
+    want = to_rec32(z["recs"]) if compact else z["recs"]
+    d = diff_records(ring.recs.cpu().numpy().reshape(-1), want,
+                     dtype=REC32_DTYPE if compact else as_records(z["recs"]).dtype)
+    assert not d, d
+    del ring
+    gc.collect()
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info(dev)
+    assert free1 >= free0 - (64 << 20)
+    ctx.close()
+
+
+def test_ring_alloc_rejects(dev):
+    """Bad ring specs are -EINVAL before anything is allocated."""
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    for kw in (dict(frame_bytes=0, nrec=10), dict(frame_bytes=1 << 20, nrec=0),
+               dict(frame_bytes=1 << 20, nrec=10, rec_bytes=48),
+               dict(frame_bytes=1 << 20, nrec=10, probe_len=63),
+               dict(frame_bytes=1 << 20, nrec=10, probe_len=1537),
+               dict(frame_bytes=1 << 20, nrec=10, frame_cands=9),
+               dict(frame_bytes=1 << 20, nrec=10, rec_cands=17),
+               dict(frame_bytes=100, nrec=10)):          # no probe frame fits
+        with pytest.raises(OSError) as e:
+            ctx.ring_alloc(**kw)
+        assert e.value.errno == 22, kw
+    ctx.close()

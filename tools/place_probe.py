@@ -410,6 +410,84 @@ def bursts(args):
     print(json.dumps({"pairs": out, "sol_setting": sol_how}), flush=True)
 
 
+def xstage(args):
+    """Round-4 probe: records staged per XCD group and flushed as 256 KB
+    runs (tools/rwmix.hip rw_xstage_kernel) against the rx kernel and the
+    4 KB / 256 KB burst kernels, on every (frames, records) pair as
+    `bursts` allocates them.  One JSON line: per pair the medians, plus the
+    blockIdx -> XCC census of the probe's grid."""
+    import ctypes
+    import torch
+    from pptk_amd.rx import RxContext
+    from tools.rwmix import _lib
+    from tools.synth import make_batch
+    dev = torch.device("cuda", 0)
+    n = args.n
+    ctx = RxContext(0, bytes(range(1, 17)))
+    L = _lib()
+    vp = ctypes.c_void_p
+    L.rwxstage_run.argtypes = [vp, vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32,
+                               ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.rwxstage_run.restype = ctypes.c_int
+    L.xcc_census.argtypes = [vp, ctypes.c_int, vp]
+    L.rwblk_run.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                            ctypes.c_int, ctypes.c_int, vp, vp]
+    hold, bs, rs = [], [], []
+    for k in range(args.batches):
+        if k:
+            hold.append(torch.empty(8 << 30, dtype=torch.uint8, device=dev))
+        bs.append(make_batch("c1500", n, dev, first=k * n))
+    for _ in range(args.matrix or 2):
+        hold.append(torch.empty(4 << 30, dtype=torch.uint8, device=dev))
+        rs.append(torch.zeros((n, 64), dtype=torch.uint8, device=dev))
+    sink = torch.zeros(64, dtype=torch.int32, device=dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    s = torch.cuda.current_stream(dev)
+    ntiles = n * 1500 // 96000
+    stg = torch.empty(8 * 32 * 64 * 4096, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros((ntiles + 63) // 64 + 64, dtype=torch.int32, device=dev)
+    gen = torch.zeros(8 * 32, dtype=torch.int32, device=dev)
+    census = torch.zeros(ncu * 2, dtype=torch.int32, device=dev)
+    L.xcc_census(census.data_ptr(), ncu * 2, vp(s.cuda_stream))
+    torch.cuda.synchronize()
+    cen = census.tolist()
+    groups_ok = all(cen[b] == cen[b % 8] for b in range(len(cen)))
+    modes = [("rx", 0, 0), ("mix4k", 96000, 4096), ("mix256k", 64 * 96000, 262144),
+             ("xorder", 0, 0), ("xst4nosync", 4, 5), ("xst8nosync", 8, 5),
+             ("xst16nosync", 16, 5), ("xst8nosync_nt", 8, 7)]
+    t = {}
+    for rep in range(args.reps + 1):
+        for bi, b in enumerate(bs):
+            for ri, r in enumerate(rs):
+                for name, p1, p2 in modes:
+                    a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    if name == "rx":
+                        ctx.batch_device(b["frames"], n, stride=1500, fixed_len=1500, recs=r)
+                    elif name.startswith("blk"):
+                        L.rwblk_run(b["frames"].data_ptr(), r.data_ptr(), ntiles, 96000, 4096, p1,
+                                    ncu * 2, sink.data_ptr(), vp(s.cuda_stream))
+                    elif name.startswith("mix"):
+                        L.rwmix_run(b["frames"].data_ptr(), r.data_ptr(), n * 1500 // p1, p1, p2, 1,
+                                    ncu * 2, sink.data_ptr(), vp(s.cuda_stream))
+                    else:
+                        ns, mode = (8, 0) if name == "xorder" else (p1, p2)
+                        rc = L.rwxstage_run(b["frames"].data_ptr(), r.data_ptr(), stg.data_ptr(),
+                                            cnt.data_ptr(), gen.data_ptr(), ntiles, 96000, 4096,
+                                            ns, mode, ncu * 2, sink.data_ptr(), vp(s.cuda_stream))
+                        assert rc == 0, rc
+                    z.record()
+                    torch.cuda.synchronize()
+                    if rep:
+                        t.setdefault((bi, ri, name), []).append(a.elapsed_time(z))
+        print(json.dumps({"rep": rep}), file=sys.stderr, flush=True)
+    out = {}
+    for (bi, ri, name), v in sorted(t.items()):
+        out.setdefault(f"{bi},{ri}", {})[name] = round(sorted(v)[len(v) // 2], 3)
+    print(json.dumps({"pairs": out, "census_groups_share_xcc": groups_ok,
+                      "census_first16": cen[:16]}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-mb", type=float, default=16)
@@ -426,6 +504,7 @@ def main():
     ap.add_argument("--txplace", action="store_true")
     ap.add_argument("--txside", action="store_true")
     ap.add_argument("--bursts", action="store_true")
+    ap.add_argument("--xstage", action="store_true")
     ap.add_argument("--batches", type=int, default=2)
     ap.add_argument("--spacer-gb", type=float, default=0.0,
                     help="matrix: allocate this many GB before every batch after the first "
@@ -433,6 +512,8 @@ def main():
     args = ap.parse_args()
     if args.bursts:
         return bursts(args)
+    if args.xstage:
+        return xstage(args)
     if args.matrix:
         return matrix(args)
     if args.policies:

@@ -44,6 +44,46 @@ __global__ __launch_bounds__(256) void rw_kernel(const u32x4 *in, u32x4 *out, ui
   if (x == 0x9e3779b9u) sink[lane] = x;
 }
 
+// Blocked tile order: wave w takes runs of B consecutive tiles (run w,
+// w + nwaves, ...) and writes each tile's wb bytes right after it (4 KB
+// bursts, like the rx kernel, but a wave's reads walk one contiguous span).
+template <int B>
+__global__ __launch_bounds__(256) void rw_blk_kernel(const u32x4 *in, u32x4 *out, uint64_t ntiles,
+                                                     uint32_t rb16, uint32_t wb16, uint32_t *sink) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  const uint64_t wid = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  u32x4 acc = {0, 0, 0, 0};
+  for (uint64_t r = wid; r * B < ntiles; r += nwaves)
+    for (uint64_t t = r * B; t < min(ntiles, r * B + B); ++t) {
+      const u32x4 *p = in + t * rb16;
+      uint32_t k = lane;
+      for (; k + 7 * 64 < rb16; k += 8 * 64) {
+        u32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + k + u * 64);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= v[u];
+      }
+      for (; k < rb16; k += 64) acc ^= __builtin_nontemporal_load(p + k);
+      u32x4 *q = out + t * (uint64_t)wb16;
+      for (uint32_t e = lane; e < wb16; e += 64) __builtin_nontemporal_store(acc, q + e);
+    }
+  const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (x == 0x9e3779b9u) sink[lane] = x;
+}
+
+extern "C" int rwblk_run(const void *in, void *out, uint64_t ntiles, uint32_t rb, uint32_t wb,
+                         int b, int grid, uint32_t *sink, void *stream) {
+  if (b == 64)
+    hipLaunchKernelGGL(rw_blk_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4 *)in, (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  else
+    hipLaunchKernelGGL(rw_blk_kernel<8>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4 *)in, (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 // Speed-of-light kernel for an rx launch's exact traffic (bench.py mix_sol):
 // tile t = frames [64t, 64t + 64); its bytes are the contiguous span
 // [t * rb, t * rb + rb) (fixed stride) or, for frames packed in batch order
@@ -231,6 +271,115 @@ extern "C" int rwstage_run(const void *in, void *out, uint64_t ntiles, uint32_t 
   else
     hipLaunchKernelGGL(rw_stage_kernel<4>, dim3(grid), dim3(256), lds, s, (const u32x4 *)in,
                        (u32x4 *)out, ntiles, rb / 16, wb / 16, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// XCD-staged record writes (round-4 probe): can records written 4 KB per
+// tile still leave the GPU as 256 KB bursts, without LDS?  Runs of 64
+// consecutive tiles go to one group of blocks (blockIdx % 8: blocks that
+// share an XCD and its L2, observed placement); inside a group the waves
+// take the group's tiles grid-strided.  A tile's 4 KB output goes into the
+// run's slot of a small per-group staging ring (L2-resident), then the
+// wave counts the tile in (agent-scope atomic); the wave completing a run
+// copies the run's 256 KB from staging to the output in one burst and frees
+// the slot for the run NS later.  A wave whose slot is still busy writes
+// its tile directly.  mode bit 0: stage (else: same tile order, direct
+// stores); bit 1: non-temporal staging stores.  Values are garbage (the
+// real kernel needs the XCC check of the rx kernel's protocol), only the
+// time counts.  cnt[] (one word per run) and gen[] (8 * NS words) must be
+// zero at launch.
+__global__ __launch_bounds__(256) void rw_xstage_kernel(const u32x4 *in, u32x4 *out, u32x4 *stg,
+                                                        uint32_t *cnt, uint32_t *gen,
+                                                        uint64_t ntiles, uint32_t rb16,
+                                                        uint32_t wb16, uint32_t ns, int mode,
+                                                        uint32_t *sink) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  const uint32_t x = blockIdx.x & 7u;                    // group (shared XCD, observed)
+  const uint64_t wg = (uint64_t)(gridDim.x / 8) * 4;     // waves per group
+  const uint64_t gw = (uint64_t)(blockIdx.x / 8) * 4 + w;
+  const uint64_t nruns = (ntiles + 63) / 64;
+  u32x4 acc = {0, 0, 0, 0};
+  for (uint64_t s = gw;; s += wg) {
+    const uint64_t k = s / 64, run = k * 8 + x, tile = run * 64 + s % 64;
+    if (run >= nruns || tile >= ntiles) break;
+    const u32x4 *p = in + tile * rb16;
+    uint32_t e = lane;
+    for (; e + 7 * 64 < rb16; e += 8 * 64) {
+      u32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + e + u * 64);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc ^= v[u];
+    }
+    for (; e < rb16; e += 64) acc ^= __builtin_nontemporal_load(p + e);
+    const uint32_t slot = (uint32_t)(k % ns);
+    uint32_t *g = gen + x * ns + slot;
+    // bit 2: no protocol at all (always stage; the wave of the run's last
+    // tile flushes right after its own tile): the data movement alone
+    const bool nosync = mode & 4;
+    const bool stage = (mode & 1) &&
+        (nosync || __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(k / ns));
+    u32x4 *q = stage ? stg + ((uint64_t)(x * ns + slot) * 64 + s % 64) * wb16 : out + tile * wb16;
+    for (uint32_t f = lane; f < wb16; f += 64) {
+      if (!stage || (mode & 2)) __builtin_nontemporal_store(acc, q + f);
+      else q[f] = acc;
+    }
+    if (!(mode & 1)) continue;
+    const uint32_t tir = (uint32_t)min((uint64_t)64, ntiles - run * 64);
+    if (nosync) {
+      // the flusher rotates over the run's tiles (and so over the waves)
+      if (s % 64 != (k * 37 + x * 11) % tir) continue;
+    } else {
+      // bit 3: no drain of the stores before the count (timing only)
+      if (!(mode & 8)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint32_t prev = 0;
+      if (lane == 0) prev = __hip_atomic_fetch_add(cnt + run, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      prev = __builtin_amdgcn_readfirstlane(prev);
+      if (prev + 1 != tir) continue;
+    }
+    // last tile of the run: the staged tiles' bytes as one burst (a direct
+    // tile is rewritten with garbage too: timing only)
+    const u32x4 *src = stg + (uint64_t)(x * ns + slot) * 64 * wb16;
+    u32x4 *dst = out + run * 64 * wb16;
+    const uint32_t tot = tir * wb16;
+    for (uint32_t f = lane; f < tot; f += 8 * 64) {
+      u32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = __builtin_nontemporal_load(src + min(f + u * 64, tot - 1));
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (f + u * 64 < tot) __builtin_nontemporal_store(v[u], dst + f + u * 64);
+    }
+    if (nosync) continue;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_max(g, (uint32_t)(k / ns) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const uint32_t y = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (y == 0x9e3779b9u) sink[lane] = y;
+}
+
+extern "C" int rwxstage_run(const void *in, void *out, void *stg, uint32_t *cnt, uint32_t *gen,
+                            uint64_t ntiles, uint32_t rb, uint32_t wb, uint32_t ns, int mode,
+                            int grid, uint32_t *sink, void *stream) {
+  const hipStream_t s = (hipStream_t)stream;
+  const uint64_t nruns = (ntiles + 63) / 64;
+  if (grid % 8 || ns == 0) return -22;
+  if (hipMemsetAsync(cnt, 0, nruns * 4, s) != hipSuccess || hipMemsetAsync(gen, 0, 8 * ns * 4, s) != hipSuccess)
+    return -5;
+  hipLaunchKernelGGL(rw_xstage_kernel, dim3(grid), dim3(256), 0, s, (const u32x4 *)in, (u32x4 *)out,
+                     (u32x4 *)stg, cnt, gen, ntiles, rb / 16, wb / 16, ns, mode, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Which XCD each block of a grid runs on (HW_REG_XCC_ID), for the
+// blockIdx % 8 grouping the staged probe assumes.
+__global__ void xcc_census_kernel(uint32_t *out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = __builtin_amdgcn_s_getreg(0x1814);
+}
+
+extern "C" int xcc_census(uint32_t *out, int grid, void *stream) {
+  hipLaunchKernelGGL(xcc_census_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, out);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
