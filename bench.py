@@ -444,7 +444,10 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
     return res
 
 
-def gathered_check(prim, gbs, n, dev, k=64):
+GATHER_CHECK_FRAMES = 4096    # per rank: regenerated and run through the CPU oracle
+
+
+def gathered_check(prim, gbs, n, dev, k=GATHER_CHECK_FRAMES):
     """The all-gathered flow hashes: this rank's slice equals the flow_hash
     column of its own records (every frame), and the first k frames of
     every rank's shard, regenerated here from the same synthetic recipe and
@@ -468,8 +471,50 @@ def gathered_check(prim, gbs, n, dev, k=64):
         want = Oracle().rx_batch(host, None, None, stride=b["stride"], fixed_len=b["fixed_len"],
                                  n=cnt, opts=make_opts(KEY))
         bad += int((want["flow_hash"] != got[lo:lo + cnt]).sum())
-    return {"own_slice_equals_records": ok_own, "sampled_frames": k * gb.world,
-            "sampled_mismatches": bad}
+    sampled = sum(min(k, max(0, gb.n_total - r * gb.per)) for r in range(gb.world))
+    return {"own_slice_equals_records": ok_own, "sampled_frames": sampled,
+            "sampled_frames_per_rank": k, "sampled_mismatches": bad}
+
+
+def validate_line(line):
+    """The checks the multi-GPU line must pass before it is printed (the
+    driver's 8-GPU run is not rehearsable here): the communicator spans every
+    rank, the all-gather was measured, its gathered array was checked on at
+    least GATHER_CHECK_FRAMES frames of every rank's shard with no mismatch,
+    and every rank reported its kernel time.  Returns the list of problems
+    (empty: the line is good); a one-GPU line without a gather passes."""
+    bad = []
+    ws = line.get("n_gpus")
+    gat = line.get("allgather")
+    if not isinstance(ws, int) or ws < 1:
+        return ["n_gpus missing"]
+    if ws > 1 and not gat:
+        bad.append("N > 1 without an all-gather")
+    if gat:
+        if line.get("config", {}).get("rccl_ranks") != ws:
+            bad.append(f"config.rccl_ranks {line.get('config', {}).get('rccl_ranks')} != n_gpus {ws}")
+        if gat.get("rccl_ranks") != ws:
+            bad.append(f"allgather.rccl_ranks {gat.get('rccl_ranks')} != n_gpus {ws}")
+        for key in ("ms", "algbw_gbs", "busbw_gbs", "overlap_loss"):
+            if not isinstance(gat.get(key), (int, float)):
+                bad.append(f"allgather.{key} missing")
+        chk = gat.get("gathered_check")
+        if not chk:
+            bad.append("allgather.gathered_check missing")
+        else:
+            if chk.get("sampled_frames_per_rank", 0) < GATHER_CHECK_FRAMES:
+                bad.append("gathered check samples fewer than "
+                           f"{GATHER_CHECK_FRAMES} frames per rank")
+            if chk.get("sampled_mismatches") != 0:
+                bad.append(f"gathered check: {chk.get('sampled_mismatches')} mismatches")
+            if chk.get("own_slice_equals_records") is not True:
+                bad.append("own slice != records")
+        if not isinstance(line.get("value_no_gather"), (int, float)):
+            bad.append("value_no_gather missing")
+    prk = line.get("per_rank_kernel_ms")
+    if not isinstance(prk, list) or len(prk) != ws:
+        bad.append("per_rank_kernel_ms does not list every rank")
+    return bad
 
 
 def mix_sol(b, recs, n):
@@ -828,7 +873,7 @@ def mss_bench(ctx, n, dev, steps, warmup, stride=80):
 
 
 def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
-                 runs=("records", "keys", "keys_denying")):
+                 runs=("records", "keys", "keys_denying"), tune=None):
     """Batched ip_permitted over a C64 batch: buckets of
     the /24 source prefixes in 2^16 buckets, every IPv4 frame a subject, one
     token array carried across the timed batches.  Three runs:
@@ -849,6 +894,8 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
     from tools.synth import make_batch
     b = make_batch("c64", n, dev, first=rank * n)
     ctx = RxContext(dev.index, KEY, 24, 0, hash_size)
+    if tune is not None:          # (A/B: PPTK_RX_TUNE_PERMIT_PASSES = the four-launch path)
+        ctx.set_tuning(-1, tune)
     keys = torch.empty(n, dtype=torch.int32, device=dev)
     recs = ctx.batch_device(b["frames"], n, stride=b["stride"], fixed_len=b["fixed_len"],
                             key_out=keys)
@@ -1073,6 +1120,8 @@ def main():
         del nog["_batch"], nog["_recs"]
         nog["mpkts"] = n_total * args.steps / nog["wall_s"] / 1e6
         gat = gather_bench(ctx, gbs[0], ws, dev, args.steps)
+        if gat["rccl_ranks"] != ws:
+            raise RuntimeError(f"the RCCL communicator has {gat['rccl_ranks']} ranks, not {ws}")
         gat["overlap_loss"] = round(1.0 - prim["mpkts"] / nog["mpkts"], 4)
         gat["buffer_placement"] = prim.get("gather_placement")
         if check:
@@ -1242,7 +1291,12 @@ def main():
             "rewrite": rewrite,
             "mss_clamp": mss,
         }
+        problems = validate_line(line)
+        if problems:
+            line["line_problems"] = problems
         print(json.dumps(line), flush=True)
+        if problems and dist_on(ws):
+            raise SystemExit(f"multi-GPU line failed its checks: {problems}")
     if dist_on(ws):
         import torch.distributed as dist
         # every rank tears its RCCL communicator down at the same point,

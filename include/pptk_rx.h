@@ -285,7 +285,12 @@ int pptk_rx_permit_device(struct pptk_rx_ctx *ctx, const struct pptk_rx_rec *d_r
 /* The same from the dense keys the receive transform wrote into
  * pptk_rx_dev_batch.d_key (4 bytes per frame instead of a 16-byte slice of
  * each record).  Results are those of pptk_rx_permit_device on the
- * records of the same batch; same scratch size. */
+ * records of the same batch; same scratch size.  A key whose bucket (bits
+ * 0..30) is >= opts.iphash_size -- only caller-made keys can be -- is not a
+ * subject (verdict 2, no token touched).  Up to 2^16 buckets and 16 M
+ * frames (65 536 per CU) this runs as one persistent launch that reads the
+ * keys once (DESIGN.md section 5 "Rate limiter"); beyond, or with
+ * PPTK_RX_TUNE_PERMIT_PASSES set, as four launches. */
 int pptk_rx_permit_keys_device(struct pptk_rx_ctx *ctx, const uint32_t *d_keys, uint64_t n,
                                int family, const uint8_t *d_subject, uint32_t *d_tokens,
                                uint8_t *d_verdict, void *d_scratch, void *stream);
@@ -399,7 +404,8 @@ int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const 
  * PPTK_RX_TUNE_NT_STORES (non-temporal record stores),
  * PPTK_RX_TUNE_SC1_STORES (write-through record stores),
  * PPTK_RX_TUNE_BLOCKED (each wavefront takes a contiguous block of tiles
- * instead of every nwaves-th tile).
+ * instead of every nwaves-th tile), PPTK_RX_TUNE_PERMIT_PASSES (the rate
+ * limiter's four-launch path instead of its fused one-launch path).
  * Variants and flags change speed only: results are identical for every
  * setting on every input.  Any other flag bit is rejected with -EINVAL
  * (PPTK_RX_TUNE in the environment is masked to these bits). */
@@ -408,6 +414,7 @@ int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const 
 #define PPTK_RX_TUNE_NT_STORES 0x20
 #define PPTK_RX_TUNE_SC1_STORES 0x40
 #define PPTK_RX_TUNE_BLOCKED 0x100   /* contiguous tiles per wavefront */
+#define PPTK_RX_TUNE_PERMIT_PASSES 0x400   /* rate limiter: four launches, not one */
 int pptk_rx_set_tuning(struct pptk_rx_ctx *ctx, int variant, int flags);
 int pptk_rx_variant_count(void);
 /* The kernel variant the last device batch of this context launched (the

@@ -60,7 +60,9 @@ __global__ __launch_bounds__(BT) void bin_count(const uint16_t *len, uint64_t n,
 
 // exclusive scan of m = NB * nblocks counters (bin-major), one block; then
 // table[k] = start of bin k, table[NB] = total, table[NB + 1] = plan (1 =
-// bin; adaptive: only with >= kBinShortPct % of the frames in group 0)
+// bin; adaptive: only when the batch mixes frames of the last group -- jumbo,
+// > 1521 bytes -- with shorter ones, else the group whose launch runs the
+// whole batch in batch order, rx_internal.h launch_bin)
 __global__ __launch_bounds__(1024) void bin_scan(uint32_t *counts, uint32_t m, uint32_t *table,
                                                  uint32_t adaptive) {
   __shared__ uint32_t part[1024];

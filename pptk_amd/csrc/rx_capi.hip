@@ -335,7 +335,7 @@ static constexpr uint32_t kTuneMask = 0xffffu;
 #else
 static constexpr uint32_t kTuneMask = PPTK_RX_TUNE_NT_LOADS | PPTK_RX_TUNE_NO_STAGING |
                                       PPTK_RX_TUNE_NT_STORES | PPTK_RX_TUNE_SC1_STORES |
-                                      PPTK_RX_TUNE_BLOCKED;
+                                      PPTK_RX_TUNE_BLOCKED | PPTK_RX_TUNE_PERMIT_PASSES;
 #endif
 
 // Memory policy (PPTK_RX_TUNE_*), from in-process A/B runs (DESIGN.md
@@ -891,6 +891,7 @@ static int permit_common(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs
   a.hash_size = hs;
   a.family = family;
   a.ncu = c->ncu;
+  a.force_passes = c->forced_flags >= 0 && (c->forced_flags & PPTK_RX_TUNE_PERMIT_PASSES) ? 1 : 0;
   return hip_err(launch_permit(a, d_scratch, (hipStream_t)stream));
 }
 

@@ -184,6 +184,7 @@ struct PermitArgs {
   uint32_t hash_size;
   int family;                   // 4 or 6
   int ncu;                      // compute units (grid of the persistent verdict pass)
+  int force_passes;             // 1: the four-pass path even where the fused one applies (tests)
 };
 size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size);
 hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t s);

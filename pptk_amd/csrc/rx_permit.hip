@@ -36,7 +36,7 @@
 // because the verdict of a frame only depends on whether its rank passes
 // T_b, and that is decided per BLOCK of frames for all but one block per
 // bucket:
-//   H. histogram: block c of HB = 65535 consecutive frames counts its
+//   H. histogram: block c of HB = 65532 consecutive frames counts its
 //      subject frames per bucket in LDS (u16 pairs, 128 KB for 2^16
 //      buckets) and writes the row bh[c][*]; it also writes each frame's
 //      subject key (bucket, or ~0) densely for the later passes;
@@ -103,7 +103,9 @@ __device__ __forceinline__ uint32_t subject_key(const PermitArgs &a, uint64_t i)
     subj = (flags & PPTK_RX_F_PARSED) && (a.family == 6 ? v6 : !v6);
   }
   if (a.subject) subj = subj && a.subject[i];
-  return subj ? bucket : NOSUBJ;
+  // a bucket outside the token array is not a subject (caller-made keys;
+  // the rx kernel's buckets are < iphash_size by construction)
+  return subj && bucket < a.hash_size ? bucket : NOSUBJ;
 }
 
 // (sort fallback: non-subjects get key hash_size, sorted last)
@@ -135,7 +137,9 @@ __device__ __forceinline__ uint32_t key_at(const PermitArgs &a, const uint32_t *
 }
 
 __device__ __forceinline__ uint32_t filter_key(const PermitArgs &a, uint32_t k) {
-  return k != NOSUBJ && ((k >> 31) == (a.family == 6 ? 1u : 0u)) ? (k & 0x7fffffffu) : NOSUBJ;
+  return k != NOSUBJ && ((k >> 31) == (a.family == 6 ? 1u : 0u)) && (k & 0x7fffffffu) < a.hash_size
+             ? (k & 0x7fffffffu)
+             : NOSUBJ;
 }
 
 // Subject keys of frames i .. i + 3 (i + 4 <= n): one 16-byte load when the
@@ -406,6 +410,459 @@ __global__ __launch_bounds__(HT) void permit_verdicts_tab(PermitArgs a, const ui
   }
 }
 
+// ---- the fused path: one persistent launch, every key read once ----------
+//
+// The four passes above read the keys twice and write + read a 32 MB table
+// of u16 per-block bucket counts: 221 MB of HBM traffic for 84 MB of
+// algorithmic bytes (16 M dense keys in, 16 M verdicts out), 80 us.  Here
+// one workgroup per CU owns a contiguous segment of up to 65 536 frames and
+// keeps its keys in registers (64 per thread) through three phases split by
+// two grid barriers:
+//   1. LDS histogram of the segment's subject keys; the row written to the
+//      table as u8 counts (saturated at 255; exact counts of saturated
+//      buckets, at most 257 per segment, in a per-segment overflow list);
+//   2. per bucket, down its column (the table read once): total, the segment
+//      c* holding the T_b-th frame and that frame's rank need_b inside c*;
+//      code[b] (all / none / c*) and the new token count;
+//   3. the code table staged in LDS; a segment that is some bucket's c*
+//      ranks, round by round in frame order, its frames of such buckets
+//      (ballots, as permit_resolve) -- the keys are its own registers, no
+//      second read -- and every thread writes its 64 verdicts.
+// HBM: keys once (67 MB), the u8 table twice (2 x 16.8 MB), verdicts (17
+// MB): ~118 MB, 1.4 x the algorithmic bytes.  The table and the phase-2
+// outputs are handed between workgroups with write-through (sc1) stores and
+// sc1 loads behind one agent-scope counter per barrier (MI355X_MICROARCH.md
+// "inter-workgroup visibility", the one-workgroup-per-CU row): no L2
+// write-back fences.  Co-residency: the grid is at most one workgroup per
+// CU and each needs > 80 KB of LDS, so no CU holds two; a workgroup not yet
+// resident (a CU busy with another stream's kernel) only delays the others.
+// Every spin is bounded (FUSED_SPIN_TICKS): a barrier that times out marks
+// the status word (PermitFused::status) instead of hanging the GPU.
+constexpr int FT = 1024;                  // threads per workgroup
+constexpr int FKV = 16;                   // 16-byte key loads per thread (64 frames)
+constexpr uint32_t FSEG = FT * 4 * FKV;   // frames per segment at most (65 536)
+constexpr uint32_t FOVF = FSEG / 255 + 1; // saturated buckets per segment at most
+constexpr int FSL = 16;                   // phase 2: row slices per word
+constexpr uint32_t FMAXBLK = 256;         // segments at most (rows of phase 2: 16 x 16)
+constexpr uint64_t FUSED_SPIN_TICKS = 200000000ull;   // 2 s of the 100 MHz clock
+
+struct PermitFused {
+  uint32_t *table;   // nblk rows x nwords u32 (4 u8 counts each)
+  uint32_t *ovf;     // nblk x FOVF (bucket, count) pairs
+  uint32_t *novf;    // nblk
+  uint32_t *need;    // hash_size
+  uint32_t *code;    // ceil(hash_size / 2) words of u16 pairs
+  uint32_t *lim;     // hash_size
+  uint32_t *sync;    // [0], [1] barrier counters, [2] status (zeroed per launch)
+  uint32_t nblk, seg, nwords;
+};
+
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid barrier: every wave's stores complete, then one agent-scope add per
+// workgroup and an sc1 poll of the counter (bounded).
+__device__ __forceinline__ void fused_barrier(uint32_t *ctr, uint32_t nblk, uint32_t *status) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (ld_sc1(ctr) < nblk) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > FUSED_SPIN_TICKS) {
+        st_sc1(status, 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Subject keys of frames i .. i + 3 of the segment [.., hi).
+template <bool KEYS>
+__device__ __forceinline__ void fused_keys4(const PermitArgs &a, uint64_t i, uint64_t hi,
+                                            bool vec, uint32_t k[4]) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  if (KEYS && vec && i + 4 <= hi) {
+    const u32x4 q = *(const u32x4 *)(a.keys_in + i);
+    k[0] = filter_key(a, q.x);
+    k[1] = filter_key(a, q.y);
+    k[2] = filter_key(a, q.z);
+    k[3] = filter_key(a, q.w);
+    if (a.subject) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) k[u] = a.subject[i + u] ? k[u] : NOSUBJ;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = i + u < hi ? subject_key(a, i + u) : NOSUBJ;
+  }
+}
+
+// Exact count of bucket b in segment r whose u8 table entry saturated.
+__device__ __forceinline__ uint32_t fused_ovf(const PermitFused &f, uint32_t r, uint32_t b) {
+  const uint32_t m = ld_sc1(f.novf + r);
+  const uint32_t *e = f.ovf + (uint64_t)r * FOVF * 2;
+  for (uint32_t j = 0; j < m; ++j)
+    if (ld_sc1(e + 2 * j) == b) return ld_sc1(e + 2 * j + 1);
+  return 255u;   // (unreachable: a saturated entry is always listed)
+}
+
+// KEYS: the dense keys (pptk_rx_permit_keys_device), else records.
+template <bool KEYS>
+__global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) {
+  __shared__ uint32_t tab[HMAX / 2];    // phase 1 histogram (u16 pairs); phase 3 code table
+  __shared__ uint32_t rbit[HMAX / 32];  // phase 3: buckets whose c* is this segment
+  __shared__ uint32_t list[FT * 4];     // phase 2 partial sums; phase 3 candidate list
+  __shared__ uint32_t wsum[FT / 64 + 1];
+  const uint32_t c = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const uint64_t lo = (uint64_t)c * f.seg;
+  const uint64_t hi = min(lo + f.seg, a.n);
+  const uint32_t words = hwords(a.hash_size);   // u16-pair words of the histogram / code table
+  const bool vec = ((uintptr_t)a.keys_in & 15u) == 0;
+  // phase timestamps of workgroup 0 (100 MHz clock) in sync[8..15]: read by
+  // tools/permit_run.py --stamps, nothing else
+#define FSTAMP(k)                                                                     \
+  do {                                                                                \
+    if (c == 0 && tid == 0) f.sync[8 + (k)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  FSTAMP(0);
+
+  // ---- phase 1: keys into registers, LDS histogram, the u8 row ------------
+  for (uint32_t w = tid; w < words; w += FT) tab[w] = 0;
+  __syncthreads();
+  // the 64 keys, two 16-bit buckets per register, and which are subjects
+  uint32_t kp[FKV * 2];
+  uint64_t sm = 0;
+#pragma unroll
+  for (int v = 0; v < FKV; ++v) {
+    // four rounds of key loads in flight at a time (all sixteen would hold
+    // 64 registers of loads at once); one of record loads (16 registers)
+    if (v % (KEYS ? 4 : 1) == 0) __builtin_amdgcn_sched_barrier(0);
+    uint32_t kk[4];
+    fused_keys4<KEYS>(a, lo + (uint64_t)v * FT * 4 + 4 * tid, hi, vec, kk);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (kk[u] != NOSUBJ) {
+        atomicAdd(&tab[kk[u] >> 1], 1u << ((kk[u] & 1u) * 16u));
+        sm |= 1ull << (v * 4 + u);
+      }
+    }
+    kp[2 * v] = (kk[0] & 0xffffu) | kk[1] << 16;
+    kp[2 * v + 1] = (kk[2] & 0xffffu) | kk[3] << 16;
+    // opaque: otherwise the compiler keeps the 64 unpacked keys alive for
+    // the later phases instead of these 32 registers
+    asm volatile("" : "+v"(kp[2 * v]), "+v"(kp[2 * v + 1]));
+  }
+#define FKEY(v, u) ((kp[2 * (v) + ((u) >> 1)] >> (((u) & 1) * 16)) & 0xffffu)
+#define FSUBJ(v, u) ((sm >> ((v) * 4 + (u))) & 1ull)
+  const uint32_t nsubj = (uint32_t)__popcll(sm);
+  // A bucket holding all 65 536 frames of a full segment wraps its u16
+  // counter: detected by the segment being all one bucket.
+  bool whole = false;
+  if (f.seg == FSEG && hi - lo == FSEG) {
+    if (tid == 0) wsum[FT / 64] = FSUBJ(0, 0) ? FKEY(0, 0) : NOSUBJ;
+    uint32_t s = nsubj;
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    if (lane == 0) wsum[wv] = s;
+    __syncthreads();
+    uint32_t tot = 0;
+    for (int w = 0; w < FT / 64; ++w) tot += wsum[w];
+    const uint32_t b0 = wsum[FT / 64];
+    bool same = true;
+#pragma unroll
+    for (int v = 0; v < FKV; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) same = same && FKEY(v, u) == b0;
+    whole = __syncthreads_and(same) && tot == FSEG;
+  }
+  __syncthreads();
+  {
+    __shared__ uint32_t novf_l;
+    if (tid == 0) novf_l = 0;
+    __syncthreads();
+    uint32_t *row = f.table + (uint64_t)c * f.nwords;
+    uint32_t *ovf = f.ovf + (uint64_t)c * FOVF * 2;
+    const uint32_t b0 = whole ? FKEY(0, 0) : NOSUBJ;
+    for (uint32_t w = tid; w < f.nwords; w += FT) {
+      const uint32_t h0 = whole ? 0u : tab[2 * w];
+      const uint32_t h1 = whole || 2 * w + 1 >= words ? 0u : tab[2 * w + 1];
+      uint32_t cnt[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
+      if (whole && b0 >> 2 == w) cnt[b0 & 3] = FSEG;
+      uint32_t packed = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (cnt[q] >= 255u) {
+          const uint32_t j = atomicAdd(&novf_l, 1u);
+          st_sc1(ovf + 2 * j, 4 * w + q);
+          st_sc1(ovf + 2 * j + 1, cnt[q]);
+        }
+        packed |= min(cnt[q], 255u) << (8 * q);
+      }
+      st_sc1(row + w, packed);
+    }
+    __syncthreads();
+    if (tid == 0) st_sc1(f.novf + c, novf_l);
+  }
+  FSTAMP(1);
+  fused_barrier(f.sync, f.nblk, f.sync + 2);
+  FSTAMP(2);
+
+  // ---- phase 2: per bucket down its column ---------------------------------
+  // Workgroup c takes a range of table words (4 buckets each); its threads
+  // are 64 word lanes x 16 row slices (up to 16 rows each, all loads in
+  // flight), so a bucket's column is summed by 16 threads at once.
+  {
+    __shared__ uint32_t cst[64 * 4];    // c* found per (word lane, bucket)
+    __shared__ uint32_t tokl[64 * 4];   // the tokens before the batch
+    const uint32_t wpb = (f.nwords + f.nblk - 1) / f.nblk;
+    const uint32_t wlo = min(f.nwords, c * wpb), whi = min(f.nwords, wlo + wpb);
+    const uint32_t rs = (f.nblk + FSL - 1) / FSL;          // rows per slice (<= 16)
+    const uint32_t wl = tid & 63, s = tid >> 6;
+    uint32_t *part = list;                                  // [FSL][64][4]
+    for (uint32_t w0 = wlo; w0 < whi; w0 += 64) {
+      const uint32_t w = w0 + wl;
+      const bool on = w < whi;
+      const uint32_t *col = f.table + (uint64_t)(s * rs) * f.nwords + w;
+      uint32_t p[4] = {0, 0, 0, 0};
+      uint64_t sat = 0;   // saturated entries (bit 4 j + q): exact counts below
+      uint32_t rowv[16];  // (kept for the boundary walk: no second load)
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        rowv[j] = on && (uint32_t)j < rs && s * rs + j < f.nblk
+                      ? ld_sc1(col + (uint64_t)j * f.nwords) : 0u;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t x = rowv[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t y = (x >> (8 * q)) & 0xffu;
+          sat |= (uint64_t)(y == 255u) << (4 * j + q);
+          p[q] += y;
+        }
+      }
+      for (uint64_t m = sat; m; m &= m - 1) {   // (rare: heavy buckets)
+        const int e = __ffsll((unsigned long long)m) - 1;
+        const int q = e & 3;
+        const uint32_t x = fused_ovf(f, s * rs + (e >> 2), 4 * w + q) - 255u;
+        p[0] += q == 0 ? x : 0u;
+        p[1] += q == 1 ? x : 0u;
+        p[2] += q == 2 ? x : 0u;
+        p[3] += q == 3 ? x : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[(s * 64 + wl) * 4 + q] = p[q];
+      if (s == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          cst[wl * 4 + q] = NOBLK;
+          tokl[wl * 4 + q] = on && 4 * w + q < a.hash_size ? a.tokens[4 * w + q] : 0u;
+        }
+      }
+      __syncthreads();
+      // the slice holding the T_b-th frame finds its segment and rank
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t b = 4 * w + q;
+        uint32_t pre = 0, tot = 0;
+        for (uint32_t s2 = 0; s2 < FSL; ++s2) {
+          const uint32_t x = part[(s2 * 64 + wl) * 4 + q];
+          pre += s2 < s ? x : 0u;
+          tot += x;
+        }
+        const uint32_t t = tokl[wl * 4 + q];
+        const uint32_t pq = part[(s * 64 + wl) * 4 + q];
+        if (on && b < a.hash_size && tot > t && t > 0 && pre < t && t <= pre + pq) {
+          uint32_t cum = pre;
+          for (uint32_t j = 0; j < rs; ++j) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) x = (uint32_t)jj == j ? rowv[jj] : x;
+            x = (x >> (8 * q)) & 0xffu;
+            if (x == 255u) x = fused_ovf(f, s * rs + j, b);
+            if (cum + x >= t) {
+              st_sc1(f.need + b, t - cum);
+              cst[wl * 4 + q] = s * rs + j;
+              break;
+            }
+            cum += x;
+          }
+        }
+      }
+      __syncthreads();
+      if (s == 0 && on) {   // code pairs and the new token counts
+        uint32_t cd[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t b = 4 * w + q;
+          uint32_t tot = 0;
+          for (uint32_t s2 = 0; s2 < FSL; ++s2) tot += part[(s2 * 64 + wl) * 4 + q];
+          const uint32_t t = tokl[wl * 4 + q];
+          cd[q] = tot <= t ? CODE_ALL : t == 0 ? CODE_NONE : cst[wl * 4 + q];
+          if (b < a.hash_size) a.tokens[b] = t > tot ? t - tot : 0u;
+        }
+        if (2 * w < words) st_sc1(f.code + 2 * w, cd[0] | cd[1] << 16);
+        if (2 * w + 1 < words) st_sc1(f.code + 2 * w + 1, cd[2] | cd[3] << 16);
+      }
+      __syncthreads();
+    }
+  }
+  FSTAMP(3);
+  fused_barrier(f.sync + 1, f.nblk, f.sync + 2);
+  FSTAMP(4);
+
+  // ---- phase 3: code table in LDS, the boundary ranks, the verdicts --------
+  const uint32_t rbw = (a.hash_size + 31) / 32;
+  for (uint32_t w = tid; w < rbw; w += FT) rbit[w] = 0;
+  __syncthreads();
+  bool mine = false;
+  constexpr int SW = HMAX / 2 / FT;   // code words per thread (at most)
+  uint32_t cw[SW];                    // all loads in flight at once
+#pragma unroll
+  for (int j = 0; j < SW; ++j) {
+    const uint32_t w = tid + j * FT;
+    cw[j] = w < words ? ld_sc1(f.code + w) : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < SW; ++j) {
+    const uint32_t w = tid + j * FT;
+    if (w >= words) break;
+    uint32_t x = cw[j];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t b = 2 * w + h;
+      if (b < a.hash_size && ((x >> (16 * h)) & 0xffffu) == c) {
+        atomicOr(&rbit[b >> 5], 1u << (b & 31));
+        // rank to find, as a u16 (0: nothing left to find); the T_b-th
+        // frame being the segment's 65 536th means every frame of b here
+        const uint32_t nd = ld_sc1(f.need + b);
+        uint32_t rem = nd;
+        if (nd > 0xffffu) {
+          f.lim[b] = (uint32_t)(lo + nd);
+          rem = 0;
+        }
+        x = (x & ~(0xffffu << (16 * h))) | (rem << (16 * h));
+        mine = true;
+      }
+    }
+    tab[w] = x;
+  }
+  mine = __syncthreads_or(mine);
+  FSTAMP(5);
+  // (16-bit accesses: the two buckets of a word are walked by different waves)
+  uint16_t *const tab16 = (uint16_t *)tab;
+  auto tabh = [&](uint32_t b) { return (uint32_t)tab16[b]; };
+  auto isc = [&](uint32_t b) { return (rbit[b >> 5] >> (b & 31)) & 1u; };
+  if (mine) {
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t cm = 0;   // candidate frames of this thread (bit 4 v + u)
+#pragma unroll
+    for (int v = 0; v < FKV; ++v) {
+      __builtin_amdgcn_sched_barrier(0);   // (else all 64 LDS lookups are hoisted)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (FSUBJ(v, u) && isc(FKEY(v, u))) cm |= 1ull << (4 * v + u);
+    }
+#pragma unroll 1
+    for (int v = 0; v < FKV; ++v) {
+      const uint32_t base_off = (uint32_t)v * FT * 4 + 4 * tid;
+      const uint32_t m = (uint32_t)(cm >> (4 * v)) & 15u;
+      // this round's two key registers (a select: the array stays in registers)
+      uint32_t k01 = 0, k23 = 0;
+#pragma unroll
+      for (int vv = 0; vv < FKV; ++vv) {
+        k01 = vv == v ? kp[2 * vv] : k01;
+        k23 = vv == v ? kp[2 * vv + 1] : k23;
+      }
+      // block exclusive scan of the candidate counts (frame order)
+      const uint32_t cnt = (uint32_t)__popc(m);
+      uint32_t inc = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d);
+        if (lane >= d) inc += y;
+      }
+      if (lane == 63) wsum[wv] = inc;
+      __syncthreads();
+      uint32_t basep = 0, total = 0;
+      for (int w = 0; w < FT / 64; ++w) {
+        const uint32_t y = wsum[w];
+        basep += w < wv ? y : 0u;
+        total += y;
+      }
+      basep += inc - cnt;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (m & (1u << u))
+          list[basep++] = (base_off + u) << 16 | (((u < 2 ? k01 : k23) >> ((u & 1) * 16)) & 0xffffu);
+      __syncthreads();
+      // the ordered walk: wave wv takes the buckets with b % 16 == wv
+      for (uint32_t s0 = 0; s0 < total; s0 += 64) {
+        const uint32_t e = s0 + (uint32_t)lane < total ? list[s0 + lane] : NOSUBJ;
+        const uint32_t b = e & 0xffffu;
+        const bool on = e != NOSUBJ && (b & (FT / 64 - 1)) == (uint32_t)wv;
+        uint64_t todo = __ballot(on);
+        while (todo) {
+          const int leader = __ffsll((unsigned long long)todo) - 1;
+          const uint32_t bb = __shfl(b, leader);
+          const uint64_t mm = __ballot(on && b == bb);
+          const uint32_t r0 = tabh(bb);
+          const uint32_t pc = (uint32_t)__popcll(mm);
+          if (r0 != 0) {
+            if (on && b == bb && (uint32_t)__popcll(mm & lt) + 1u == r0)
+              f.lim[bb] = (uint32_t)(lo + (e >> 16)) + 1u;
+            if (lane == leader) tab16[bb] = (uint16_t)(r0 > pc ? r0 - pc : 0u);
+          }
+          todo &= ~mm;
+        }
+      }
+      __syncthreads();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the lim stores, before the reads below
+    __syncthreads();
+  }
+  // (32-bit offsets from the segment start: the 64-bit frame index of
+  // every round would be hoisted into 32 registers)
+  FSTAMP(6);
+  const bool aligned = ((uintptr_t)a.verdict & 3u) == 0;
+  uint8_t *const vbase = a.verdict + lo;
+  const uint32_t nrel = (uint32_t)(hi - lo), lo32 = (uint32_t)lo;
+#pragma unroll
+  for (int v = 0; v < FKV; ++v) {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t rel = (uint32_t)v * FT * 4 + 4 * tid;
+    if (rel >= nrel) break;
+    uint32_t vd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t kk = FKEY(v, u);
+      if (!FSUBJ(v, u)) {
+        vd[u] = 2u;
+      } else if (isc(kk)) {
+        vd[u] = lo32 + rel + u < ld_sc1(f.lim + kk) ? 1u : 0u;
+      } else {
+        const uint32_t cd = tabh(kk);
+        vd[u] = cd == CODE_ALL ? 1u : cd == CODE_NONE ? 0u : c < cd ? 1u : 0u;
+      }
+    }
+    if (aligned && rel + 4 <= nrel) {
+      *(uint32_t *)(vbase + rel) = vd[0] | vd[1] << 8 | vd[2] << 16 | vd[3] << 24;
+    } else {
+      for (uint32_t u = 0; u < 4 && rel + u < nrel; ++u) vbase[rel + u] = (uint8_t)vd[u];
+    }
+  }
+  FSTAMP(7);
+#undef FKEY
+#undef FSUBJ
+#undef FSTAMP
+}
+
 // Run boundaries of the sorted keys: first[b] and end[b] of every bucket
 // present (non-subject keys, == hash_size, sort last and are skipped).  Four
 // keys per thread (one 16-byte load); the neighbours across a thread's
@@ -594,13 +1051,75 @@ hipError_t layout(uint64_t n, uint32_t hash_size, void *base, PermitScratch &s) 
 
 unsigned blocks(uint64_t n) { return (unsigned)((n + PT - 1) / PT); }
 
+// Fused path geometry: nblk segments of seg frames (a multiple of 4096,
+// at most FSEG), at most one workgroup per CU.
+struct FusedGeom {
+  uint32_t nblk, seg;
+};
+
+bool fused_geom(uint64_t n, uint32_t hash_size, int ncu, FusedGeom &g) {
+  if (hash_size > HMAX || ncu < 1 || n == 0) return false;
+  const uint64_t maxblk = std::min<uint64_t>((uint64_t)ncu, FMAXBLK);
+  if (n > maxblk * FSEG) return false;
+  const uint64_t want = std::min<uint64_t>(maxblk, (n + 4095) / 4096);
+  const uint64_t seg = ((n + want - 1) / want + 4095) / 4096 * 4096;
+  g.seg = (uint32_t)seg;
+  g.nblk = (uint32_t)((n + seg - 1) / seg);
+  return true;
+}
+
+void fused_layout(uint32_t nblk, uint32_t seg, uint32_t hash_size, void *base, PermitFused &f,
+                  size_t &total) {
+  uint8_t *p = (uint8_t *)base;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    uint32_t *q = p ? (uint32_t *)(p + off) : nullptr;
+    off += align256(bytes);
+    return q;
+  };
+  f.nblk = nblk;
+  f.seg = seg;
+  f.nwords = (hash_size + 3) / 4;
+  f.sync = take(256);
+  f.table = take((size_t)nblk * f.nwords * 4);
+  f.ovf = take((size_t)nblk * FOVF * 8);
+  f.novf = take((size_t)nblk * 4);
+  f.need = take((size_t)hash_size * 4);
+  f.code = take((size_t)((hash_size + 1) / 2) * 4);
+  f.lim = take((size_t)hash_size * 4);
+  total = off;
+}
+
+// The fused kernel fits one workgroup per CU (its registers and 150 KB of
+// LDS); checked once.
+bool fused_fits() {
+  static const bool ok = [] {
+    int nb = 0;
+    int nr = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, permit_fused<true>, FT, 0) ==
+               hipSuccess &&
+           hipOccupancyMaxActiveBlocksPerMultiprocessor(&nr, permit_fused<false>, FT, 0) ==
+               hipSuccess &&
+           nb >= 1 && nr >= 1;
+  }();
+  return ok;
+}
+
 }  // namespace
 
 size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
+  size_t fused = 0;
+  FusedGeom g;
+  if (fused_geom(n, hash_size, (int)FMAXBLK, g)) {
+    // (every geometry the fused path may pick for n takes at most this:
+    // its table grows with the segment count, at most FMAXBLK)
+    PermitFused f;
+    fused_layout(FMAXBLK, FSEG, hash_size, nullptr, f, fused);
+  }
   if (hash_size <= HMAX && (n + HB - 1) / HB <= MAX_BLOCKS) {
     HistScratch h;
     hist_layout(n, hash_size, nullptr, h);
-    return h.total;
+    return std::max(h.total, fused);
   }
   PermitScratch s;
   if (layout(n, hash_size, nullptr, s) != hipSuccess) return 0;
@@ -609,6 +1128,22 @@ size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size) {
 
 hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   if (a.n == 0) return hipSuccess;
+  FusedGeom g;
+  // (records: the four passes -- their 1 GB read dominates, and the fused
+  // kernel's records loads, one round in flight for its register budget,
+  // measured slower: 0.351 vs 0.238 ms per 16 M records)
+  if (!a.force_passes && a.keys_in && fused_geom(a.n, a.hash_size, a.ncu, g) && fused_fits()) {
+    PermitFused f;
+    size_t total = 0;
+    fused_layout(g.nblk, g.seg, a.hash_size, scratch, f, total);
+    hipError_t e = hipMemsetAsync(f.sync, 0, 64, st);
+    if (e != hipSuccess) return e;
+    if (a.keys_in)
+      hipLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, a, f);
+    else
+      hipLaunchKernelGGL(permit_fused<false>, dim3(g.nblk), dim3(FT), 0, st, a, f);
+    return hipGetLastError();
+  }
   if (a.hash_size <= HMAX && (a.n + HB - 1) / HB <= MAX_BLOCKS) {
     HistScratch h;
     hist_layout(a.n, a.hash_size, scratch, h);

@@ -146,3 +146,60 @@ def test_bench_launches_ranks_itself(tmp_path, monkeypatch):
     monkeypatch.setenv("LOCAL_RANK", "0")
     bench.launch_ranks(["--gpus", "4"], 4)          # under a launcher: no-op
     bench.launch_ranks([], 1)
+
+
+def _dist_line(ws):
+    return {"n_gpus": ws, "value": 1.0, "value_no_gather": 1.1,
+            "config": {"rccl_ranks": ws}, "per_rank_kernel_ms": [4.1] * ws,
+            "allgather": {"ms": 0.2, "algbw_gbs": 600.0, "busbw_gbs": 525.0, "rccl_ranks": ws,
+                          "overlap_loss": 0.05,
+                          "gathered_check": {"own_slice_equals_records": True,
+                                             "sampled_frames": 4096 * ws,
+                                             "sampled_frames_per_rank": 4096,
+                                             "sampled_mismatches": 0}}}
+
+
+def test_bench_validates_multi_gpu_line():
+    """bench.validate_line: the N > 1 fields the driver's 8-GPU line must
+    carry (communicator spans every rank, gathered array checked on >= 4096
+    frames per rank with no mismatch, every rank's kernel time), and what it
+    flags when they are missing or wrong."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    for ws in (1, 2, 8):
+        assert bench.validate_line(_dist_line(ws)) == []
+    assert bench.validate_line({"n_gpus": 1, "per_rank_kernel_ms": [4.0]}) == []
+    bad = _dist_line(8)
+    bad["allgather"]["rccl_ranks"] = 1
+    bad["config"]["rccl_ranks"] = 1
+    assert len(bench.validate_line(bad)) == 2
+    bad = _dist_line(8)
+    bad["allgather"]["gathered_check"]["sampled_frames_per_rank"] = 64
+    bad["allgather"]["gathered_check"]["sampled_mismatches"] = 3
+    assert len(bench.validate_line(bad)) == 2
+    bad = _dist_line(2)
+    del bad["allgather"]
+    assert bench.validate_line(bad) == ["N > 1 without an all-gather"]
+    bad = _dist_line(4)
+    bad["per_rank_kernel_ms"] = [4.0]
+    assert bench.validate_line(bad) == ["per_rank_kernel_ms does not list every rank"]
+
+
+def test_committed_forced_dist_line_passes():
+    """The one-rank RCCL bench line committed under profiles/ (round 4,
+    PPTK_BENCH_FORCE_DIST=1 on one MI355X) carries every N > 1 field and
+    passes bench.validate_line."""
+    import glob
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "dist1", "bench_dist1*.json")))
+    if not files:
+        pytest.skip("no round-4 forced one-rank line committed yet")
+    for f in files:
+        with open(f) as fh:
+            line = json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
+        assert line["allgather"]["rccl_ranks"] == line["n_gpus"] == line["config"]["rccl_ranks"]
+        assert bench.validate_line(line) == [], f

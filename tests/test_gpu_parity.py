@@ -1027,3 +1027,25 @@ def test_ring_alloc_rejects(dev):
             ctx.ring_alloc(**kw)
         assert e.value.errno == 22, kw
     ctx.close()
+
+
+@pytest.mark.parametrize("name,stride", [("c64", 64), ("c1500", 1500)])
+def test_m6_fixed_stride_forced(name, stride, dev):
+    """The mixed-shape kernel (M6) forced on a fixed-stride batch -- its
+    masked-sum instantiation, rx_kernel_mixed<NT, false>, which autotune
+    never picks (it is a candidate for offset-described batches only): the
+    launch really is M6, and the records are exact, full and compact."""
+    from pptk_amd.rx import VARIANTS
+    z = load_golden(name)
+    ctx = _ctx(z)
+    m6 = VARIANTS.index("M6")
+    for flags in (0, 1):
+        ctx.set_tuning(m6, flags)
+        for shift in (0, 3):
+            got = _run(ctx, z, dev, shift=shift, stride=stride)
+            assert ctx.last_variant() == m6
+            d = diff_records(got, z["recs"])
+            assert not d, f"shift {shift} flags {flags}: {d}"
+            got = _run(ctx, z, dev, shift=shift, stride=stride, compact=True)
+            d = diff_records(got, to_rec32(z["recs"]), dtype=REC32_DTYPE)
+            assert not d, f"compact shift {shift} flags {flags}: {d}"

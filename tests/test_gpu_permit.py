@@ -20,10 +20,25 @@ def dev():
     return torch.device("cuda:0")
 
 
+PERMIT_PASSES = 0x400   # PPTK_RX_TUNE_PERMIT_PASSES: the four-launch path
+_PATH = ["fused"]
+
+
+@pytest.fixture(params=["fused", "passes"], autouse=True)
+def permit_path(request):
+    """Every test runs on both rate-limiter paths: the one-launch fused
+    kernel (the default wherever it applies) and the four-launch path."""
+    _PATH[0] = request.param
+    yield request.param
+
+
 def _ctx(z):
     from pptk_amd.rx import RxContext
     b4, b6, hs = (int(x) for x in z["iphash"])
-    return RxContext(0, z["key"].tobytes(), b4, b6, hs)
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs)
+    if _PATH[0] == "passes":
+        ctx.set_tuning(-1, PERMIT_PASSES)
+    return ctx
 
 
 def _gpu_records(ctx, z, dev, compact=False):
@@ -119,8 +134,7 @@ def test_permit_large_skewed_batch(dev):
 
 
 def test_permit_rejects_disabled_family(dev):
-    from pptk_amd.rx import RxContext
-    ctx = RxContext(0, bytes(16), 24, 0, 64)
+    ctx = _ctx({"key": np.zeros(16, np.uint8), "iphash": np.array([24, 0, 64])})
     recs = torch.zeros((4, 64), dtype=torch.uint8, device=dev)
     tok = torch.zeros(64, dtype=torch.int32, device=dev)
     with pytest.raises(OSError):
@@ -234,3 +248,89 @@ def test_permit_regimes_against_oracle(case, dev):
         torch.cuda.synchronize()
         assert np.array_equal(v.cpu().numpy(), vh), via_keys
         assert np.array_equal(tok.cpu().numpy().view(np.uint32), th), via_keys
+
+
+def _np_permit(k, hs, tok):
+    """Frame-by-frame ip_permitted semantics on subject keys k (bucket, or
+    -1: not a subject), vectorised: the rank of each frame among the earlier
+    frames of its bucket (stable sort) against the bucket's tokens."""
+    k = k.astype(np.int64)
+    subj = k >= 0
+    idx = np.nonzero(subj)[0]
+    kb = k[idx]
+    order = np.argsort(kb, kind="stable")
+    sk = kb[order]
+    start = np.searchsorted(sk, sk, side="left")
+    rank = np.empty(len(idx), np.int64)
+    rank[order] = np.arange(len(idx)) - start
+    v = np.full(len(k), 2, np.uint8)
+    v[idx] = (rank < tok[kb].astype(np.int64)).astype(np.uint8)
+    cnt = np.bincount(kb, minlength=hs).astype(np.int64)
+    t2 = (tok.astype(np.int64) - np.minimum(tok.astype(np.int64), cnt)).astype(np.uint32)
+    return v, t2
+
+
+def test_np_permit_matches_oracle():
+    """The vectorised restatement used below equals the C restatement (which
+    is pinned to the reference's own calls, tests/test_oracle.py)."""
+    from oracle.oracle import Oracle
+    from pptk_amd.records import F_PARSED
+    rng = np.random.default_rng(5)
+    n, hs = 200_000, 1 << 12
+    r = np.zeros(n, dtype=REC_DTYPE)
+    r["flags"] = np.where(rng.random(n) < 0.9, F_PARSED, 0)
+    r["src_bucket"] = np.minimum(rng.zipf(1.3, n) - 1, hs - 1)
+    tok = rng.integers(0, 60, hs).astype(np.uint32)
+    vh, th = Oracle().permit_batch(r, 4, None, tok)
+    k = np.where(r["flags"] & F_PARSED, r["src_bucket"].astype(np.int64), -1)
+    v, t = _np_permit(k, hs, tok)
+    assert np.array_equal(v, vh) and np.array_equal(t, th)
+
+
+@pytest.mark.parametrize("case", ["whole_segment", "spread"])
+def test_permit_keys_full_size(case, dev):
+    """16 M dense keys (BASELINE's C64 batch size: one 65 536-frame segment
+    per CU on the fused path).  whole_segment: the first segment is one
+    bucket throughout (its u16 histogram counter wraps: the fused kernel
+    detects it) with the bucket's T_b-th frame inside it, and a second
+    bucket whose budget ends in a late segment; spread: 2^16 buckets, half
+    the frames denied.  GPU == restatement, both paths."""
+    rng = np.random.default_rng(77 if case == "spread" else 78)
+    n, hs = 1 << 24, 1 << 16
+    if case == "whole_segment":
+        k = rng.integers(0, hs, n).astype(np.int64)
+        k[:65536] = 5
+        k[rng.random(n) < 0.3] = 9
+        tok = rng.integers(0, 400, hs).astype(np.uint32)
+        tok[5] = 30000
+        tok[9] = 4_000_000
+    else:
+        k = rng.integers(0, hs, n).astype(np.int64)
+        tok = rng.integers(0, 256, hs).astype(np.uint32)
+    k[rng.random(n) < 0.02] = -1
+    v_want, t_want = _np_permit(k, hs, tok)
+    assert (v_want == 0).sum() > 1000 and (v_want == 1).sum() > 1000
+    ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+    keys = torch.from_numpy(np.where(k >= 0, k, 0xFFFFFFFF).astype(np.uint32).view(np.int32)).to(dev)
+    tokt = torch.from_numpy(tok.view(np.int32).copy()).to(dev)
+    v = ctx.permit_keys_device(keys, 4, tokt)
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), v_want)
+    assert np.array_equal(tokt.cpu().numpy().view(np.uint32), t_want)
+
+
+def test_permit_keys_out_of_range_are_not_subjects(dev):
+    """Caller-made keys whose bucket is >= iphash_size are not subjects:
+    verdict 2, no token touched (they used to index past the tables)."""
+    rng = np.random.default_rng(3)
+    n, hs = 300_001, 1 << 10
+    kr = rng.integers(0, 4 * hs, n).astype(np.int64)
+    tok = rng.integers(0, 100, hs).astype(np.uint32)
+    v_want, t_want = _np_permit(np.where(kr < hs, kr, -1), hs, tok)
+    ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+    keys = torch.from_numpy(kr.astype(np.uint32).view(np.int32)).to(dev)
+    tokt = torch.from_numpy(tok.view(np.int32).copy()).to(dev)
+    v = ctx.permit_keys_device(keys, 4, tokt)
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), v_want)
+    assert np.array_equal(tokt.cpu().numpy().view(np.uint32), t_want)

@@ -154,3 +154,17 @@ def test_tx_two_streams_one_context(dev):
         torch.cuda.synchronize()
         assert np.array_equal(fa.cpu().numpy(), wa)
         assert np.array_equal(fb.cpu().numpy(), wb)
+
+
+def test_tx_m6_fixed_stride_forced(dev):
+    """Tx with the mixed-shape kernel forced on a fixed-stride batch (its
+    masked-sum instantiation): the launch is M6 and the frames are exact."""
+    from pptk_amd.rx import VARIANTS
+    z, buf_in, buf_out = _case("c64")
+    ctx = _ctx()
+    m6 = VARIANTS.index("M6")
+    ctx.set_tuning(m6, 0)
+    for shift in (0, 5):
+        big, frames = _tx(ctx, z, buf_in, dev, shift, stride=64)
+        assert ctx.last_variant() == m6
+        assert np.array_equal(frames[:buf_in.size].cpu().numpy(), buf_out), shift
