@@ -18,6 +18,10 @@
  *   gcc -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude examples/rx_perf.c \
  *       -Lpptk_amd -lpptkrx -L/opt/rocm/lib -lamdhip64 -o rx_perf
  *   ./rx_perf [frames [bytes [reps [device]]]]     (16777216 1500 20 0)
+ *
+ * The device rings come from the library (pptk_rx_ring_alloc: placed by a
+ * probe at allocation, the product default);
+ * RX_PERF_RING=0 uses plain hipMalloc buffers instead.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -125,14 +129,38 @@ int main(int argc, char **argv)
             2 * POOL);
     return 2;
   }
+  const char *ring_env = getenv("RX_PERF_RING");
+  const int use_ring = !(ring_env && ring_env[0] == '0');
+  struct pptk_rx_ring ring;
+  memset(&ring, 0, sizeof(ring));
   pool = malloc((size_t)POOL * bytes);
   recs = malloc(2 * (size_t)POOL * sizeof(*recs));
   ms = malloc(sizeof(float) * (size_t)reps);
   if (!pool || !recs || !ms) return 1;
   for (i = 0; i < POOL; i++) make_frame(pool + i * bytes, bytes);
-  if (hipSetDevice(device) != hipSuccess ||
-      hipMalloc((void **)&d_frames, n * bytes + 64) != hipSuccess ||
-      hipMalloc((void **)&d_recs, n * sizeof(*d_recs)) != hipSuccess) {
+  pptk_rx_opts_default(&o);
+  o.device = device;
+  memcpy(o.key, key, 16);
+  if (hipSetDevice(device) != hipSuccess || (rc = pptk_rx_ctx_create(&ctx, &o)) != 0) {
+    fprintf(stderr, "pptk_rx_ctx_create: %d\n", rc);
+    return 1;
+  }
+  if (use_ring) {   /* the library's placed rings (the product default) */
+    struct pptk_rx_ring_spec spec;
+    memset(&spec, 0, sizeof(spec));
+    spec.frame_bytes = n * bytes;
+    spec.nrec = n;
+    spec.rec_bytes = sizeof(struct pptk_rx_rec);
+    spec.probe_len = bytes < 64 ? 64 : bytes > 1536 ? 1536 : bytes;
+    spec.flags = PPTK_RX_RING_SETTLE;
+    if ((rc = pptk_rx_ring_alloc(ctx, &spec, &ring, NULL)) != 0) {
+      fprintf(stderr, "pptk_rx_ring_alloc: %d\n", rc);
+      return 1;
+    }
+    d_frames = ring.d_frames;
+    d_recs = (struct pptk_rx_rec *)ring.d_recs;
+  } else if (hipMalloc((void **)&d_frames, n * bytes + 64) != hipSuccess ||
+             hipMalloc((void **)&d_recs, n * sizeof(*d_recs)) != hipSuccess) {
     fprintf(stderr, "device %d: allocation of %.1f GB failed\n", device, n * (bytes + 64.0) / 1e9);
     return 1;
   }
@@ -144,13 +172,6 @@ int main(int argc, char **argv)
     if (hipMemcpy(d_frames + have * bytes, d_frames, m * bytes, hipMemcpyDeviceToDevice) !=
         hipSuccess)
       return 1;
-  }
-  pptk_rx_opts_default(&o);
-  o.device = device;
-  memcpy(o.key, key, 16);
-  if ((rc = pptk_rx_ctx_create(&ctx, &o)) != 0) {
-    fprintf(stderr, "pptk_rx_ctx_create: %d\n", rc);
-    return 1;
   }
   memset(&b, 0, sizeof(b));
   b.d_frames = d_frames;
@@ -192,10 +213,21 @@ int main(int argc, char **argv)
            (unsigned long long)n, bytes, bytes < 54 ? "IPv4/UDP" : "IPv4/TCP",
            pptk_rx_last_variant(ctx), med, ms[0], n / (med * 1e-3) / 1e6, gbs, gbs / 8000.0,
            2 * POOL, (unsigned long long)bad);
+    if (use_ring)
+      printf("rx_perf: rings from pptk_rx_ring_alloc: %u x %u candidate pairs probed, plain "
+             "allocation %.4f ms, kept pair %.4f ms, %.1f GB freed, %u ms settled\n",
+             ring.frame_cands, ring.rec_cands, ring.first_ms, ring.chosen_ms,
+             ring.freed_bytes / 1e9, ring.settle_ms);
+    else
+      printf("rx_perf: plain hipMalloc buffers (RX_PERF_RING=0)\n");
   }
   pptk_rx_ctx_destroy(ctx);
-  (void)hipFree(d_frames);
-  (void)hipFree(d_recs);
+  if (use_ring) {
+    pptk_rx_ring_free(&ring);
+  } else {
+    (void)hipFree(d_frames);
+    (void)hipFree(d_recs);
+  }
   free(pool);
   free(recs);
   free(ms);

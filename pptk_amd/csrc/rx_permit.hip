@@ -540,6 +540,50 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   // the 64 keys, two 16-bit buckets per register, and which are subjects
   uint32_t kp[FKV * 2];
   uint64_t sm = 0;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  // Whole, aligned segment of dense keys: straight-line 16-byte loads, eight
+  // rounds in flight (a load under a per-round branch was waited for before
+  // the next one issued: 16 serial round trips, 19 us); rounds past the
+  // segment re-read round 0 and are dropped; no subject array reads the keys
+  // again and ORs in "subject".
+  const bool fast = KEYS && vec && hi == lo + f.seg &&
+                    (!a.subject || ((uintptr_t)a.subject & 3u) == 0);
+  if (fast) {
+    const uint32_t nv = f.seg / (FT * 4);
+    const uint8_t *sp = a.subject ? a.subject : (const uint8_t *)a.keys_in;
+    const uint32_t sor = a.subject ? 0u : 0x01010101u;
+#pragma unroll
+    for (int h = 0; h < FKV / 8; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
+      u32x4 q[8];
+      uint32_t sb[8];
+#pragma unroll
+      for (int v8 = 0; v8 < 8; ++v8) {
+        const int v = h * 8 + v8;
+        const uint64_t i = lo + (uint64_t)((uint32_t)v < nv ? v : 0) * FT * 4 + 4 * tid;
+        q[v8] = *(const u32x4 *)(a.keys_in + i);
+        sb[v8] = *(const uint32_t *)(sp + i);
+      }
+#pragma unroll
+      for (int v8 = 0; v8 < 8; ++v8) {
+        const int v = h * 8 + v8;
+        const bool live = (uint32_t)v < nv;
+        const uint32_t sw = sb[v8] | sor;
+        uint32_t kk[4] = {q[v8].x, q[v8].y, q[v8].z, q[v8].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          kk[u] = live && ((sw >> (8 * u)) & 0xffu) ? filter_key(a, kk[u]) : NOSUBJ;
+          if (kk[u] != NOSUBJ) {
+            atomicAdd(&tab[kk[u] >> 1], 1u << ((kk[u] & 1u) * 16u));
+            sm |= 1ull << (v * 4 + u);
+          }
+        }
+        kp[2 * v] = (kk[0] & 0xffffu) | kk[1] << 16;
+        kp[2 * v + 1] = (kk[2] & 0xffffu) | kk[3] << 16;
+        asm volatile("" : "+v"(kp[2 * v]), "+v"(kp[2 * v + 1]));
+      }
+    }
+  } else {
 #pragma unroll
   for (int v = 0; v < FKV; ++v) {
     // four rounds of key loads in flight at a time (all sixteen would hold
@@ -559,6 +603,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     // opaque: otherwise the compiler keeps the 64 unpacked keys alive for
     // the later phases instead of these 32 registers
     asm volatile("" : "+v"(kp[2 * v]), "+v"(kp[2 * v + 1]));
+  }
   }
 #define FKEY(v, u) ((kp[2 * (v) + ((u) >> 1)] >> (((u) & 1) * 16)) & 0xffffu)
 #define FSUBJ(v, u) ((sm >> ((v) * 4 + (u))) & 1ull)
@@ -630,6 +675,14 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       const uint32_t w = w0 + wl;
       const bool on = w < whi;
       const uint32_t *col = f.table + (uint64_t)(s * rs) * f.nwords + w;
+      // (slice 0 reads the tokens now, beside the table loads: one round
+      // trip instead of two)
+      uint32_t tk[4] = {0u, 0u, 0u, 0u};
+      if (s == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          tk[q] = on && 4 * w + q < a.hash_size ? a.tokens[4 * w + q] : 0u;
+      }
       uint32_t p[4] = {0, 0, 0, 0};
       uint64_t sat = 0;   // saturated entries (bit 4 j + q): exact counts below
       uint32_t rowv[16];  // (kept for the boundary walk: no second load)
@@ -662,7 +715,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           cst[wl * 4 + q] = NOBLK;
-          tokl[wl * 4 + q] = on && 4 * w + q < a.hash_size ? a.tokens[4 * w + q] : 0u;
+          tokl[wl * 4 + q] = tk[q];
         }
       }
       __syncthreads();
@@ -844,7 +897,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       const uint32_t kk = FKEY(v, u);
       if (!FSUBJ(v, u)) {
         vd[u] = 2u;
-      } else if (isc(kk)) {
+      } else if (mine && isc(kk)) {   // (no candidate bucket here: no lookup)
         vd[u] = lo32 + rel + u < ld_sc1(f.lim + kk) ? 1u : 0u;
       } else {
         const uint32_t cd = tabh(kk);
@@ -1095,12 +1148,9 @@ void fused_layout(uint32_t nblk, uint32_t seg, uint32_t hash_size, void *base, P
 bool fused_fits() {
   static const bool ok = [] {
     int nb = 0;
-    int nr = 0;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, permit_fused<true>, FT, 0) ==
                hipSuccess &&
-           hipOccupancyMaxActiveBlocksPerMultiprocessor(&nr, permit_fused<false>, FT, 0) ==
-               hipSuccess &&
-           nb >= 1 && nr >= 1;
+           nb >= 1;
   }();
   return ok;
 }
@@ -1138,10 +1188,7 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
     fused_layout(g.nblk, g.seg, a.hash_size, scratch, f, total);
     hipError_t e = hipMemsetAsync(f.sync, 0, 64, st);
     if (e != hipSuccess) return e;
-    if (a.keys_in)
-      hipLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, a, f);
-    else
-      hipLaunchKernelGGL(permit_fused<false>, dim3(g.nblk), dim3(FT), 0, st, a, f);
+    hipLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, a, f);
     return hipGetLastError();
   }
   if (a.hash_size <= HMAX && (a.n + HB - 1) / HB <= MAX_BLOCKS) {

@@ -21,4 +21,11 @@ for run in keys keys_denying; do
 done
 timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_comm.py tests/test_examples.py -m gpu > gpurun_out/r04c/comm_tests.log 2>&1
 rc=$?; echo "comm tests rc=$rc"; grep -E "passed|failed|Error|FAIL" gpurun_out/r04c/comm_tests.log | tail -8
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/ab.py cmix 3:0 14:0 3:0 14:0 13:0 > gpurun_out/r04c/ab_cmix.json 2> gpurun_out/r04c/ab_cmix.log
+rc=$?; echo "ab cmix rc=$rc"; cat gpurun_out/r04c/ab_cmix.json | cut -c1-700
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/ab.py c1500 4:1 14:1 3:1 > gpurun_out/r04c/ab_c1500.json 2> gpurun_out/r04c/ab_c1500.log
+rc=$?; echo "ab c1500 rc=$rc"; cat gpurun_out/r04c/ab_c1500.json | cut -c1-700
+[ $rc -eq 0 ] || exit $rc
+bash scripts/gpu_r04_sq.sh

@@ -6,7 +6,7 @@ mkdir -p gpurun_out/sq
 export TMPDIR=/tmp
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
 P2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT"
-for spec in cmix:3 cmix:13 c1500:4; do
+for spec in cmix:3 cmix:13 cmix:14 c1500:4; do
   cfg=${spec%%:*}; var=${spec##*:}
   for pass in 1 2; do
     if [ $pass = 1 ]; then C=$P1; else C=$P2; fi

@@ -145,14 +145,16 @@ def test_rx_multigpu_failed_thread_exits_nonzero(tmp_path, join, ranks):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nbytes", [1500, 64])
-def test_rx_perf_device_resident_from_c(tmp_path, nbytes):
+@pytest.mark.parametrize("nbytes,ring", [(1500, "1"), (64, "1"), (1500, "0")])
+def test_rx_perf_device_resident_from_c(tmp_path, nbytes, ring):
     """examples/rx_perf.c: the device-resident throughput timed from a plain
     C host (the GPU counterpart of iphdr/ipcksumperf.c), its records checked
-    against the kept per-packet C APIs (checksums, getters, siphash_buf)."""
+    against the kept per-packet C APIs (checksums, getters, siphash_buf); the
+    device rings from pptk_rx_ring_alloc (default) or plain hipMalloc."""
     exe = build(tmp_path, "rx_perf", hip=True)
     out = subprocess.run([exe, str(1 << 20), str(nbytes), "5"], capture_output=True, text=True,
-                         timeout=300)
+                         timeout=300, env=dict(os.environ, RX_PERF_RING=ring))
     assert out.returncode == 0, out.stdout + out.stderr
     assert "8192 records checked against the host APIs, 0 mismatches" in out.stdout, out.stdout
+    assert ("rings from pptk_rx_ring_alloc" in out.stdout) == (ring == "1"), out.stdout
     print(out.stdout)

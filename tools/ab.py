@@ -11,7 +11,8 @@ lib names come from AB_LIBS (name=path,...), default = pptk_amd/libpptkrx.so.
 Generates the batch once, then times every setting in interleaved rounds
 (A B C A B C ...) so that clock and thermal drift hit all settings alike;
 prints one JSON line with the median kernel ms and GB/s per setting.
-AB_PLACE=1 times on placed frame and record buffers (bench.placed_buffers).
+AB_PLACE=1 times on placed frame and record buffers (bench.placed_buffers);
+AB_SOL=1 adds the speed of light of the launch's traffic (bench.mix_sol).
 AB_BIN=1 processes mixed batches in length-binned order (pptk_rx_bin_device,
 timed inside each launch's window); AB_MIXED=1 through
 pptk_rx_batch_device_mixed (binning + one launch per length group)."""
@@ -110,6 +111,13 @@ def main():
                 times[s].append(e0.elapsed_time(e1))
     out = {"cfg": cfg, "frames": n, "binned": binned, "mixed": mixed,
            "box": measure(b["frames"]), "placement": placement}
+    if os.environ.get("AB_SOL"):
+        # the speed of light of this launch's traffic on these buffers
+        # (tools/rwmix.py sol_ms, as bench.mix_sol)
+        import bench
+        sol = bench.mix_sol(b, recs64, n)
+        if sol:
+            out["sol_ms"], out["sol_desc"] = round(sol[0], 4), sol[1]
     for s, t in times.items():
         ms = float(np.median(t))
         key = ":".join(str(x) for x in s[:3] if x != "") + (":c" if s[3] else "") + \
