@@ -655,6 +655,25 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     __syncthreads();
     if (tid == 0) st_sc1(f.novf + c, novf_l);
   }
+  // Speculative verdicts: as if no bucket ran out of tokens (the common
+  // case: every subject permitted).  Phase 2 raises sync[3] if some bucket
+  // does; only then does phase 3 write the verdicts again from the codes.
+  const bool valigned = ((uintptr_t)a.verdict & 3u) == 0;
+  uint8_t *const vbase = a.verdict + lo;
+  const uint32_t nrel = (uint32_t)(hi - lo), lo32 = (uint32_t)lo;
+#pragma unroll
+  for (int v = 0; v < FKV; ++v) {
+    const uint32_t rel = (uint32_t)v * FT * 4 + 4 * tid;
+    if (rel >= nrel) break;
+    const uint32_t sv = (uint32_t)(sm >> (4 * v)) & 15u;   // subject bits -> 1, else 2
+    const uint32_t word = (sv & 1u ? 1u : 2u) | (sv & 2u ? 1u : 2u) << 8 |
+                          (sv & 4u ? 1u : 2u) << 16 | (sv & 8u ? 1u : 2u) << 24;
+    if (valigned && rel + 4 <= nrel) {
+      *(uint32_t *)(vbase + rel) = word;
+    } else {
+      for (uint32_t u = 0; u < 4 && rel + u < nrel; ++u) vbase[rel + u] = (uint8_t)(word >> (8 * u));
+    }
+  }
   FSTAMP(1);
   fused_barrier(f.sync, f.nblk, f.sync + 2);
   FSTAMP(2);
@@ -762,6 +781,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         }
         if (2 * w < words) st_sc1(f.code + 2 * w, cd[0] | cd[1] << 16);
         if (2 * w + 1 < words) st_sc1(f.code + 2 * w + 1, cd[2] | cd[3] << 16);
+        if ((cd[0] & cd[1] & cd[2] & cd[3]) != CODE_ALL) st_sc1(f.sync + 3, 1u);
       }
       __syncthreads();
     }
@@ -769,6 +789,16 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   FSTAMP(3);
   fused_barrier(f.sync + 1, f.nblk, f.sync + 2);
   FSTAMP(4);
+  // no bucket ran out: the speculative verdicts stand
+  {
+    __shared__ uint32_t any_out;
+    if (tid == 0) any_out = ld_sc1(f.sync + 3);
+    __syncthreads();
+    if (any_out == 0) {
+      FSTAMP(7);
+      return;
+    }
+  }
 
   // ---- phase 3: code table in LDS, the boundary ranks, the verdicts --------
   const uint32_t rbw = (a.hash_size + 31) / 32;
@@ -883,9 +913,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   // (32-bit offsets from the segment start: the 64-bit frame index of
   // every round would be hoisted into 32 registers)
   FSTAMP(6);
-  const bool aligned = ((uintptr_t)a.verdict & 3u) == 0;
-  uint8_t *const vbase = a.verdict + lo;
-  const uint32_t nrel = (uint32_t)(hi - lo), lo32 = (uint32_t)lo;
+  const bool aligned = valigned;
 #pragma unroll
   for (int v = 0; v < FKV; ++v) {
     __builtin_amdgcn_sched_barrier(0);

@@ -20,3 +20,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pmc cmix $c rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
+timeout -s KILL 60 rocprofv3 --list-avail > gpurun_out/r04d/list_avail.txt 2>&1
+echo "list-avail rc=$?"

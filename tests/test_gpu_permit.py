@@ -297,17 +297,16 @@ def test_permit_keys_full_size(case, dev):
     the frames denied.  GPU == restatement, both paths."""
     rng = np.random.default_rng(77 if case == "spread" else 78)
     n, hs = 1 << 24, 1 << 16
+    k = rng.integers(0, hs, n).astype(np.int64)
+    k[rng.random(n) < 0.02] = -1
     if case == "whole_segment":
-        k = rng.integers(0, hs, n).astype(np.int64)
-        k[:65536] = 5
         k[rng.random(n) < 0.3] = 9
+        k[:65536] = 5                    # last: the first segment is bucket 5 throughout
         tok = rng.integers(0, 400, hs).astype(np.uint32)
         tok[5] = 30000
         tok[9] = 4_000_000
     else:
-        k = rng.integers(0, hs, n).astype(np.int64)
         tok = rng.integers(0, 256, hs).astype(np.uint32)
-    k[rng.random(n) < 0.02] = -1
     v_want, t_want = _np_permit(k, hs, tok)
     assert (v_want == 0).sum() > 1000 and (v_want == 1).sum() > 1000
     ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
