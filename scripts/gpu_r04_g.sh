@@ -23,3 +23,6 @@ for run in keys keys_denying; do
     [ $rc -eq 0 ] || exit $rc
   done
 done
+PPTK_BENCH_FORCE_DIST=1 timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r04g/bench_dist1.json 2> gpurun_out/r04g/bench_dist1.log
+rc=$?; echo "dist1 rc=$rc"; tail -c 1500 gpurun_out/r04g/bench_dist1.json
+[ $rc -eq 0 ] || exit $rc
