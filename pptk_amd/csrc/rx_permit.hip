@@ -52,8 +52,11 @@
 // 16 M frames, 2^16 buckets: the histogram table is 32 MB, the passes read
 // the keys twice -- no 64 MB x (2 passes x 3 arrays) radix sort.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <random>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -440,6 +443,10 @@ __global__ __launch_bounds__(HT) void permit_verdicts_tab(PermitArgs a, const ui
 // the status word (PermitFused::status) instead of hanging the GPU.
 constexpr int FT = 1024;                  // threads per workgroup
 constexpr int FKV = 16;                   // 16-byte key loads per thread (64 frames)
+#ifndef PPTK_PERMIT_FKB
+#define PPTK_PERMIT_FKB 16
+#endif
+constexpr int FKB = PPTK_PERMIT_FKB;      // of them in flight at once (whole segments)
 constexpr uint32_t FSEG = FT * 4 * FKV;   // frames per segment at most (65 536)
 constexpr uint32_t FOVF = FSEG / 255 + 1; // saturated buckets per segment at most
 constexpr int FSL = 16;                   // phase 2: row slices per word
@@ -452,10 +459,13 @@ struct PermitFused {
   uint32_t *novf;    // nblk
   uint32_t *need;    // hash_size
   uint32_t *code;    // ceil(hash_size / 2) words of u16 pairs
-  uint32_t *lim;     // hash_size
-  uint32_t *sync;    // [0], [1] barrier counters, [2] status (zeroed per launch)
+  uint64_t *arrive;  // FMAXBLK: workgroup c's barrier generation (nonce + k)
+  uint64_t *out;     // [0] = nonce: some bucket ran out of tokens; [1] status
+  uint32_t *stamps;  // FSTAMPS x FMAXBLK phase timestamps (tools/permit_run.py)
+  uint64_t nonce;    // this launch's, low two bits clear (never 0 or ~0)
   uint32_t nblk, seg, nwords;
 };
+constexpr int FSTAMPS = 7;
 
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -464,18 +474,34 @@ __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Grid barrier: every wave's stores complete, then one agent-scope add per
-// workgroup and an sc1 poll of the counter (bounded).
-__device__ __forceinline__ void fused_barrier(uint32_t *ctr, uint32_t nblk, uint32_t *status) {
+__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid barrier k (1, 2) of the launch with nonce N: every wave's stores
+// complete, workgroup c publishes N + k in arrive[c], and wave 0 polls all
+// nblk words (sc1, bounded) until each holds N + k or later.  Nothing needs
+// zeroing between launches: a word left by another launch (or garbage) never
+// matches this launch's nonce, so there is no memset before each launch.
+__device__ __forceinline__ void fused_barrier(const PermitFused &f, uint32_t c, uint64_t k) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 64) {
+    if (threadIdx.x == 0) st_sc1(f.arrive + c, f.nonce + k);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (ld_sc1(ctr) < nblk) {
-      __builtin_amdgcn_s_sleep(2);
+    for (;;) {
+      bool ok = true;
+      for (uint32_t i = threadIdx.x; i < f.nblk; i += 64) {
+        const uint64_t x = ld_sc1(f.arrive + i);
+        ok = ok && (x & ~3ull) == f.nonce && (x & 3ull) >= k;
+      }
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > FUSED_SPIN_TICKS) {
-        st_sc1(status, 1u);
+        if (threadIdx.x == 0) st_sc1(f.out + 1, f.nonce | 1u);
         break;
       }
     }
@@ -518,25 +544,30 @@ template <bool KEYS>
 __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) {
   __shared__ uint32_t tab[HMAX / 2];    // phase 1 histogram (u16 pairs); phase 3 code table
   __shared__ uint32_t rbit[HMAX / 32];  // phase 3: buckets whose c* is this segment
-  __shared__ uint32_t list[FT * 4];     // phase 2 partial sums; phase 3 candidate list
+  __shared__ __attribute__((aligned(16))) uint32_t list[FT * 4];   // phase 2 partial sums; phase 3 candidate list
   __shared__ uint32_t wsum[FT / 64 + 1];
+  // phase 2: c* found and tokens per (word lane, bucket); phase 3: per-wave
+  // totals of the candidate partition
+  __shared__ __attribute__((aligned(16))) uint32_t p23[512];
   const uint32_t c = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const uint64_t lo = (uint64_t)c * f.seg;
   const uint64_t hi = min(lo + f.seg, a.n);
   const uint32_t words = hwords(a.hash_size);   // u16-pair words of the histogram / code table
   const bool vec = ((uintptr_t)a.keys_in & 15u) == 0;
-  // phase timestamps of workgroup 0 (100 MHz clock) in sync[8..15]: read by
+  // phase timestamps of every workgroup (100 MHz clock): read by
   // tools/permit_run.py --stamps, nothing else
-#define FSTAMP(k)                                                                     \
-  do {                                                                                \
-    if (c == 0 && tid == 0) f.sync[8 + (k)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+#define FSTAMP(k)                                                                          \
+  do {                                                                                     \
+    if (tid == 0) f.stamps[(k) * FMAXBLK + c] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
   FSTAMP(0);
 
   // ---- phase 1: keys into registers, LDS histogram, the u8 row ------------
-  for (uint32_t w = tid; w < words; w += FT) tab[w] = 0;
-  __syncthreads();
+  auto clear_tab = [&]() {
+    for (uint32_t w = tid; w < words; w += FT) tab[w] = 0;
+    __syncthreads();
+  };
   // the 64 keys, two 16-bit buckets per register, and which are subjects
   uint32_t kp[FKV * 2];
   uint64_t sm = 0;
@@ -550,25 +581,25 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
                     (!a.subject || ((uintptr_t)a.subject & 3u) == 0);
   if (fast) {
     const uint32_t nv = f.seg / (FT * 4);
-    const uint8_t *sp = a.subject ? a.subject : (const uint8_t *)a.keys_in;
-    const uint32_t sor = a.subject ? 0u : 0x01010101u;
+    const bool subj = a.subject != nullptr;
 #pragma unroll
-    for (int h = 0; h < FKV / 8; ++h) {
+    for (int h = 0; h < FKV / FKB; ++h) {
       __builtin_amdgcn_sched_barrier(0);
-      u32x4 q[8];
-      uint32_t sb[8];
+      u32x4 q[FKB];
+      uint32_t sb[FKB];
 #pragma unroll
-      for (int v8 = 0; v8 < 8; ++v8) {
-        const int v = h * 8 + v8;
+      for (int v8 = 0; v8 < FKB; ++v8) {
+        const int v = h * FKB + v8;
         const uint64_t i = lo + (uint64_t)((uint32_t)v < nv ? v : 0) * FT * 4 + 4 * tid;
         q[v8] = *(const u32x4 *)(a.keys_in + i);
-        sb[v8] = *(const uint32_t *)(sp + i);
+        sb[v8] = subj ? *(const uint32_t *)(a.subject + i) : 0x01010101u;
       }
+      if (h == 0) clear_tab();   // (behind the first loads)
 #pragma unroll
-      for (int v8 = 0; v8 < 8; ++v8) {
-        const int v = h * 8 + v8;
+      for (int v8 = 0; v8 < FKB; ++v8) {
+        const int v = h * FKB + v8;
         const bool live = (uint32_t)v < nv;
-        const uint32_t sw = sb[v8] | sor;
+        const uint32_t sw = sb[v8];
         uint32_t kk[4] = {q[v8].x, q[v8].y, q[v8].z, q[v8].w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -584,6 +615,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       }
     }
   } else {
+  clear_tab();
 #pragma unroll
   for (int v = 0; v < FKV; ++v) {
     // four rounds of key loads in flight at a time (all sixteen would hold
@@ -605,6 +637,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     asm volatile("" : "+v"(kp[2 * v]), "+v"(kp[2 * v + 1]));
   }
   }
+  FSTAMP(1);
 #define FKEY(v, u) ((kp[2 * (v) + ((u) >> 1)] >> (((u) & 1) * 16)) & 0xffffu)
 #define FSUBJ(v, u) ((sm >> ((v) * 4 + (u))) & 1ull)
   const uint32_t nsubj = (uint32_t)__popcll(sm);
@@ -656,35 +689,44 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     if (tid == 0) st_sc1(f.novf + c, novf_l);
   }
   // Speculative verdicts: as if no bucket ran out of tokens (the common
-  // case: every subject permitted).  Phase 2 raises sync[3] if some bucket
-  // does; only then does phase 3 write the verdicts again from the codes.
+  // case: every subject permitted), written as phase 2 starts (they drain
+  // beside its table loads; phase 1 ends without waiting for them).  Phase 2 flags out[0] if some bucket does run out;
+  // only then does phase 3 write the verdicts that differ.
   const bool valigned = ((uintptr_t)a.verdict & 3u) == 0;
   uint8_t *const vbase = a.verdict + lo;
-  const uint32_t nrel = (uint32_t)(hi - lo), lo32 = (uint32_t)lo;
-#pragma unroll
-  for (int v = 0; v < FKV; ++v) {
-    const uint32_t rel = (uint32_t)v * FT * 4 + 4 * tid;
-    if (rel >= nrel) break;
-    const uint32_t sv = (uint32_t)(sm >> (4 * v)) & 15u;   // subject bits -> 1, else 2
-    const uint32_t word = (sv & 1u ? 1u : 2u) | (sv & 2u ? 1u : 2u) << 8 |
-                          (sv & 4u ? 1u : 2u) << 16 | (sv & 8u ? 1u : 2u) << 24;
+  const uint32_t nrel = (uint32_t)(hi - lo);
+  auto spec_word = [&](int v) {   // subject bits -> 1, else 2
+    const uint32_t sv = (uint32_t)(sm >> (4 * v)) & 15u;
+    return (sv & 1u ? 1u : 2u) | (sv & 2u ? 1u : 2u) << 8 | (sv & 4u ? 1u : 2u) << 16 |
+           (sv & 8u ? 1u : 2u) << 24;
+  };
+  auto put_word = [&](uint32_t rel, uint32_t word) {
     if (valigned && rel + 4 <= nrel) {
       *(uint32_t *)(vbase + rel) = word;
     } else {
       for (uint32_t u = 0; u < 4 && rel + u < nrel; ++u) vbase[rel + u] = (uint8_t)(word >> (8 * u));
     }
-  }
-  FSTAMP(1);
-  fused_barrier(f.sync, f.nblk, f.sync + 2);
+  };
+  auto put_spec = [&]() {
+#pragma unroll
+    for (int v = 0; v < FKV; ++v) {
+      const uint32_t rel = (uint32_t)v * FT * 4 + 4 * tid;
+      if (rel >= nrel) break;
+      put_word(rel, spec_word(v));
+    }
+  };
   FSTAMP(2);
+  fused_barrier(f, c, 1);
+  FSTAMP(3);
+  put_spec();
 
   // ---- phase 2: per bucket down its column ---------------------------------
   // Workgroup c takes a range of table words (4 buckets each); its threads
   // are 64 word lanes x 16 row slices (up to 16 rows each, all loads in
   // flight), so a bucket's column is summed by 16 threads at once.
   {
-    __shared__ uint32_t cst[64 * 4];    // c* found per (word lane, bucket)
-    __shared__ uint32_t tokl[64 * 4];   // the tokens before the batch
+    uint32_t *const cst = p23;          // c* found per (word lane, bucket)
+    uint32_t *const tokl = p23 + 256;   // the tokens before the batch
     const uint32_t wpb = (f.nwords + f.nblk - 1) / f.nblk;
     const uint32_t wlo = min(f.nwords, c * wpb), whi = min(f.nwords, wlo + wpb);
     const uint32_t rs = (f.nblk + FSL - 1) / FSL;          // rows per slice (<= 16)
@@ -738,20 +780,30 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         }
       }
       __syncthreads();
+      // the four buckets' totals and this slice's prefix (16-byte reads of
+      // the partial sums: one per slice, not one per slice and bucket)
+      uint32_t pre[4] = {0u, 0u, 0u, 0u}, tot[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (uint32_t s2 = 0; s2 < FSL; ++s2) {
+        const u32x4 x = *(const u32x4 *)(part + (s2 * 64 + wl) * 4);
+        const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          tot[q] += xs[q];
+          pre[q] += s2 < s ? xs[q] : 0u;
+        }
+      }
       // the slice holding the T_b-th frame finds its segment and rank
 #pragma unroll 1
       for (int q = 0; q < 4; ++q) {
         const uint32_t b = 4 * w + q;
-        uint32_t pre = 0, tot = 0;
-        for (uint32_t s2 = 0; s2 < FSL; ++s2) {
-          const uint32_t x = part[(s2 * 64 + wl) * 4 + q];
-          pre += s2 < s ? x : 0u;
-          tot += x;
-        }
         const uint32_t t = tokl[wl * 4 + q];
-        const uint32_t pq = part[(s * 64 + wl) * 4 + q];
-        if (on && b < a.hash_size && tot > t && t > 0 && pre < t && t <= pre + pq) {
-          uint32_t cum = pre;
+        // (selects: a register array indexed by the rolled q would go to scratch)
+        const uint32_t tq = q == 0 ? tot[0] : q == 1 ? tot[1] : q == 2 ? tot[2] : tot[3];
+        const uint32_t prq = q == 0 ? pre[0] : q == 1 ? pre[1] : q == 2 ? pre[2] : pre[3];
+        const uint32_t pq = q == 0 ? p[0] : q == 1 ? p[1] : q == 2 ? p[2] : p[3];
+        if (on && b < a.hash_size && tq > t && t > 0 && prq < t && t <= prq + pq) {
+          uint32_t cum = prq;
           for (uint32_t j = 0; j < rs; ++j) {
             uint32_t x = 0;
 #pragma unroll
@@ -773,29 +825,27 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t b = 4 * w + q;
-          uint32_t tot = 0;
-          for (uint32_t s2 = 0; s2 < FSL; ++s2) tot += part[(s2 * 64 + wl) * 4 + q];
           const uint32_t t = tokl[wl * 4 + q];
-          cd[q] = tot <= t ? CODE_ALL : t == 0 ? CODE_NONE : cst[wl * 4 + q];
-          if (b < a.hash_size) a.tokens[b] = t > tot ? t - tot : 0u;
+          cd[q] = tot[q] <= t ? CODE_ALL : t == 0 ? CODE_NONE : cst[wl * 4 + q];
+          if (b < a.hash_size) a.tokens[b] = t > tot[q] ? t - tot[q] : 0u;
         }
         if (2 * w < words) st_sc1(f.code + 2 * w, cd[0] | cd[1] << 16);
         if (2 * w + 1 < words) st_sc1(f.code + 2 * w + 1, cd[2] | cd[3] << 16);
-        if ((cd[0] & cd[1] & cd[2] & cd[3]) != CODE_ALL) st_sc1(f.sync + 3, 1u);
+        if ((cd[0] & cd[1] & cd[2] & cd[3]) != CODE_ALL) st_sc1(f.out, f.nonce);
       }
       __syncthreads();
     }
   }
-  FSTAMP(3);
-  fused_barrier(f.sync + 1, f.nblk, f.sync + 2);
   FSTAMP(4);
+  fused_barrier(f, c, 2);
+  FSTAMP(5);
   // no bucket ran out: the speculative verdicts stand
   {
     __shared__ uint32_t any_out;
-    if (tid == 0) any_out = ld_sc1(f.sync + 3);
+    if (tid == 0) any_out = ld_sc1(f.out) == f.nonce;
     __syncthreads();
-    if (any_out == 0) {
-      FSTAMP(7);
+    if (!any_out) {
+      FSTAMP(6);
       return;
     }
   }
@@ -821,30 +871,32 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     for (int h = 0; h < 2; ++h) {
       const uint32_t b = 2 * w + h;
       if (b < a.hash_size && ((x >> (16 * h)) & 0xffffu) == c) {
-        atomicOr(&rbit[b >> 5], 1u << (b & 31));
-        // rank to find, as a u16 (0: nothing left to find); the T_b-th
-        // frame being the segment's 65 536th means every frame of b here
+        // the rank to find, as a u16; the T_b-th frame being the segment's
+        // 65 536th means every frame of b here is permitted: CODE_ALL
         const uint32_t nd = ld_sc1(f.need + b);
-        uint32_t rem = nd;
-        if (nd > 0xffffu) {
-          f.lim[b] = (uint32_t)(lo + nd);
-          rem = 0;
+        uint32_t e = CODE_ALL;
+        if (nd <= 0xffffu) {
+          atomicOr(&rbit[b >> 5], 1u << (b & 31));
+          e = nd;
+          mine = true;
         }
-        x = (x & ~(0xffffu << (16 * h))) | (rem << (16 * h));
-        mine = true;
+        x = (x & ~(0xffffu << (16 * h))) | (e << (16 * h));
       }
     }
     tab[w] = x;
   }
   mine = __syncthreads_or(mine);
-  FSTAMP(5);
   // (16-bit accesses: the two buckets of a word are walked by different waves)
   uint16_t *const tab16 = (uint16_t *)tab;
   auto tabh = [&](uint32_t b) { return (uint32_t)tab16[b]; };
   auto isc = [&](uint32_t b) { return (rbit[b >> 5] >> (b & 31)) & 1u; };
+  // Candidate frames of this thread (bit 4 v + u): subjects of a bucket
+  // whose c* is this segment.  The ordered walk below leaves, for each such
+  // bucket, tab16[b] = the segment offset of its T_b-th frame (the last one
+  // permitted) and clears its rbit bit: the verdicts need no global limit.
+  uint64_t cm = 0;
   if (mine) {
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint64_t cm = 0;   // candidate frames of this thread (bit 4 v + u)
 #pragma unroll
     for (int v = 0; v < FKV; ++v) {
       __builtin_amdgcn_sched_barrier(0);   // (else all 64 LDS lookups are hoisted)
@@ -863,56 +915,111 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         k01 = vv == v ? kp[2 * vv] : k01;
         k23 = vv == v ? kp[2 * vv + 1] : k23;
       }
-      // block exclusive scan of the candidate counts (frame order)
-      const uint32_t cnt = (uint32_t)__popc(m);
-      uint32_t inc = cnt;
+      // Stable partition of the round's candidates by owner wave (b % 16),
+      // frame order kept inside each part: per-thread counts of the 16 parts
+      // packed four to a u64 (16-bit fields: a part holds <= 4096), block
+      // exclusive scan, one list slot per candidate.
+      constexpr int NW = FT / 64;
+      static_assert(NW == 16, "16 parts");
+      uint32_t bk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bk[u] = ((u < 2 ? k01 : k23) >> ((u & 1) * 16)) & 0xffffu;
+      uint64_t pc4[4] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t one = (m >> u) & 1u ? 1ull << (16 * (bk[u] & 3u)) : 0ull;
+        const uint32_t g = (bk[u] >> 2) & 3u;
+        pc4[0] += g == 0 ? one : 0ull;
+        pc4[1] += g == 1 ? one : 0ull;
+        pc4[2] += g == 2 ? one : 0ull;
+        pc4[3] += g == 3 ? one : 0ull;
+      }
+      // (no carries between the fields: every partial sum is <= 4096)
+      uint64_t off4[4] = {pc4[0], pc4[1], pc4[2], pc4[3]};   // inclusive, then exclusive
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d);
-        if (lane >= d) inc += y;
-      }
-      if (lane == 63) wsum[wv] = inc;
-      __syncthreads();
-      uint32_t basep = 0, total = 0;
-      for (int w = 0; w < FT / 64; ++w) {
-        const uint32_t y = wsum[w];
-        basep += w < wv ? y : 0u;
-        total += y;
-      }
-      basep += inc - cnt;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (m & (1u << u))
-          list[basep++] = (base_off + u) << 16 | (((u < 2 ? k01 : k23) >> ((u & 1) * 16)) & 0xffffu);
+        for (int g = 0; g < 4; ++g) {
+          const uint64_t y = __shfl_up(off4[g], d);
+          if (lane >= d) off4[g] += y;
+        }
+      }
+      uint64_t *const wtot = (uint64_t *)p23;   // [NW][4]
+      if (lane == 63) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) wtot[wv * 4 + g] = off4[g];
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) off4[g] -= pc4[g];
       __syncthreads();
-      // the ordered walk: wave wv takes the buckets with b % 16 == wv
-      for (uint32_t s0 = 0; s0 < total; s0 += 64) {
-        const uint32_t e = s0 + (uint32_t)lane < total ? list[s0 + lane] : NOSUBJ;
+      uint64_t tot4[4] = {0ull, 0ull, 0ull, 0ull};
+      for (int w = 0; w < NW; ++w) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint64_t y = wtot[w * 4 + g];
+          off4[g] += w < wv ? y : 0ull;
+          tot4[g] += y;
+        }
+      }
+      // part k: total and start in the list
+      auto field = [](const uint64_t x[4], uint32_t k) {
+        const uint64_t q = k >> 2 == 0 ? x[0] : k >> 2 == 1 ? x[1] : k >> 2 == 2 ? x[2] : x[3];
+        return (uint32_t)(q >> (16 * (k & 3u))) & 0xffffu;
+      };
+      uint32_t mybase = 0, mytot = 0, run = 0;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        const uint32_t t = field(tot4, (uint32_t)k);
+        mybase = k == wv ? run : mybase;
+        mytot = k == wv ? t : mytot;
+        run += t;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if ((m >> u) & 1u) {
+          const uint32_t k = bk[u] & 15u;
+          uint32_t kb = 0;   // start of part k
+          for (uint32_t k2 = 0; k2 < k; ++k2) kb += field(tot4, k2);
+          uint32_t pos = kb + field(off4, k);
+#pragma unroll
+          for (int u2 = 0; u2 < u; ++u2) pos += ((m >> u2) & 1u) && (bk[u2] & 15u) == k ? 1u : 0u;
+          list[pos] = (base_off + u) << 16 | bk[u];
+        }
+      }
+      __syncthreads();
+      // Wave wv walks its part in frame order, 64 candidates a step: lanes of
+      // one bucket found with 12 ballots (the bucket's low 4 bits are wv's),
+      // then every lane at once -- the T_b-th frame's lane records its offset
+      // and retires the bucket, else the bucket's last lane lowers the rank
+      // still to find.
+      for (uint32_t s0 = 0; s0 < mytot; s0 += 64) {
+        const bool valid = s0 + (uint32_t)lane < mytot;
+        const uint32_t e = valid ? list[mybase + s0 + lane] : 0u;
         const uint32_t b = e & 0xffffu;
-        const bool on = e != NOSUBJ && (b & (FT / 64 - 1)) == (uint32_t)wv;
-        uint64_t todo = __ballot(on);
-        while (todo) {
-          const int leader = __ffsll((unsigned long long)todo) - 1;
-          const uint32_t bb = __shfl(b, leader);
-          const uint64_t mm = __ballot(on && b == bb);
-          const uint32_t r0 = tabh(bb);
-          const uint32_t pc = (uint32_t)__popcll(mm);
-          if (r0 != 0) {
-            if (on && b == bb && (uint32_t)__popcll(mm & lt) + 1u == r0)
-              f.lim[bb] = (uint32_t)(lo + (e >> 16)) + 1u;
-            if (lane == leader) tab16[bb] = (uint16_t)(r0 > pc ? r0 - pc : 0u);
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for (int k = 4; k < 16; ++k) {
+          const bool bit = (b >> k) & 1u;
+          const uint64_t bm = __ballot(valid && bit);
+          same &= bit ? bm : ~bm;
+        }
+        const uint32_t rank = (uint32_t)__popcll(same & lt), cnt = (uint32_t)__popcll(same);
+        if (valid && isc(b)) {
+          const uint32_t r0 = tabh(b);   // rank still to find, >= 1
+          if (rank + 1u == r0) {
+            tab16[b] = (uint16_t)(e >> 16);
+            atomicAnd(&rbit[b >> 5], ~(1u << (b & 31)));
+          } else if (rank + 1u == cnt && r0 > cnt) {
+            tab16[b] = (uint16_t)(r0 - cnt);
           }
-          todo &= ~mm;
         }
       }
       __syncthreads();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the lim stores, before the reads below
     __syncthreads();
   }
   // (32-bit offsets from the segment start: the 64-bit frame index of
   // every round would be hoisted into 32 registers)
-  FSTAMP(6);
   const bool aligned = valigned;
 #pragma unroll
   for (int v = 0; v < FKV; ++v) {
@@ -925,20 +1032,24 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       const uint32_t kk = FKEY(v, u);
       if (!FSUBJ(v, u)) {
         vd[u] = 2u;
-      } else if (mine && isc(kk)) {   // (no candidate bucket here: no lookup)
-        vd[u] = lo32 + rel + u < ld_sc1(f.lim + kk) ? 1u : 0u;
+      } else if ((cm >> (4 * v + u)) & 1ull) {   // up to its T_b-th frame
+        vd[u] = rel + u <= tabh(kk) ? 1u : 0u;
       } else {
         const uint32_t cd = tabh(kk);
         vd[u] = cd == CODE_ALL ? 1u : cd == CODE_NONE ? 0u : c < cd ? 1u : 0u;
       }
     }
-    if (aligned && rel + 4 <= nrel) {
-      *(uint32_t *)(vbase + rel) = vd[0] | vd[1] << 8 | vd[2] << 16 | vd[3] << 24;
-    } else {
-      for (uint32_t u = 0; u < 4 && rel + u < nrel; ++u) vbase[rel + u] = (uint8_t)vd[u];
+    // (only the words that differ from the speculative ones)
+    const uint32_t word = vd[0] | vd[1] << 8 | vd[2] << 16 | vd[3] << 24;
+    if (word != spec_word(v)) {
+      if (aligned && rel + 4 <= nrel) {
+        *(uint32_t *)(vbase + rel) = word;
+      } else {
+        for (uint32_t u = 0; u < 4 && rel + u < nrel; ++u) vbase[rel + u] = (uint8_t)vd[u];
+      }
     }
   }
-  FSTAMP(7);
+  FSTAMP(6);
 #undef FKEY
 #undef FSUBJ
 #undef FSTAMP
@@ -1161,14 +1272,34 @@ void fused_layout(uint32_t nblk, uint32_t seg, uint32_t hash_size, void *base, P
   f.nblk = nblk;
   f.seg = seg;
   f.nwords = (hash_size + 3) / 4;
-  f.sync = take(256);
+  f.arrive = (uint64_t *)take(FMAXBLK * 8);
+  f.out = (uint64_t *)take(16);
+  f.stamps = take(FSTAMPS * FMAXBLK * 4);
   f.table = take((size_t)nblk * f.nwords * 4);
   f.ovf = take((size_t)nblk * FOVF * 8);
   f.novf = take((size_t)nblk * 4);
   f.need = take((size_t)hash_size * 4);
   f.code = take((size_t)((hash_size + 1) / 2) * 4);
-  f.lim = take((size_t)hash_size * 4);
   total = off;
+}
+
+// A launch's barrier nonce: distinct per launch in this process, random
+// across processes (a stale word in a reused scratch buffer never matches),
+// low two bits clear for the barrier generation, never 0 or ~0.
+uint64_t fused_nonce() {
+  static const uint64_t seed = [] {
+    std::random_device rd;
+    return ((uint64_t)rd() << 32 ^ rd()) ^
+           (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+  }();
+  static std::atomic<uint64_t> ctr{0};
+  for (;;) {
+    uint64_t z = seed + 0x9e3779b97f4a7c15ull * (ctr.fetch_add(1) + 1);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    z = (z ^ (z >> 31)) & ~3ull;
+    if (z != 0 && z != (~0ull & ~3ull)) return z;
+  }
 }
 
 // The fused kernel fits one workgroup per CU (its registers and 150 KB of
@@ -1214,8 +1345,7 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
     PermitFused f;
     size_t total = 0;
     fused_layout(g.nblk, g.seg, a.hash_size, scratch, f, total);
-    hipError_t e = hipMemsetAsync(f.sync, 0, 64, st);
-    if (e != hipSuccess) return e;
+    f.nonce = fused_nonce();
     hipLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, a, f);
     return hipGetLastError();
   }

@@ -9,30 +9,37 @@ sys.path.insert(0, ROOT)
 
 
 def stamps():
-    """The fused rate limiter's phase timestamps (workgroup 0, 100 MHz
-    clock, PermitFused::sync[8..15]) on 16 M dense keys, 2^16 buckets, as
-    bench's keys / keys_denying runs: microseconds from the kernel's start."""
+    """The fused rate limiter's phase timestamps (every workgroup, 100 MHz
+    clock, PermitFused::stamps: 7 x 256 words after the 2 KB of barrier
+    words and 256 B of flags at the start of the scratch) on 16 M dense keys,
+    2^16 buckets, as bench's keys / keys_denying runs: microseconds from the
+    earliest workgroup start, min / median / max over the 256 workgroups."""
     import numpy as np
     import torch
     from pptk_amd.rx import RxContext
     dev = torch.device("cuda", 0)
-    n, hs = 16 * 1024 * 1024, 1 << 16
+    n, hs, nblk = 16 * 1024 * 1024, 1 << 16, 256
     ctx = RxContext(0, bytes(range(1, 17)), 24, 0, hs)
     keys = torch.randint(0, hs, (n,), dtype=torch.int32, device=dev)
     scratch = torch.zeros(ctx._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8, device=dev)
+    labels = ["start", "histogram", "row written", "barrier 1", "phase 2", "barrier 2", "verdicts"]
+    off = 2048 + 256
     out = {}
     for name, t in (("keys", 1 << 20), ("keys_denying", 128)):
-        rows = []
+        runs = []
         for _ in range(8):
             tok = torch.full((hs,), t, dtype=torch.int32, device=dev)
             ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
             torch.cuda.synchronize()
-            w = scratch[:64].view(torch.int32).cpu().numpy().view(np.uint32)
-            st = w[8:16].astype(np.int64)
-            rows.append([round(float(x - st[0]) / 100.0, 2) for x in st])
-        out[name] = {"phase_stamps_us": rows[len(rows) // 2],
-                     "labels": ["start", "row written", "barrier 1", "phase 2", "barrier 2",
-                                "code staged", "resolved", "verdicts"]}
+            w = scratch[off:off + len(labels) * nblk * 4].view(torch.int32).cpu().numpy()
+            st = w.view(np.uint32).astype(np.int64).reshape(len(labels), nblk)
+            runs.append((st - st[0].min()) / 100.0)
+        r = runs[len(runs) // 2]
+        out[name] = {lab: [round(float(r[k].min()), 2), round(float(np.median(r[k])), 2),
+                           round(float(r[k].max()), 2)] for k, lab in enumerate(labels)}
+        out[name]["slowest_phase1_blocks"] = [int(x) for x in np.argsort(r[2] - r[0])[-8:]]
+        out[name]["slowest_phase2_blocks"] = [int(x) for x in np.argsort(r[4] - r[3])[-8:]]
+    out["unit"] = "us from the earliest workgroup start: [min, median, max] over workgroups"
     print(json.dumps(out), flush=True)
 
 
