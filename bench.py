@@ -873,7 +873,7 @@ def mss_bench(ctx, n, dev, steps, warmup, stride=80):
 
 
 def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
-                 runs=("records", "keys", "keys_denying"), tune=None):
+                 runs=("records", "keys", "keys_denying"), tune=None, lib_path=None):
     """Batched ip_permitted over a C64 batch: buckets of
     the /24 source prefixes in 2^16 buckets, every IPv4 frame a subject, one
     token array carried across the timed batches.  Three runs:
@@ -893,7 +893,7 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
     from pptk_amd.rx import RxContext
     from tools.synth import make_batch
     b = make_batch("c64", n, dev, first=rank * n)
-    ctx = RxContext(dev.index, KEY, 24, 0, hash_size)
+    ctx = RxContext(dev.index, KEY, 24, 0, hash_size, lib_path=lib_path)
     if tune is not None:          # (A/B: PPTK_RX_TUNE_PERMIT_PASSES = the four-launch path)
         ctx.set_tuning(-1, tune)
     keys = torch.empty(n, dtype=torch.int32, device=dev)

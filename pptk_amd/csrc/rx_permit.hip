@@ -427,26 +427,29 @@ __global__ __launch_bounds__(HT) void permit_verdicts_tab(PermitArgs a, const ui
 //   2. per bucket, down its column (the table read once): total, the segment
 //      c* holding the T_b-th frame and that frame's rank need_b inside c*;
 //      code[b] (all / none / c*) and the new token count;
-//   3. the code table staged in LDS; a segment that is some bucket's c*
-//      ranks, round by round in frame order, its frames of such buckets
-//      (ballots, as permit_resolve) -- the keys are its own registers, no
-//      second read -- and every thread writes its 64 verdicts.
+//   3. only if some bucket ran out (else the speculative verdicts, written
+//      at the start of phase 2 as if every subject were permitted, stand and
+//      the launch ends): the code table staged in LDS; a segment that is
+//      some bucket's c* ranks, round by round in frame order, its frames of
+//      such buckets (ballots, as permit_resolve; buckets whose T_b-th frame
+//      is their last one here need no ranking) -- the keys are its own
+//      registers, no second read -- and every thread rewrites the verdict
+//      words that differ.
 // HBM: keys once (67 MB), the u8 table twice (2 x 16.8 MB), verdicts (17
 // MB): ~118 MB, 1.4 x the algorithmic bytes.  The table and the phase-2
 // outputs are handed between workgroups with write-through (sc1) stores and
-// sc1 loads behind one agent-scope counter per barrier (MI355X_MICROARCH.md
-// "inter-workgroup visibility", the one-workgroup-per-CU row): no L2
-// write-back fences.  Co-residency: the grid is at most one workgroup per
-// CU and each needs > 80 KB of LDS, so no CU holds two; a workgroup not yet
-// resident (a CU busy with another stream's kernel) only delays the others.
-// Every spin is bounded (FUSED_SPIN_TICKS): a barrier that times out marks
-// the status word (PermitFused::status) instead of hanging the GPU.
+// sc1 loads; the grid barriers are per-workgroup arrival words holding the
+// launch's nonce (no memset before a launch: a stale word never matches)
+// (MI355X_MICROARCH.md "inter-workgroup visibility", the
+// one-workgroup-per-CU row): no L2 write-back fences.  Co-residency: the
+// grid is at most one workgroup per CU and each needs > 80 KB of LDS, so no
+// CU holds two; a workgroup not yet resident (a CU busy with another
+// stream's kernel) only delays the others.  Every spin is bounded
+// (FUSED_SPIN_TICKS): a barrier that times out marks a status word
+// (PermitFused::out[1]) instead of hanging the GPU.
 constexpr int FT = 1024;                  // threads per workgroup
 constexpr int FKV = 16;                   // 16-byte key loads per thread (64 frames)
-#ifndef PPTK_PERMIT_FKB
-#define PPTK_PERMIT_FKB 16
-#endif
-constexpr int FKB = PPTK_PERMIT_FKB;      // of them in flight at once (whole segments)
+constexpr int FKB = 4;                    // of them per batch (two batches in flight)
 constexpr uint32_t FSEG = FT * 4 * FKV;   // frames per segment at most (65 536)
 constexpr uint32_t FOVF = FSEG / 255 + 1; // saturated buckets per segment at most
 constexpr int FSL = 16;                   // phase 2: row slices per word
@@ -465,7 +468,7 @@ struct PermitFused {
   uint64_t nonce;    // this launch's, low two bits clear (never 0 or ~0)
   uint32_t nblk, seg, nwords;
 };
-constexpr int FSTAMPS = 7;
+constexpr int FSTAMPS = 11;
 
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -546,8 +549,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   __shared__ uint32_t rbit[HMAX / 32];  // phase 3: buckets whose c* is this segment
   __shared__ __attribute__((aligned(16))) uint32_t list[FT * 4];   // phase 2 partial sums; phase 3 candidate list
   __shared__ uint32_t wsum[FT / 64 + 1];
-  // phase 2: c* found and tokens per (word lane, bucket); phase 3: per-wave
-  // totals of the candidate partition
+  // phase 2: c* found and tokens per (word lane, bucket)
   __shared__ __attribute__((aligned(16))) uint32_t p23[512];
   const uint32_t c = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
@@ -582,28 +584,31 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   if (fast) {
     const uint32_t nv = f.seg / (FT * 4);
     const bool subj = a.subject != nullptr;
-#pragma unroll
-    for (int h = 0; h < FKV / FKB; ++h) {
+    // Batches of FKB rounds, double-buffered: batch h + 1 is in flight while
+    // batch h is counted (2 FKB loads outstanding per thread at most)
+    u32x4 qa[FKB], qb[FKB];
+    uint32_t sa[FKB], sbb[FKB];
+    auto load = [&](u32x4 (&q)[FKB], uint32_t (&sw)[FKB], int h) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
-      u32x4 q[FKB];
-      uint32_t sb[FKB];
 #pragma unroll
-      for (int v8 = 0; v8 < FKB; ++v8) {
-        const int v = h * FKB + v8;
+      for (int k = 0; k < FKB; ++k) {
+        const int v = h * FKB + k;
         const uint64_t i = lo + (uint64_t)((uint32_t)v < nv ? v : 0) * FT * 4 + 4 * tid;
-        q[v8] = *(const u32x4 *)(a.keys_in + i);
-        sb[v8] = subj ? *(const uint32_t *)(a.subject + i) : 0x01010101u;
+        q[k] = *(const u32x4 *)(a.keys_in + i);
+        sw[k] = subj ? *(const uint32_t *)(a.subject + i) : 0x01010101u;
       }
-      if (h == 0) clear_tab();   // (behind the first loads)
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto count = [&](const u32x4 (&q)[FKB], const uint32_t (&sw)[FKB], int h)
+        __attribute__((always_inline)) {
 #pragma unroll
-      for (int v8 = 0; v8 < FKB; ++v8) {
-        const int v = h * FKB + v8;
+      for (int k = 0; k < FKB; ++k) {
+        const int v = h * FKB + k;
         const bool live = (uint32_t)v < nv;
-        const uint32_t sw = sb[v8];
-        uint32_t kk[4] = {q[v8].x, q[v8].y, q[v8].z, q[v8].w};
+        uint32_t kk[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          kk[u] = live && ((sw >> (8 * u)) & 0xffu) ? filter_key(a, kk[u]) : NOSUBJ;
+          kk[u] = live && ((sw[k] >> (8 * u)) & 0xffu) ? filter_key(a, kk[u]) : NOSUBJ;
           if (kk[u] != NOSUBJ) {
             atomicAdd(&tab[kk[u] >> 1], 1u << ((kk[u] & 1u) * 16u));
             sm |= 1ull << (v * 4 + u);
@@ -613,7 +618,18 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         kp[2 * v + 1] = (kk[2] & 0xffffu) | kk[3] << 16;
         asm volatile("" : "+v"(kp[2 * v]), "+v"(kp[2 * v + 1]));
       }
-    }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    static_assert(FKV / FKB == 4, "four batches");
+    clear_tab();   // (a barrier after the loads would wait for them all)
+    load(qa, sa, 0);
+    load(qb, sbb, 1);
+    count(qa, sa, 0);
+    load(qa, sa, 2);
+    count(qb, sbb, 1);
+    load(qb, sbb, 3);
+    count(qa, sa, 2);
+    count(qb, sbb, 3);
   } else {
   clear_tab();
 #pragma unroll
@@ -716,9 +732,11 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     }
   };
   FSTAMP(2);
+#ifdef PPTK_PERMIT_SPEC_EARLY   // (A/B: the speculative verdicts before the table loads)
+  put_spec();
+#endif
   fused_barrier(f, c, 1);
   FSTAMP(3);
-  put_spec();
 
   // ---- phase 2: per bucket down its column ---------------------------------
   // Workgroup c takes a range of table words (4 buckets each); its threads
@@ -835,6 +853,12 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       }
       __syncthreads();
     }
+    // the speculative verdicts, after the table loads (issued ahead of them
+    // they would hold up their first use: loads and stores share one
+    // in-order memory counter); they drain into the barrier
+#ifndef PPTK_PERMIT_SPEC_EARLY
+    put_spec();
+#endif
   }
   FSTAMP(4);
   fused_barrier(f, c, 2);
@@ -855,6 +879,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   for (uint32_t w = tid; w < rbw; w += FT) rbit[w] = 0;
   __syncthreads();
   bool mine = false;
+  uint16_t *const tab16s = (uint16_t *)tab;
   constexpr int SW = HMAX / 2 / FT;   // code words per thread (at most)
   uint32_t cw[SW];                    // all loads in flight at once
 #pragma unroll
@@ -862,30 +887,57 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     const uint32_t w = tid + j * FT;
     cw[j] = w < words ? ld_sc1(f.code + w) : 0u;
   }
+  // the codes into LDS; this segment's c* buckets (bit 2 j + h) get, in a
+  // second pass, the rank to find
+  uint64_t cs = 0;
 #pragma unroll
   for (int j = 0; j < SW; ++j) {
     const uint32_t w = tid + j * FT;
     if (w >= words) break;
-    uint32_t x = cw[j];
+    const uint32_t x = cw[j];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t b = 2 * w + h;
-      if (b < a.hash_size && ((x >> (16 * h)) & 0xffffu) == c) {
-        // the rank to find, as a u16; the T_b-th frame being the segment's
-        // 65 536th means every frame of b here is permitted: CODE_ALL
-        const uint32_t nd = ld_sc1(f.need + b);
-        uint32_t e = CODE_ALL;
-        if (nd <= 0xffffu) {
-          atomicOr(&rbit[b >> 5], 1u << (b & 31));
-          e = nd;
-          mine = true;
-        }
-        x = (x & ~(0xffffu << (16 * h))) | (e << (16 * h));
-      }
-    }
+    for (int h = 0; h < 2; ++h)
+      if (2 * w + h < a.hash_size && ((x >> (16 * h)) & 0xffffu) == c) cs |= 1ull << (2 * j + h);
     tab[w] = x;
   }
+  // The rank to find, as a u16.  The T_b-th frame being b's last frame here
+  // (its count in this segment's row) means every frame of b here is
+  // permitted: CODE_ALL, no ranking -- with few frames per bucket and
+  // segment the common case.  Loads in batches of 8 buckets, unconditional
+  // (bucket 0 for the others), so a segment that is c* for most buckets
+  // waits 8 round trips, not one per bucket.
+  if (cs) {
+#pragma unroll
+    for (int j0 = 0; j0 < SW; j0 += 4) {
+      if (((cs >> (2 * j0)) & 0xffull) == 0) continue;
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t nd[8], rw[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = j0 + k / 2, h = k & 1;
+        const uint32_t b = (cs >> (2 * j + h)) & 1ull ? 2 * (tid + j * FT) + h : 0u;
+        nd[k] = ld_sc1(f.need + b);
+        rw[k] = ld_sc1(f.table + (uint64_t)c * f.nwords + (b >> 2));
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = j0 + k / 2, h = k & 1;
+        if (!((cs >> (2 * j + h)) & 1ull)) continue;
+        const uint32_t b = 2 * (tid + j * FT) + h;
+        uint32_t kb = (rw[k] >> (8 * (b & 3u))) & 0xffu;
+        if (kb == 255u) kb = fused_ovf(f, c, b);
+        uint32_t e = CODE_ALL;
+        if (nd[k] < kb) {
+          atomicOr(&rbit[b >> 5], 1u << (b & 31));
+          e = nd[k];
+          mine = true;
+        }
+        tab16s[b] = (uint16_t)e;
+      }
+    }
+  }
   mine = __syncthreads_or(mine);
+  FSTAMP(7);
   // (16-bit accesses: the two buckets of a word are walked by different waves)
   uint16_t *const tab16 = (uint16_t *)tab;
   auto tabh = [&](uint32_t b) { return (uint32_t)tab16[b]; };
@@ -904,8 +956,11 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       for (int u = 0; u < 4; ++u)
         if (FSUBJ(v, u) && isc(FKEY(v, u))) cm |= 1ull << (4 * v + u);
     }
+    // (diagnostics: wave 0's time in the list building and in the walk)
+    uint64_t t_list = 0, t_walk = 0, tr0 = 0, tw0 = 0;
 #pragma unroll 1
     for (int v = 0; v < FKV; ++v) {
+      if (tid == 0) tr0 = __builtin_amdgcn_s_memrealtime();
       const uint32_t base_off = (uint32_t)v * FT * 4 + 4 * tid;
       const uint32_t m = (uint32_t)(cm >> (4 * v)) & 15u;
       // this round's two key registers (a select: the array stays in registers)
@@ -915,109 +970,69 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         k01 = vv == v ? kp[2 * vv] : k01;
         k23 = vv == v ? kp[2 * vv + 1] : k23;
       }
-      // Stable partition of the round's candidates by owner wave (b % 16),
-      // frame order kept inside each part: per-thread counts of the 16 parts
-      // packed four to a u64 (16-bit fields: a part holds <= 4096), block
-      // exclusive scan, one list slot per candidate.
-      constexpr int NW = FT / 64;
-      static_assert(NW == 16, "16 parts");
-      uint32_t bk[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) bk[u] = ((u < 2 ? k01 : k23) >> ((u & 1) * 16)) & 0xffffu;
-      uint64_t pc4[4] = {0ull, 0ull, 0ull, 0ull};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t one = (m >> u) & 1u ? 1ull << (16 * (bk[u] & 3u)) : 0ull;
-        const uint32_t g = (bk[u] >> 2) & 3u;
-        pc4[0] += g == 0 ? one : 0ull;
-        pc4[1] += g == 1 ? one : 0ull;
-        pc4[2] += g == 2 ? one : 0ull;
-        pc4[3] += g == 3 ? one : 0ull;
-      }
-      // (no carries between the fields: every partial sum is <= 4096)
-      uint64_t off4[4] = {pc4[0], pc4[1], pc4[2], pc4[3]};   // inclusive, then exclusive
+      // block exclusive scan of the candidate counts (frame order)
+      const uint32_t cnt = (uint32_t)__popc(m);
+      uint32_t inc = cnt;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint64_t y = __shfl_up(off4[g], d);
-          if (lane >= d) off4[g] += y;
-        }
+        const uint32_t y = __shfl_up(inc, d);
+        if (lane >= d) inc += y;
       }
-      uint64_t *const wtot = (uint64_t *)p23;   // [NW][4]
-      if (lane == 63) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) wtot[wv * 4 + g] = off4[g];
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) off4[g] -= pc4[g];
+      if (lane == 63) wsum[wv] = inc;
       __syncthreads();
-      uint64_t tot4[4] = {0ull, 0ull, 0ull, 0ull};
-      for (int w = 0; w < NW; ++w) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint64_t y = wtot[w * 4 + g];
-          off4[g] += w < wv ? y : 0ull;
-          tot4[g] += y;
-        }
+      uint32_t basep = 0, total = 0;
+      for (int w = 0; w < FT / 64; ++w) {
+        const uint32_t y = wsum[w];
+        basep += w < wv ? y : 0u;
+        total += y;
       }
-      // part k: total and start in the list
-      auto field = [](const uint64_t x[4], uint32_t k) {
-        const uint64_t q = k >> 2 == 0 ? x[0] : k >> 2 == 1 ? x[1] : k >> 2 == 2 ? x[2] : x[3];
-        return (uint32_t)(q >> (16 * (k & 3u))) & 0xffffu;
-      };
-      uint32_t mybase = 0, mytot = 0, run = 0;
+      basep += inc - cnt;
 #pragma unroll
-      for (int k = 0; k < NW; ++k) {
-        const uint32_t t = field(tot4, (uint32_t)k);
-        mybase = k == wv ? run : mybase;
-        mytot = k == wv ? t : mytot;
-        run += t;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if ((m >> u) & 1u) {
-          const uint32_t k = bk[u] & 15u;
-          uint32_t kb = 0;   // start of part k
-          for (uint32_t k2 = 0; k2 < k; ++k2) kb += field(tot4, k2);
-          uint32_t pos = kb + field(off4, k);
-#pragma unroll
-          for (int u2 = 0; u2 < u; ++u2) pos += ((m >> u2) & 1u) && (bk[u2] & 15u) == k ? 1u : 0u;
-          list[pos] = (base_off + u) << 16 | bk[u];
-        }
-      }
+      for (int u = 0; u < 4; ++u)
+        if (m & (1u << u))
+          list[basep++] = (base_off + u) << 16 | (((u < 2 ? k01 : k23) >> ((u & 1) * 16)) & 0xffffu);
       __syncthreads();
-      // Wave wv walks its part in frame order, 64 candidates a step: lanes of
-      // one bucket found with 12 ballots (the bucket's low 4 bits are wv's),
-      // then every lane at once -- the T_b-th frame's lane records its offset
-      // and retires the bucket, else the bucket's last lane lowers the rank
-      // still to find.
-      for (uint32_t s0 = 0; s0 < mytot; s0 += 64) {
-        const bool valid = s0 + (uint32_t)lane < mytot;
-        const uint32_t e = valid ? list[mybase + s0 + lane] : 0u;
+      // the ordered walk: wave wv takes the buckets with b % 16 == wv, one
+      // distinct bucket of a 64-entry step per ballot
+      if (tid == 0) tw0 = __builtin_amdgcn_s_memrealtime();
+      for (uint32_t s0 = 0; s0 < total; s0 += 64) {
+        const uint32_t e = s0 + (uint32_t)lane < total ? list[s0 + lane] : NOSUBJ;
         const uint32_t b = e & 0xffffu;
-        uint64_t same = __ballot(valid);
-#pragma unroll
-        for (int k = 4; k < 16; ++k) {
-          const bool bit = (b >> k) & 1u;
-          const uint64_t bm = __ballot(valid && bit);
-          same &= bit ? bm : ~bm;
-        }
-        const uint32_t rank = (uint32_t)__popcll(same & lt), cnt = (uint32_t)__popcll(same);
-        if (valid && isc(b)) {
-          const uint32_t r0 = tabh(b);   // rank still to find, >= 1
-          if (rank + 1u == r0) {
-            tab16[b] = (uint16_t)(e >> 16);
-            atomicAnd(&rbit[b >> 5], ~(1u << (b & 31)));
-          } else if (rank + 1u == cnt && r0 > cnt) {
-            tab16[b] = (uint16_t)(r0 - cnt);
+        const bool on = e != NOSUBJ && (b & (FT / 64 - 1)) == (uint32_t)wv;
+        uint64_t todo = __ballot(on);
+        while (todo) {
+          const int leader = __ffsll((unsigned long long)todo) - 1;
+          const uint32_t bb = __shfl(b, leader);
+          const uint64_t mm = __ballot(on && b == bb);
+          if (isc(bb)) {   // (else its frame was found in an earlier step)
+            const uint32_t r0 = tabh(bb);   // rank still to find, >= 1
+            const uint32_t pc = (uint32_t)__popcll(mm);
+            if (r0 <= pc) {
+              if (on && b == bb && (uint32_t)__popcll(mm & lt) + 1u == r0) {
+                tab16[bb] = (uint16_t)(e >> 16);
+                atomicAnd(&rbit[bb >> 5], ~(1u << (bb & 31)));
+              }
+            } else if (lane == leader) {
+              tab16[bb] = (uint16_t)(r0 - pc);
+            }
           }
+          todo &= ~mm;
         }
+      }
+      if (tid == 0) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        t_walk += t - tw0;
+        t_list += tw0 - tr0;
       }
       __syncthreads();
     }
     __syncthreads();
+    if (tid == 0) {
+      f.stamps[9 * FMAXBLK + c] = (uint32_t)t_list;
+      f.stamps[10 * FMAXBLK + c] = (uint32_t)t_walk;
+    }
   }
+  FSTAMP(8);
   // (32-bit offsets from the segment start: the 64-bit frame index of
   // every round would be hoisted into 32 registers)
   const bool aligned = valigned;

@@ -1,5 +1,5 @@
 """BENCH TOOLING: run bench.py's rate-limiter workload once (for rocprofv3
-wrapping): python tools/permit_run.py [runs] [--ab]"""
+wrapping): python tools/permit_run.py [runs] [--ab] [--lib=NAME=PATH ...]"""
 import json
 import os
 import sys
@@ -10,7 +10,7 @@ sys.path.insert(0, ROOT)
 
 def stamps():
     """The fused rate limiter's phase timestamps (every workgroup, 100 MHz
-    clock, PermitFused::stamps: 7 x 256 words after the 2 KB of barrier
+    clock, PermitFused::stamps: 11 x 256 words after the 2 KB of barrier
     words and 256 B of flags at the start of the scratch) on 16 M dense keys,
     2^16 buckets, as bench's keys / keys_denying runs: microseconds from the
     earliest workgroup start, min / median / max over the 256 workgroups."""
@@ -22,7 +22,8 @@ def stamps():
     ctx = RxContext(0, bytes(range(1, 17)), 24, 0, hs)
     keys = torch.randint(0, hs, (n,), dtype=torch.int32, device=dev)
     scratch = torch.zeros(ctx._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8, device=dev)
-    labels = ["start", "histogram", "row written", "barrier 1", "phase 2", "barrier 2", "verdicts"]
+    labels = ["start", "histogram", "row written", "barrier 1", "phase 2", "barrier 2", "verdicts",
+              "codes staged", "boundaries found"]
     off = 2048 + 256
     out = {}
     for name, t in (("keys", 1 << 20), ("keys_denying", 128)):
@@ -35,6 +36,14 @@ def stamps():
             st = w.view(np.uint32).astype(np.int64).reshape(len(labels), nblk)
             runs.append((st - st[0].min()) / 100.0)
         r = runs[len(runs) // 2]
+        # durations (ticks) of wave 0's list building and walk, phase 3
+        dur = scratch[off + len(labels) * nblk * 4:off + (len(labels) + 2) * nblk * 4]
+        dur = dur.view(torch.int32).cpu().numpy().view(np.uint32).reshape(2, nblk) / 100.0
+        hb = int(np.argmax(r[8] - r[7])) if name == "keys_denying" else 0
+        out[name + "_phase3_heaviest"] = {"block": hb, "list_us": float(dur[0, hb]),
+                                          "walk_us": float(dur[1, hb]),
+                                          "median_list_us": float(np.median(dur[0])),
+                                          "median_walk_us": float(np.median(dur[1]))}
         out[name] = {lab: [round(float(r[k].min()), 2), round(float(np.median(r[k])), 2),
                            round(float(r[k].max()), 2)] for k, lab in enumerate(labels)}
         out[name]["slowest_phase1_blocks"] = [int(x) for x in np.argsort(r[2] - r[0])[-8:]]
@@ -57,6 +66,12 @@ def main():
     if ab:   # the four-launch path on the same workload
         print(json.dumps({"passes": bench.permit_bench(16 * 1024 * 1024, dev, 1, 0, 20, 3, runs=runs,
                                                        tune=0x400)}), flush=True)
+    for a in sys.argv[1:]:   # --lib NAME=PATH: the fused path of another build
+        if a.startswith("--lib="):
+            name, path = a[6:].split("=", 1)
+            print(json.dumps({name: bench.permit_bench(16 * 1024 * 1024, dev, 1, 0, 20, 3, runs=runs,
+                                                       lib_path=os.path.join(ROOT, path))}),
+                  flush=True)
 
 
 if __name__ == "__main__":
