@@ -290,7 +290,10 @@ int pptk_rx_permit_device(struct pptk_rx_ctx *ctx, const struct pptk_rx_rec *d_r
  * subject (verdict 2, no token touched).  Up to 2^16 buckets and 16 M
  * frames (65 536 per CU) this runs as one persistent launch that reads the
  * keys once (DESIGN.md section 5 "Rate limiter"); beyond, or with
- * PPTK_RX_TUNE_PERMIT_PASSES set, as four launches. */
+ * PPTK_RX_TUNE_PERMIT_PASSES set, as four launches.  The scratch needs no
+ * initialisation; calls that share one scratch buffer must be ordered on
+ * one stream (a call overlapping another on the same scratch gives wrong
+ * verdicts, bounded by a 2 s spin, never a hang). */
 int pptk_rx_permit_keys_device(struct pptk_rx_ctx *ctx, const uint32_t *d_keys, uint64_t n,
                                int family, const uint8_t *d_subject, uint32_t *d_tokens,
                                uint8_t *d_verdict, void *d_scratch, void *stream);
