@@ -454,6 +454,9 @@ constexpr uint32_t FSEG = FT * 4 * FKV;   // frames per segment at most (65 536)
 constexpr uint32_t FOVF = FSEG / 255 + 1; // saturated buckets per segment at most
 constexpr int FSL = 16;                   // phase 2: row slices per word
 constexpr uint32_t FMAXBLK = 256;         // segments at most (rows of phase 2: 16 x 16)
+constexpr uint32_t FHASH_PASS = 2048;     // phase 3: candidates per hash-table pass at most
+constexpr uint32_t FHASH_MAXP = 32;       // hash-table passes at most
+constexpr uint32_t FHASH_K = 64;          // frames of one ranked bucket at most, hash path
 constexpr uint64_t FUSED_SPIN_TICKS = 200000000ull;   // 2 s of the 100 MHz clock
 
 struct PermitFused {
@@ -468,7 +471,7 @@ struct PermitFused {
   uint64_t nonce;    // this launch's, low two bits clear (never 0 or ~0)
   uint32_t nblk, seg, nwords;
 };
-constexpr int FSTAMPS = 11;
+constexpr int FSTAMPS = 12;
 
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -743,6 +746,11 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   // are 64 word lanes x 16 row slices (up to 16 rows each, all loads in
   // flight), so a bucket's column is summed by 16 threads at once.
   {
+    // some bucket of this workgroup's words ran out: one flag store per
+    // workgroup, not one per word (thousands of write-through stores to one
+    // address, all waited for by the barrier)
+    __shared__ uint32_t out_l;
+    if (tid == 0) out_l = 0;
     uint32_t *const cst = p23;          // c* found per (word lane, bucket)
     uint32_t *const tokl = p23 + 256;   // the tokens before the batch
     const uint32_t wpb = (f.nwords + f.nblk - 1) / f.nblk;
@@ -849,7 +857,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         }
         if (2 * w < words) st_sc1(f.code + 2 * w, cd[0] | cd[1] << 16);
         if (2 * w + 1 < words) st_sc1(f.code + 2 * w + 1, cd[2] | cd[3] << 16);
-        if ((cd[0] & cd[1] & cd[2] & cd[3]) != CODE_ALL) st_sc1(f.out, f.nonce);
+        if ((cd[0] & cd[1] & cd[2] & cd[3]) != CODE_ALL) out_l = 1u;
       }
       __syncthreads();
     }
@@ -859,6 +867,8 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #ifndef PPTK_PERMIT_SPEC_EARLY
     put_spec();
 #endif
+    __syncthreads();
+    if (tid == 0 && out_l) st_sc1(f.out, f.nonce);
   }
   FSTAMP(4);
   fused_barrier(f, c, 2);
@@ -878,7 +888,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   const uint32_t rbw = (a.hash_size + 31) / 32;
   for (uint32_t w = tid; w < rbw; w += FT) rbit[w] = 0;
   __syncthreads();
-  bool mine = false;
+  bool mine = false, many = false;
   uint16_t *const tab16s = (uint16_t *)tab;
   constexpr int SW = HMAX / 2 / FT;   // code words per thread (at most)
   uint32_t cw[SW];                    // all loads in flight at once
@@ -903,27 +913,56 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   // The rank to find, as a u16.  The T_b-th frame being b's last frame here
   // (its count in this segment's row) means every frame of b here is
   // permitted: CODE_ALL, no ranking -- with few frames per bucket and
-  // segment the common case.  Loads in batches of 8 buckets, unconditional
-  // (bucket 0 for the others), so a segment that is c* for most buckets
-  // waits 8 round trips, not one per bucket.
-  if (cs) {
+  // segment the common case.  The segment's c* buckets are compacted into
+  // the list (4 096 at a time) and spread evenly over the threads, so a
+  // segment that is c* for thousands of buckets costs one round trip of
+  // loads per 4 096 of them, not one per batch of a thread's words.
+  {
+    const uint32_t ncs = (uint32_t)__popcll(cs);
+    uint32_t inc = ncs;
 #pragma unroll
-    for (int j0 = 0; j0 < SW; j0 += 4) {
-      if (((cs >> (2 * j0)) & 0xffull) == 0) continue;
-      __builtin_amdgcn_sched_barrier(0);
-      uint32_t nd[8], rw[8];
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d);
+      if (lane >= d) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t base = inc - ncs, tcs = 0;
+    for (int w = 0; w < FT / 64; ++w) {
+      const uint32_t y = wsum[w];
+      base += w < wv ? y : 0u;
+      tcs += y;
+    }
+    constexpr uint32_t CH = FT * 4;
+#pragma unroll 1
+    for (uint32_t ch = 0; ch < tcs; ch += CH) {
+      __syncthreads();   // (the previous chunk's list reads are done)
+      if (cs) {
+        uint32_t pos = base;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int j = j0 + k / 2, h = k & 1;
-        const uint32_t b = (cs >> (2 * j + h)) & 1ull ? 2 * (tid + j * FT) + h : 0u;
+        for (int j = 0; j < SW; ++j) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (!((cs >> (2 * j + h)) & 1ull)) continue;
+            if (pos >= ch && pos < ch + CH) list[pos - ch] = 2 * (tid + (uint32_t)j * FT) + (uint32_t)h;
+            ++pos;
+          }
+        }
+      }
+      __syncthreads();
+      const uint32_t nch = min(CH, tcs - ch);
+      uint32_t nd[CH / FT], rw[CH / FT];
+#pragma unroll
+      for (int k = 0; k < (int)(CH / FT); ++k) {   // all loads first
+        const uint32_t i = tid + (uint32_t)k * FT;
+        const uint32_t b = i < nch ? list[i] : 0u;
         nd[k] = ld_sc1(f.need + b);
         rw[k] = ld_sc1(f.table + (uint64_t)c * f.nwords + (b >> 2));
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int j = j0 + k / 2, h = k & 1;
-        if (!((cs >> (2 * j + h)) & 1ull)) continue;
-        const uint32_t b = 2 * (tid + j * FT) + h;
+      for (int k = 0; k < (int)(CH / FT); ++k) {
+        if (tid + (uint32_t)k * FT >= nch) continue;
+        const uint32_t b = list[tid + (uint32_t)k * FT];
         uint32_t kb = (rw[k] >> (8 * (b & 3u))) & 0xffu;
         if (kb == 255u) kb = fused_ovf(f, c, b);
         uint32_t e = CODE_ALL;
@@ -931,12 +970,14 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
           atomicOr(&rbit[b >> 5], 1u << (b & 31));
           e = nd[k];
           mine = true;
+          many = many || kb > FHASH_K;
         }
         tab16s[b] = (uint16_t)e;
       }
     }
   }
   mine = __syncthreads_or(mine);
+  many = __syncthreads_or(many);
   FSTAMP(7);
   // (16-bit accesses: the two buckets of a word are walked by different waves)
   uint16_t *const tab16 = (uint16_t *)tab;
@@ -956,6 +997,139 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       for (int u = 0; u < 4; ++u)
         if (FSUBJ(v, u) && isc(FKEY(v, u))) cm |= 1ull << (4 * v + u);
     }
+    // the segment's candidate count
+    uint32_t ncand = (uint32_t)__popcll(cm);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) ncand += __shfl_xor(ncand, d);
+    if (lane == 0) wsum[wv] = ncand;
+    __syncthreads();
+    ncand = 0;
+    for (int w = 0; w < FT / 64; ++w) ncand += wsum[w];
+    __syncthreads();   // (wsum is reused below)
+    // Ranking by hash tables when no ranked bucket has more than FHASH_K
+    // frames here (counting along a probe sequence costs a bucket's frames
+    // once per frame): the candidates go in passes by bucket class, a pass
+    // being at most FHASH_PASS of them in the list's 4 096 slots (load <=
+    // 1/2, double hashing: short probe sequences for every lane of a wave).
+    // In a pass each candidate is inserted as (offset << 16 | bucket), then
+    // counts the frames of its bucket at smaller offsets along its bucket's
+    // probe sequence (its rank, in frame order), and the one whose rank + 1
+    // is the bucket's rank to find is the boundary frame.  More classes than
+    // FHASH_MAXP, or a class over FHASH_PASS: the ordered walk below.
+    const uint32_t npass = max(1u, (ncand + FHASH_PASS * 3 / 4 - 1) / (FHASH_PASS * 3 / 4));
+    uint32_t *const ccnt = p23 + 128;   // per-class candidate counts (p23[0..127]: occupancy)
+    bool hashed = !many && npass <= FHASH_MAXP;
+    auto hash1 = [](uint32_t b) { return b * 0x9E3779B1u; };
+    auto cls = [&](uint32_t b) { return (((hash1(b) >> 8) & 0xffffu) * npass) >> 16; };   // (no division)
+    if (hashed) {
+      for (uint32_t i = tid; i < npass; i += FT) ccnt[i] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < FKV; ++v) {
+        if (((cm >> (4 * v)) & 15ull) == 0) continue;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if ((cm >> (4 * v + u)) & 1ull) atomicAdd(&ccnt[cls(FKEY(v, u))], 1u);
+      }
+      __syncthreads();
+      bool over = false;
+      for (uint32_t i = 0; i < npass; ++i) over = over || ccnt[i] > FHASH_PASS;
+      hashed = !over;
+    }
+    if (hashed) {
+      constexpr uint32_t HC = FT * 4;
+      uint32_t *const occ = p23;        // slot occupancy, 128 words
+      uint32_t *const ent = rbit;       // the pass's candidates, compacted (no longer needed as rbit)
+      auto off_at = [&](int v, int u) { return (uint32_t)v * FT * 4 + 4 * tid + (uint32_t)u; };
+      uint64_t t_part = 0, t_rank = 0, t0 = 0;   // (diagnostics: wave 0's time)
+#pragma unroll 1
+      for (uint32_t pass = 0; pass < npass; ++pass) {
+        if (tid == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        // (opaque per pass: else the 64 keys and classes are hoisted out of
+        // the pass loop into 64 more registers)
+#pragma unroll
+        for (int q = 0; q < FKV * 2; ++q) asm volatile("" : "+v"(kp[q]));
+        for (uint32_t i = tid; i < HC / 32; i += FT) occ[i] = 0;
+        // this pass's candidates of the thread, compacted block-wide (frame
+        // order does not matter here: ranks come from the offsets), so each
+        // thread then handles at most two entries -- a wave runs two probe
+        // loops, not one per round and lane that holds a candidate
+        uint64_t pm = 0;
+#pragma unroll
+        for (int v = 0; v < FKV; ++v) {
+          if (((cm >> (4 * v)) & 15ull) == 0) continue;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (((cm >> (4 * v + u)) & 1ull) && cls(FKEY(v, u)) == pass) pm |= 1ull << (4 * v + u);
+        }
+        const uint32_t pc = (uint32_t)__popcll(pm);
+        uint32_t inc = pc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(inc, d);
+          if (lane >= d) inc += y;
+        }
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        uint32_t pos = inc - pc, ptot = 0;
+        for (int w = 0; w < FT / 64; ++w) {
+          const uint32_t y = wsum[w];
+          pos += w < wv ? y : 0u;
+          ptot += y;
+        }
+#pragma unroll
+        for (int v = 0; v < FKV; ++v) {
+          if (((pm >> (4 * v)) & 15ull) == 0) continue;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if ((pm >> (4 * v + u)) & 1ull) ent[pos++] = off_at(v, u) << 16 | FKEY(v, u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          const uint64_t t = __builtin_amdgcn_s_memrealtime();
+          t_part += t - t0;
+          t0 = t;
+        }
+        auto step_of = [](uint32_t hv) { return ((hv >> 7) | 1u) & (HC - 1); };   // odd: visits every slot
+        for (uint32_t i = tid; i < ptot; i += FT) {
+          const uint32_t e = ent[i], hv = hash1(e & 0xffffu), step = step_of(hv);
+          for (uint32_t h = hv >> 20;; h = (h + step) & (HC - 1)) {
+            const uint32_t bit = 1u << (h & 31);
+            if (!(atomicOr(&occ[h >> 5], bit) & bit)) {
+              list[h] = e;
+              break;
+            }
+          }
+        }
+        __syncthreads();
+        uint32_t bnd[FHASH_PASS / FT];   // this thread's boundary entries (or NOSUBJ)
+#pragma unroll
+        for (int k = 0; k < (int)(FHASH_PASS / FT); ++k) {
+          const uint32_t i = tid + (uint32_t)k * FT;
+          bnd[k] = NOSUBJ;
+          if (i >= ptot) continue;
+          const uint32_t e = ent[i], b = e & 0xffffu, off = e >> 16;
+          const uint32_t hv = hash1(b), step = step_of(hv);
+          uint32_t rank = 0;
+          for (uint32_t h = hv >> 20; (occ[h >> 5] >> (h & 31)) & 1u; h = (h + step) & (HC - 1)) {
+            const uint32_t x = list[h];
+            rank += (x & 0xffffu) == b && (x >> 16) < off ? 1u : 0u;
+          }
+          if (rank + 1u == tabh(b)) bnd[k] = e;
+        }
+        __syncthreads();   // (every rank read before a limit replaces it)
+#pragma unroll
+        for (int k = 0; k < (int)(FHASH_PASS / FT); ++k)
+          if (bnd[k] != NOSUBJ) tab16[bnd[k] & 0xffffu] = (uint16_t)(bnd[k] >> 16);
+        __syncthreads();   // (ent, occ and wsum are rewritten by the next pass)
+        if (tid == 0) t_rank += __builtin_amdgcn_s_memrealtime() - t0;
+      }
+      if (tid == 0) {
+        f.stamps[9 * FMAXBLK + c] = (uint32_t)t_part;
+        f.stamps[10 * FMAXBLK + c] = (uint32_t)t_rank;
+        f.stamps[11 * FMAXBLK + c] = npass;
+      }
+    } else {
     // (diagnostics: wave 0's time in the list building and in the walk)
     uint64_t t_list = 0, t_walk = 0, tr0 = 0, tw0 = 0;
 #pragma unroll 1
@@ -1030,6 +1204,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     if (tid == 0) {
       f.stamps[9 * FMAXBLK + c] = (uint32_t)t_list;
       f.stamps[10 * FMAXBLK + c] = (uint32_t)t_walk;
+    }
     }
   }
   FSTAMP(8);

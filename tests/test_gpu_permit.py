@@ -287,15 +287,20 @@ def test_np_permit_matches_oracle():
     assert np.array_equal(v, vh) and np.array_equal(t, th)
 
 
-@pytest.mark.parametrize("case", ["whole_segment", "spread"])
+@pytest.mark.parametrize("case", ["whole_segment", "spread", "bunched"])
 def test_permit_keys_full_size(case, dev):
     """16 M dense keys (BASELINE's C64 batch size: one 65 536-frame segment
     per CU on the fused path).  whole_segment: the first segment is one
     bucket throughout (its u16 histogram counter wraps: the fused kernel
     detects it) with the bucket's T_b-th frame inside it, and a second
-    bucket whose budget ends in a late segment; spread: 2^16 buckets, half
-    the frames denied.  GPU == restatement, both paths."""
-    rng = np.random.default_rng(77 if case == "spread" else 78)
+    bucket whose budget ends in a late segment; spread: 2^16 buckets, random
+    budgets, half the frames denied (few boundary frames per segment: the
+    fused kernel ranks them in its LDS hash table); bunched: every bucket's
+    budget 128 of its ~256 frames, so the boundaries crowd into the middle
+    segments (more candidates than the hash table takes there: the ordered
+    walk; the hash table elsewhere) -- bench.py's keys_denying.  GPU ==
+    restatement, both paths."""
+    rng = np.random.default_rng({"spread": 77, "whole_segment": 78, "bunched": 79}[case])
     n, hs = 1 << 24, 1 << 16
     k = rng.integers(0, hs, n).astype(np.int64)
     k[rng.random(n) < 0.02] = -1
@@ -305,8 +310,10 @@ def test_permit_keys_full_size(case, dev):
         tok = rng.integers(0, 400, hs).astype(np.uint32)
         tok[5] = 30000
         tok[9] = 4_000_000
-    else:
+    elif case == "spread":
         tok = rng.integers(0, 256, hs).astype(np.uint32)
+    else:
+        tok = np.full(hs, 128, np.uint32)
     v_want, t_want = _np_permit(k, hs, tok)
     assert (v_want == 0).sum() > 1000 and (v_want == 1).sum() > 1000
     ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})

@@ -10,10 +10,12 @@ sys.path.insert(0, ROOT)
 
 def stamps():
     """The fused rate limiter's phase timestamps (every workgroup, 100 MHz
-    clock, PermitFused::stamps: 11 x 256 words after the 2 KB of barrier
+    clock, PermitFused::stamps: 12 x 256 words after the 2 KB of barrier
     words and 256 B of flags at the start of the scratch) on 16 M dense keys,
     2^16 buckets, as bench's keys / keys_denying runs: microseconds from the
-    earliest workgroup start, min / median / max over the 256 workgroups."""
+    earliest workgroup start, min / median / max over the 256 workgroups;
+    rows 9-11 are phase-3 durations of wave 0 (ordered walk: list building /
+    walk; hash tables: partition / ranking / passes)."""
     import numpy as np
     import torch
     from pptk_amd.rx import RxContext
@@ -24,7 +26,7 @@ def stamps():
     scratch = torch.zeros(ctx._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8, device=dev)
     labels = ["start", "histogram", "row written", "barrier 1", "phase 2", "barrier 2", "verdicts",
               "codes staged", "boundaries found"]
-    off = 2048 + 256
+    off, nrow = 2048 + 256, 12
     out = {}
     for name, t in (("keys", 1 << 20), ("keys_denying", 128)):
         runs = []
@@ -32,22 +34,19 @@ def stamps():
             tok = torch.full((hs,), t, dtype=torch.int32, device=dev)
             ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
             torch.cuda.synchronize()
-            w = scratch[off:off + len(labels) * nblk * 4].view(torch.int32).cpu().numpy()
-            st = w.view(np.uint32).astype(np.int64).reshape(len(labels), nblk)
-            runs.append((st - st[0].min()) / 100.0)
-        r = runs[len(runs) // 2]
-        # durations (ticks) of wave 0's list building and walk, phase 3
-        dur = scratch[off + len(labels) * nblk * 4:off + (len(labels) + 2) * nblk * 4]
-        dur = dur.view(torch.int32).cpu().numpy().view(np.uint32).reshape(2, nblk) / 100.0
-        hb = int(np.argmax(r[8] - r[7])) if name == "keys_denying" else 0
-        out[name + "_phase3_heaviest"] = {"block": hb, "list_us": float(dur[0, hb]),
-                                          "walk_us": float(dur[1, hb]),
-                                          "median_list_us": float(np.median(dur[0])),
-                                          "median_walk_us": float(np.median(dur[1]))}
+            w = scratch[off:off + nrow * nblk * 4].view(torch.int32).cpu().numpy()
+            runs.append(w.view(np.uint32).astype(np.int64).reshape(nrow, nblk))
+        st = runs[len(runs) // 2]
+        t0 = st[0].min()
+        r = (st - t0) / 100.0
         out[name] = {lab: [round(float(r[k].min()), 2), round(float(np.median(r[k])), 2),
                            round(float(r[k].max()), 2)] for k, lab in enumerate(labels)}
         out[name]["slowest_phase1_blocks"] = [int(x) for x in np.argsort(r[2] - r[0])[-8:]]
         out[name]["slowest_phase2_blocks"] = [int(x) for x in np.argsort(r[4] - r[3])[-8:]]
+        hb = int(np.argmax(r[8] - r[7])) if name == "keys_denying" else 0
+        out[name + "_phase3_heaviest"] = {"block": hb, "part_or_list_us": st[9, hb] / 100.0,
+                                          "rank_or_walk_us": st[10, hb] / 100.0,
+                                          "hash_passes": int(st[11, hb])}
     out["unit"] = "us from the earliest workgroup start: [min, median, max] over workgroups"
     print(json.dumps(out), flush=True)
 
