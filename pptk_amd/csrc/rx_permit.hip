@@ -488,31 +488,47 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
 }
 
 // Grid barrier k (1, 2) of the launch with nonce N: every wave's stores
-// complete, workgroup c publishes N + k in arrive[c], and wave 0 polls all
-// nblk words (sc1, bounded) until each holds N + k or later.  Nothing needs
-// zeroing between launches: a word left by another launch (or garbage) never
-// matches this launch's nonce, so there is no memset before each launch.
-__device__ __forceinline__ void fused_barrier(const PermitFused &f, uint32_t c, uint64_t k) {
+// complete, workgroup c publishes N + k (+ 1 with `flag`, at k = 2) in
+// arrive[c], and wave 0 polls all nblk words (sc1, bounded) until each holds
+// N + k or later.  Nothing needs zeroing between launches: a word left by
+// another launch (or garbage) never matches this launch's nonce, so there is
+// no memset before each launch.  Returns whether some workgroup raised its
+// flag -- phase 2's "a bucket ran out", carried by the arrival words rather
+// than by one word every workgroup would store to (write-through stores to
+// one address are served one after another: 10 us for 256 of them).
+__device__ __forceinline__ bool fused_barrier(const PermitFused &f, uint32_t c, uint64_t k,
+                                              bool flag = false) {
+  __shared__ uint32_t any_flag;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < 64) {
-    if (threadIdx.x == 0) st_sc1(f.arrive + c, f.nonce + k);
+    if (threadIdx.x == 0) st_sc1(f.arrive + c, f.nonce + k + (flag ? 1u : 0u));
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-      bool ok = true;
+      bool ok = true, fl = false;
       for (uint32_t i = threadIdx.x; i < f.nblk; i += 64) {
         const uint64_t x = ld_sc1(f.arrive + i);
         ok = ok && (x & ~3ull) == f.nonce && (x & 3ull) >= k;
+        fl = fl || (x & 3ull) == 3ull;
       }
-      if (__all(ok)) break;
+      if (__all(ok)) {
+        if (threadIdx.x == 0) any_flag = 0;
+        __builtin_amdgcn_wave_barrier();
+        if (__any(fl) && threadIdx.x == 0) any_flag = 1;
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > FUSED_SPIN_TICKS) {
-        if (threadIdx.x == 0) st_sc1(f.out + 1, f.nonce | 1u);
+        if (threadIdx.x == 0) {
+          st_sc1(f.out + 1, f.nonce | 1u);
+          any_flag = 1;   // (timed out: take the full path)
+        }
         break;
       }
     }
   }
   __syncthreads();
+  return any_flag != 0;
 }
 
 // Subject keys of frames i .. i + 3 of the segment [.., hi).
@@ -554,6 +570,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   __shared__ uint32_t wsum[FT / 64 + 1];
   // phase 2: c* found and tokens per (word lane, bucket)
   __shared__ __attribute__((aligned(16))) uint32_t p23[512];
+  __shared__ uint32_t out_l;   // phase 2: some bucket of this workgroup ran out
   const uint32_t c = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const uint64_t lo = (uint64_t)c * f.seg;
@@ -749,7 +766,6 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     // some bucket of this workgroup's words ran out: one flag store per
     // workgroup, not one per word (thousands of write-through stores to one
     // address, all waited for by the barrier)
-    __shared__ uint32_t out_l;
     if (tid == 0) out_l = 0;
     uint32_t *const cst = p23;          // c* found per (word lane, bucket)
     uint32_t *const tokl = p23 + 256;   // the tokens before the batch
@@ -830,18 +846,35 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         const uint32_t pq = q == 0 ? p[0] : q == 1 ? p[1] : q == 2 ? p[2] : p[3];
         if (on && b < a.hash_size && tq > t && t > 0 && prq < t && t <= prq + pq) {
           uint32_t cum = prq;
-          for (uint32_t j = 0; j < rs; ++j) {
-            uint32_t x = 0;
+          if (((sat >> q) & 0x1111111111111111ull) == 0) {
+            // no saturated entry in this bucket's rows: the sixteen rows
+            // unrolled, no select chain, no early exit (rows past the slice
+            // are 0 and cannot cross t again)
+            uint32_t jf = 0xffffffffu, nd = 0;
 #pragma unroll
-            for (int jj = 0; jj < 16; ++jj) x = (uint32_t)jj == j ? rowv[jj] : x;
-            x = (x >> (8 * q)) & 0xffu;
-            if (x == 255u) x = fused_ovf(f, s * rs + j, b);
-            if (cum + x >= t) {
-              st_sc1(f.need + b, t - cum);
-              cst[wl * 4 + q] = s * rs + j;
-              break;
+            for (int j = 0; j < 16; ++j) {
+              const uint32_t x = (rowv[j] >> (8 * q)) & 0xffu;
+              const bool hit = jf == 0xffffffffu && cum + x >= t;
+              nd = hit ? t - cum : nd;
+              jf = hit ? (uint32_t)j : jf;
+              cum += x;
             }
-            cum += x;
+            st_sc1(f.need + b, nd);
+            cst[wl * 4 + q] = s * rs + jf;
+          } else {
+            for (uint32_t j = 0; j < rs; ++j) {
+              uint32_t x = 0;
+#pragma unroll
+              for (int jj = 0; jj < 16; ++jj) x = (uint32_t)jj == j ? rowv[jj] : x;
+              x = (x >> (8 * q)) & 0xffu;
+              if (x == 255u) x = fused_ovf(f, s * rs + j, b);
+              if (cum + x >= t) {
+                st_sc1(f.need + b, t - cum);
+                cst[wl * 4 + q] = s * rs + j;
+                break;
+              }
+              cum += x;
+            }
           }
         }
       }
@@ -867,21 +900,15 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #ifndef PPTK_PERMIT_SPEC_EARLY
     put_spec();
 #endif
-    __syncthreads();
-    if (tid == 0 && out_l) st_sc1(f.out, f.nonce);
   }
   FSTAMP(4);
-  fused_barrier(f, c, 2);
+  __syncthreads();
+  const bool any_out = fused_barrier(f, c, 2, out_l != 0);
   FSTAMP(5);
   // no bucket ran out: the speculative verdicts stand
-  {
-    __shared__ uint32_t any_out;
-    if (tid == 0) any_out = ld_sc1(f.out) == f.nonce;
-    __syncthreads();
-    if (!any_out) {
-      FSTAMP(6);
-      return;
-    }
+  if (!any_out) {
+    FSTAMP(6);
+    return;
   }
 
   // ---- phase 3: code table in LDS, the boundary ranks, the verdicts --------
