@@ -466,7 +466,7 @@ struct PermitFused {
   uint32_t *need;    // hash_size
   uint32_t *code;    // ceil(hash_size / 2) words of u16 pairs
   uint64_t *arrive;  // FMAXBLK: workgroup c's barrier generation (nonce + k)
-  uint64_t *out;     // [0] = nonce: some bucket ran out of tokens; [1] status
+  uint64_t *out;     // [1] = nonce | 1: a barrier timed out (status; [0] unused)
   uint32_t *stamps;  // FSTAMPS x FMAXBLK phase timestamps (tools/permit_run.py)
   uint64_t nonce;    // this launch's, low two bits clear (never 0 or ~0)
   uint32_t nblk, seg, nwords;
@@ -725,9 +725,10 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     if (tid == 0) st_sc1(f.novf + c, novf_l);
   }
   // Speculative verdicts: as if no bucket ran out of tokens (the common
-  // case: every subject permitted), written as phase 2 starts (they drain
-  // beside its table loads; phase 1 ends without waiting for them).  Phase 2 flags out[0] if some bucket does run out;
-  // only then does phase 3 write the verdicts that differ.
+  // case: every subject permitted), written at the end of phase 2 (they
+  // drain into the second barrier; phase 1 ends without waiting for them).
+  // A workgroup whose buckets do run out raises its flag in that barrier's
+  // arrival word; only then does phase 3 write the verdicts that differ.
   const bool valigned = ((uintptr_t)a.verdict & 3u) == 0;
   uint8_t *const vbase = a.verdict + lo;
   const uint32_t nrel = (uint32_t)(hi - lo);
