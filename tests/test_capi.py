@@ -147,7 +147,8 @@ def test_bench_and_tools_compile():
     interpreter rejects what the local parser might let through)."""
     import py_compile
     for f in ("bench.py", "__graft_entry__.py", "tools/ab.py", "tools/e2e.py",
-              "tools/membench.py", "tools/synth.py", "tools/pmc_summary.py"):
+              "tools/membench.py", "tools/synth.py", "tools/pmc_summary.py",
+              "tools/permit_run.py", "tools/permit_pmc.py"):
         py_compile.compile(os.path.join(ROOT, f), doraise=True)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],
                          capture_output=True, text=True, timeout=120)
@@ -559,3 +560,23 @@ def test_host_sources_under_sanitizers(tmp_path):
                              timeout=120, env=env)
         assert out.returncode == 0, out.stdout + out.stderr[-4000:]
         assert "host_fuzz ok" in out.stdout
+
+
+def test_permit_pmc_summary(tmp_path):
+    """tools/permit_pmc.py: per-kernel medians of rocprofv3 counter CSVs,
+    FETCH_SIZE doubled (KiB -> MB), the call's total."""
+    import csv
+    sys.path.insert(0, ROOT)
+    from tools import permit_pmc
+    for cname, vals in (("FETCH_SIZE", [1000.0, 1200.0, 1100.0]), ("WRITE_SIZE", [500.0] * 3)):
+        d = tmp_path / f"pmc_keys_{cname}"
+        d.mkdir()
+        with open(d / "run_counter_collection.csv", "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+            for i, v in enumerate(vals):
+                w.writerow([i, "void pptk::(anonymous namespace)::permit_fused<true>(x)", cname, v / 2])
+                w.writerow([i, "void pptk::(anonymous namespace)::permit_fused<true>(x)", cname, v / 2])
+                w.writerow([i, "rx_kernel", cname, 99999.0])
+    fe = permit_pmc.per_kernel(str(tmp_path / "pmc_keys_FETCH_SIZE"), "FETCH_SIZE")
+    assert list(fe) == ["permit_fused"] and abs(fe["permit_fused"] - 1100 * 1024 / 1e6) < 1e-9

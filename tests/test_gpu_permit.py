@@ -325,6 +325,41 @@ def test_permit_keys_full_size(case, dev):
     assert np.array_equal(tokt.cpu().numpy().view(np.uint32), t_want)
 
 
+def test_permit_keys_hash_class_overflow_falls_back(dev):
+    """The fused kernel's hash-table ranking takes a segment's candidates in
+    bucket-class passes of at most 2 048; a class over that (3 000
+    candidates, every one of a bucket in class 0 of two passes: the same
+    multiplicative hash as rx_permit.hip's cls) must fall back to the
+    ordered walk with the same verdicts.  The first segment holds three
+    frames each of 1 000 such buckets (one token each: the first frame
+    permitted, the others denied; at 1 M frames a segment is 4 096 frames),
+    the rest is non-subject filler; later segments hold random keys."""
+    rng = np.random.default_rng(81)
+    n, hs = 1 << 20, 1 << 16
+    b = np.arange(hs, dtype=np.uint64)
+    cls2 = (((((b * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)) >> np.uint64(8)) & np.uint64(0xFFFF))
+            * np.uint64(2)) >> np.uint64(16)
+    S = np.nonzero(cls2 == 0)[0][:1000].astype(np.int64)
+    k = rng.integers(0, hs, n).astype(np.int64)
+    sl = n // 256                                  # the fused kernel's segment at this n
+    seg = np.full(sl, -1, np.int64)
+    seg[rng.permutation(sl)[:3000]] = np.repeat(S, 3)[rng.permutation(3000)]
+    k[:sl] = seg
+    rest = k[sl:]
+    rest[np.isin(rest, S)] = -1                    # S's frames only in the first segment
+    tok = np.full(hs, 1 << 20, np.uint32)
+    tok[S] = 1
+    v_want, t_want = _np_permit(k, hs, tok)
+    assert (v_want[:sl] == 0).sum() == 2000 and (v_want[:sl] == 1).sum() == 1000
+    ctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+    keys = torch.from_numpy(np.where(k >= 0, k, 0xFFFFFFFF).astype(np.uint32).view(np.int32)).to(dev)
+    tokt = torch.from_numpy(tok.view(np.int32).copy()).to(dev)
+    v = ctx.permit_keys_device(keys, 4, tokt)
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), v_want)
+    assert np.array_equal(tokt.cpu().numpy().view(np.uint32), t_want)
+
+
 def test_permit_keys_out_of_range_are_not_subjects(dev):
     """Caller-made keys whose bucket is >= iphash_size are not subjects:
     verdict 2, no token touched (they used to index past the tables)."""
