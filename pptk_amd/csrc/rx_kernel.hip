@@ -484,6 +484,22 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int c = s * T + j;
+#ifdef PPTK_RX_TAIL_TEMPORAL
+    // (experiment) the last 8 chunks of the window -- a full-window frame's
+    // last line, which the next frame's first chunk shares -- with a
+    // temporal load, so that line stays in L2 for the next round instead of
+    // being fetched again after the non-temporal load dropped it; the other
+    // lanes of each of the two loads re-read a neighbour's chunk (coalesced)
+    if (NT && s == S - 1 && T >= 8) {
+      const bool tl = j >= T - 8;
+      const int cn = tl ? (S - 1) * T + (T - 9) : c;    // NT instruction: tail lanes -> lane T-9's chunk
+      const int ct = tl ? c : (S - 1) * T + (T - 8);    // temporal one: other lanes -> lane T-8's chunk
+      const u32x4 a = ldc<true>(c0 + min(cn, clast));
+      const u32x4 t = c0[min(ct, clast)];
+      b.v[s] = tl ? t : a;
+      continue;
+    }
+#endif
     b.v[s] = ldc<NT>(c0 + min(c, clast));   // bytes past the frame are masked at use
   }
   return b;
