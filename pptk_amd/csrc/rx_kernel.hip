@@ -484,12 +484,14 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int c = s * T + j;
-#ifdef PPTK_RX_TAIL_TEMPORAL
-    // (experiment) the last 8 chunks of the window -- a full-window frame's
-    // last line, which the next frame's first chunk shares -- with a
-    // temporal load, so that line stays in L2 for the next round instead of
-    // being fetched again after the non-temporal load dropped it; the other
-    // lanes of each of the two loads re-read a neighbour's chunk (coalesced)
+    // Non-temporal streaming: the last 8 chunks of the window -- a
+    // full-window frame's last line, which the next frame's first chunk
+    // shares -- with a temporal load, so that line stays in L2 for the next
+    // round instead of being fetched again after the non-temporal load let it
+    // go (C1500: 201.2 M -> 197.0 M 128-byte reads per launch, the SOL
+    // kernel's 196.6 M; 4.092 -> 4.042 ms, profiles/r04/c1500_tail/); the
+    // other lanes of each of the two loads re-read a neighbour's chunk
+    // (coalesced in the instruction: no extra traffic)
     if (NT && s == S - 1 && T >= 8) {
       const bool tl = j >= T - 8;
       const int cn = tl ? (S - 1) * T + (T - 9) : c;    // NT instruction: tail lanes -> lane T-9's chunk
@@ -499,7 +501,6 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
       b.v[s] = tl ? t : a;
       continue;
     }
-#endif
     b.v[s] = ldc<NT>(c0 + min(c, clast));   // bytes past the frame are masked at use
   }
   return b;
