@@ -427,10 +427,11 @@ int pptk_rx_last_variant(const struct pptk_rx_ctx *ctx);
 
 /* Autotuning: run the batch (records are written, as by
  * pptk_rx_batch_device) with the automatic kernel variant and the shapes
- * interchangeable with it -- reps timed launches each after two warm-ups --
- * and let later device batches of the same automatic variant and layout
- * (fixed-stride or offset-described) use the fastest (another shape must
- * beat the automatic one by 1 % to replace it).  The best shape
+ * interchangeable with it -- two warm-up rounds, then reps timed rounds of
+ * one launch per shape, interleaved so that clock drift falls on all alike
+ * -- and let later device batches of the same automatic variant and layout
+ * (fixed-stride or offset-described) use the fastest median (another shape
+ * must beat the automatic one by 1 % to replace it).  The best shape
  * depends on how expensive the record writes are (which follows where the
  * record buffer sits, see pptk_rx_place_records) and, for
  * offset-described batches, on the length mix (the candidates include the

@@ -491,30 +491,35 @@ int pptk_rx_autotune(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b, i
     return -EIO;
   }
   const hipStream_t s = (hipStream_t)stream;
-  int best = base;
-  float best_ms = 1e30f;
-  for (int k = 0; k < nc && rc == 0; ++k) {
-    std::vector<float> ms;
-    for (int r = 0; r < reps + 2 && rc == 0; ++r) {   // 2 untimed warm-ups
+  // Candidates interleaved round by round (two untimed warm-up rounds), so
+  // that clock and thermal drift during the probe fall on all of them alike;
+  // the fastest median wins, but a shape other than the automatic one must
+  // beat it by 1 % (noise never moves the choice away from candidate 0).
+  std::vector<std::vector<float>> ms((size_t)nc);
+  for (int r = 0; r < reps + 2 && rc == 0; ++r) {
+    for (int k = 0; k < nc && rc == 0; ++k) {
       if (hipEventRecord(e0, s) != hipSuccess) rc = -EIO;
       if (rc == 0) rc = launch_batch(c, b, cand[k], stream);
       if (rc == 0 && (hipEventRecord(e1, s) != hipSuccess ||
                       hipEventSynchronize(e1) != hipSuccess))
         rc = -EIO;
       float t = 0.f;
-      if (rc == 0 && r >= 2 && hipEventElapsedTime(&t, e0, e1) == hipSuccess) ms.push_back(t);
+      if (rc == 0 && r >= 2 && hipEventElapsedTime(&t, e0, e1) == hipSuccess)
+        ms[(size_t)k].push_back(t);
     }
-    if (rc == 0 && !ms.empty()) {
-      std::sort(ms.begin(), ms.end());
-      // another shape must beat the best so far by 1 %: a noise-level
-      // difference never moves the choice away from the automatic variant
-      // (candidate 0)
-      const float med = ms[ms.size() / 2];
-      if (k == 0 || med < 0.99f * best_ms) {
-        best_ms = med;
-        best = cand[k];
-      }
+  }
+  int best = base;
+  if (rc == 0 && !ms[0].empty()) {
+    std::vector<float> med((size_t)nc, 1e30f);
+    for (int k = 0; k < nc; ++k) {
+      if (ms[(size_t)k].empty()) continue;
+      std::sort(ms[(size_t)k].begin(), ms[(size_t)k].end());
+      med[(size_t)k] = ms[(size_t)k][ms[(size_t)k].size() / 2];
     }
+    int kb = 0;
+    for (int k = 1; k < nc; ++k)
+      if (med[(size_t)k] < med[(size_t)kb]) kb = k;
+    if (kb != 0 && med[(size_t)kb] < 0.99f * med[0]) best = cand[kb];
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
