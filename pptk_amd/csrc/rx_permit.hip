@@ -458,6 +458,10 @@ constexpr uint32_t FHASH_PASS = 2048;     // phase 3: candidates per hash-table 
 constexpr uint32_t FHASH_MAXP = 32;       // hash-table passes at most
 constexpr uint32_t FHASH_K = 64;          // frames of one ranked bucket at most, hash path
 constexpr uint64_t FUSED_SPIN_TICKS = 200000000ull;   // 2 s of the 100 MHz clock
+#ifndef PPTK_PERMIT_CODE_REPL
+#define PPTK_PERMIT_CODE_REPL 1
+#endif
+constexpr uint32_t FCREPL = PPTK_PERMIT_CODE_REPL;   // copies of the code array (A/B)
 
 struct PermitFused {
   uint32_t *table;   // nblk rows x nwords u32 (4 u8 counts each)
@@ -889,8 +893,11 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
           cd[q] = tot[q] <= t ? CODE_ALL : t == 0 ? CODE_NONE : cst[wl * 4 + q];
           if (b < a.hash_size) a.tokens[b] = t > tot[q] ? t - tot[q] : 0u;
         }
-        if (2 * w < words) st_sc1(f.code + 2 * w, cd[0] | cd[1] << 16);
-        if (2 * w + 1 < words) st_sc1(f.code + 2 * w + 1, cd[2] | cd[3] << 16);
+        for (uint32_t r = 0; r < FCREPL; ++r) {
+          uint32_t *const cr = f.code + r * ((words + 63u) & ~63u);
+          if (2 * w < words) st_sc1(cr + 2 * w, cd[0] | cd[1] << 16);
+          if (2 * w + 1 < words) st_sc1(cr + 2 * w + 1, cd[2] | cd[3] << 16);
+        }
         if ((cd[0] & cd[1] & cd[2] & cd[3]) != CODE_ALL) out_l = 1u;
       }
       __syncthreads();
@@ -920,18 +927,25 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   uint16_t *const tab16s = (uint16_t *)tab;
   constexpr int SW = HMAX / 2 / FT;   // code words per thread (at most)
   uint32_t cw[SW];                    // all loads in flight at once
+#ifdef PPTK_PERMIT_CODE_ROT
+  const uint32_t crot = (c >> 3) & (SW - 1);
+#else
+  const uint32_t crot = 0;
+#endif
+  auto wof = [&](int j) { return (((uint32_t)j + crot) & (SW - 1)) * FT + tid; };
+  const uint32_t *const code_r = f.code + (c % FCREPL) * ((words + 63u) & ~63u);
 #pragma unroll
   for (int j = 0; j < SW; ++j) {
-    const uint32_t w = tid + j * FT;
-    cw[j] = w < words ? ld_sc1(f.code + w) : 0u;
+    const uint32_t w = wof(j);
+    cw[j] = w < words ? ld_sc1(code_r + w) : 0u;
   }
   // the codes into LDS; this segment's c* buckets (bit 2 j + h) get, in a
   // second pass, the rank to find
   uint64_t cs = 0;
 #pragma unroll
   for (int j = 0; j < SW; ++j) {
-    const uint32_t w = tid + j * FT;
-    if (w >= words) break;
+    const uint32_t w = wof(j);
+    if (w >= words) continue;
     const uint32_t x = cw[j];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -972,7 +986,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             if (!((cs >> (2 * j + h)) & 1ull)) continue;
-            if (pos >= ch && pos < ch + CH) list[pos - ch] = 2 * (tid + (uint32_t)j * FT) + (uint32_t)h;
+            if (pos >= ch && pos < ch + CH) list[pos - ch] = 2 * wof(j) + (uint32_t)h;
             ++pos;
           }
         }
@@ -1070,6 +1084,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       uint32_t *const ent = rbit;       // the pass's candidates, compacted (no longer needed as rbit)
       auto off_at = [&](int v, int u) { return (uint32_t)v * FT * 4 + 4 * tid + (uint32_t)u; };
       uint64_t t_part = 0, t_rank = 0, t0 = 0;   // (diagnostics: wave 0's time)
+      uint64_t left = cm;   // candidates of the passes still to come
 #pragma unroll 1
       for (uint32_t pass = 0; pass < npass; ++pass) {
         if (tid == 0) t0 = __builtin_amdgcn_s_memrealtime();
@@ -1082,14 +1097,20 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         // order does not matter here: ranks come from the offsets), so each
         // thread then handles at most two entries -- a wave runs two probe
         // loops, not one per round and lane that holds a candidate
+        // (the last pass takes what is left: no class sweep)
         uint64_t pm = 0;
+        if (pass + 1 == npass) {
+          pm = left;
+        } else {
 #pragma unroll
-        for (int v = 0; v < FKV; ++v) {
-          if (((cm >> (4 * v)) & 15ull) == 0) continue;
+          for (int v = 0; v < FKV; ++v) {
+            if (((left >> (4 * v)) & 15ull) == 0) continue;
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (((cm >> (4 * v + u)) & 1ull) && cls(FKEY(v, u)) == pass) pm |= 1ull << (4 * v + u);
+            for (int u = 0; u < 4; ++u)
+              if (((left >> (4 * v + u)) & 1ull) && cls(FKEY(v, u)) == pass) pm |= 1ull << (4 * v + u);
+          }
         }
+        left &= ~pm;
         const uint32_t pc = (uint32_t)__popcll(pm);
         uint32_t inc = pc;
 #pragma unroll
@@ -1241,7 +1262,9 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   const bool aligned = valigned;
 #pragma unroll
   for (int v = 0; v < FKV; ++v) {
+#ifndef PPTK_PERMIT_VERDICT_FREE
     __builtin_amdgcn_sched_barrier(0);
+#endif
     const uint32_t rel = (uint32_t)v * FT * 4 + 4 * tid;
     if (rel >= nrel) break;
     uint32_t vd[4];
@@ -1497,7 +1520,7 @@ void fused_layout(uint32_t nblk, uint32_t seg, uint32_t hash_size, void *base, P
   f.ovf = take((size_t)nblk * FOVF * 8);
   f.novf = take((size_t)nblk * 4);
   f.need = take((size_t)hash_size * 4);
-  f.code = take((size_t)((hash_size + 1) / 2) * 4);
+  f.code = take((size_t)FCREPL * ((((hash_size + 1) / 2) + 63) & ~63u) * 4);
   total = off;
 }
 
