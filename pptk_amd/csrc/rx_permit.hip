@@ -1063,7 +1063,11 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     bool hashed = !many && npass <= FHASH_MAXP;
     auto hash1 = [](uint32_t b) { return b * 0x9E3779B1u; };
     auto cls = [&](uint32_t b) { return (((hash1(b) >> 8) & 0xffffu) * npass) >> 16; };   // (no division)
-    if (hashed) {
+    // (one pass holds every candidate: no class can overflow; else the
+    // counting sweep also picks pass 0's candidates)
+    uint64_t pm0 = cm;
+    if (hashed && npass > 1) {
+      pm0 = 0;
       for (uint32_t i = tid; i < npass; i += FT) ccnt[i] = 0;
       __syncthreads();
 #pragma unroll
@@ -1071,7 +1075,11 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         if (((cm >> (4 * v)) & 15ull) == 0) continue;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if ((cm >> (4 * v + u)) & 1ull) atomicAdd(&ccnt[cls(FKEY(v, u))], 1u);
+          if ((cm >> (4 * v + u)) & 1ull) {
+            const uint32_t k = cls(FKEY(v, u));
+            atomicAdd(&ccnt[k], 1u);
+            if (k == 0) pm0 |= 1ull << (4 * v + u);
+          }
       }
       __syncthreads();
       bool over = false;
@@ -1097,10 +1105,13 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         // order does not matter here: ranks come from the offsets), so each
         // thread then handles at most two entries -- a wave runs two probe
         // loops, not one per round and lane that holds a candidate
-        // (the last pass takes what is left: no class sweep)
+        // (the last pass takes what is left, pass 0 what the counting sweep
+        // found: no class sweep of their own)
         uint64_t pm = 0;
         if (pass + 1 == npass) {
           pm = left;
+        } else if (pass == 0) {
+          pm = pm0;
         } else {
 #pragma unroll
           for (int v = 0; v < FKV; ++v) {
