@@ -950,11 +950,15 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (2 * w + h < a.hash_size && ((x >> (16 * h)) & 0xffffu) == c) cs |= 1ull << (2 * j + h);
-    tab[w] = x;
+    // in LDS, the verdict of every frame of the bucket here (1: T_b falls
+    // in a later segment, or CODE_ALL; 0: an earlier one, or CODE_NONE); a
+    // c* bucket's entry is rewritten below
+    const uint32_t lo16 = x & 0xffffu, hi16 = x >> 16;
+    tab[w] = (lo16 != CODE_NONE && c < lo16 ? 1u : 0u) | (hi16 != CODE_NONE && c < hi16 ? 1u : 0u) << 16;
   }
   // The rank to find, as a u16.  The T_b-th frame being b's last frame here
   // (its count in this segment's row) means every frame of b here is
-  // permitted: CODE_ALL, no ranking -- with few frames per bucket and
+  // permitted: verdict 1, no ranking -- with few frames per bucket and
   // segment the common case.  The segment's c* buckets are compacted into
   // the list (4 096 at a time) and spread evenly over the threads, so a
   // segment that is c* for thousands of buckets costs one round trip of
@@ -1007,7 +1011,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         const uint32_t b = list[tid + (uint32_t)k * FT];
         uint32_t kb = (rw[k] >> (8 * (b & 3u))) & 0xffu;
         if (kb == 255u) kb = fused_ovf(f, c, b);
-        uint32_t e = CODE_ALL;
+        uint32_t e = 1u;   // (every frame here permitted)
         if (nd[k] < kb) {
           atomicOr(&rbit[b >> 5], 1u << (b & 31));
           e = nd[k];
@@ -1287,8 +1291,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       } else if ((cm >> (4 * v + u)) & 1ull) {   // up to its T_b-th frame
         vd[u] = rel + u <= tabh(kk) ? 1u : 0u;
       } else {
-        const uint32_t cd = tabh(kk);
-        vd[u] = cd == CODE_ALL ? 1u : cd == CODE_NONE ? 0u : c < cd ? 1u : 0u;
+        vd[u] = tabh(kk);
       }
     }
     // (only the words that differ from the speculative ones)
