@@ -983,17 +983,12 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #pragma unroll 1
     for (uint32_t ch = 0; ch < tcs; ch += CH) {
       __syncthreads();   // (the previous chunk's list reads are done)
-      if (cs) {
-        uint32_t pos = base;
-#pragma unroll
-        for (int j = 0; j < SW; ++j) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            if (!((cs >> (2 * j + h)) & 1ull)) continue;
-            if (pos >= ch && pos < ch + CH) list[pos - ch] = 2 * wof(j) + (uint32_t)h;
-            ++pos;
-          }
-        }
+      // (over the set bits only, in bit order: a few per thread)
+      uint32_t pos = base;
+      for (uint64_t m = cs; m; m &= m - 1) {
+        const uint32_t bit = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+        if (pos >= ch && pos < ch + CH) list[pos - ch] = 2 * wof((int)(bit >> 1)) + (bit & 1u);
+        ++pos;
       }
       __syncthreads();
       const uint32_t nch = min(CH, tcs - ch);
