@@ -922,6 +922,7 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   // ---- phase 3: code table in LDS, the boundary ranks, the verdicts --------
   const uint32_t rbw = (a.hash_size + 31) / 32;
   for (uint32_t w = tid; w < rbw; w += FT) rbit[w] = 0;
+  if (tid < FHASH_MAXP) p23[128 + tid] = 0;   // (fine class counts, below)
   __syncthreads();
   bool mine = false, many = false;
   uint16_t *const tab16s = (uint16_t *)tab;
@@ -1031,12 +1032,22 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   uint64_t cm = 0;
   if (mine) {
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    // Candidates, counted by fine class (the top 5 bits of a 16-bit bucket
+    // hash: FHASH_MAXP classes); pmh = those of the lower 16 fine classes
+    auto hash1 = [](uint32_t b) { return b * 0x9E3779B1u; };
+    uint32_t *const fcnt = p23 + 128;
+    uint64_t pmh = 0;
 #pragma unroll
     for (int v = 0; v < FKV; ++v) {
       __builtin_amdgcn_sched_barrier(0);   // (else all 64 LDS lookups are hoisted)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (FSUBJ(v, u) && isc(FKEY(v, u))) cm |= 1ull << (4 * v + u);
+        if (FSUBJ(v, u) && isc(FKEY(v, u))) {
+          const uint32_t fc = (hash1(FKEY(v, u)) >> 8 & 0xffffu) >> 11;
+          atomicAdd(&fcnt[fc], 1u);
+          cm |= 1ull << (4 * v + u);
+          if (fc < FHASH_MAXP / 2) pmh |= 1ull << (4 * v + u);
+        }
     }
     // the segment's candidate count
     uint32_t ncand = (uint32_t)__popcll(cm);
@@ -1057,32 +1068,22 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
     // probe sequence (its rank, in frame order), and the one whose rank + 1
     // is the bucket's rank to find is the boundary frame.  More classes than
     // FHASH_MAXP, or a class over FHASH_PASS: the ordered walk below.
-    const uint32_t npass = max(1u, (ncand + FHASH_PASS * 3 / 4 - 1) / (FHASH_PASS * 3 / 4));
-    uint32_t *const ccnt = p23 + 128;   // per-class candidate counts (p23[0..127]: occupancy)
+    // The pass count is a power of two, so a pass is a run of fine classes
+    // (pass = fine class >> (5 - log2 npass)) and its size is known from
+    // the fine counts without another sweep; with two passes pmh is pass 0.
+    const uint32_t npr = max(1u, (ncand + FHASH_PASS * 3 / 4 - 1) / (FHASH_PASS * 3 / 4));
+    uint32_t npass = 1;
+    while (npass < npr && npass <= FHASH_MAXP) npass <<= 1;
     bool hashed = !many && npass <= FHASH_MAXP;
-    auto hash1 = [](uint32_t b) { return b * 0x9E3779B1u; };
     auto cls = [&](uint32_t b) { return (((hash1(b) >> 8) & 0xffffu) * npass) >> 16; };   // (no division)
-    // (one pass holds every candidate: no class can overflow; else the
-    // counting sweep also picks pass 0's candidates)
-    uint64_t pm0 = cm;
     if (hashed && npass > 1) {
-      pm0 = 0;
-      for (uint32_t i = tid; i < npass; i += FT) ccnt[i] = 0;
-      __syncthreads();
-#pragma unroll
-      for (int v = 0; v < FKV; ++v) {
-        if (((cm >> (4 * v)) & 15ull) == 0) continue;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if ((cm >> (4 * v + u)) & 1ull) {
-            const uint32_t k = cls(FKEY(v, u));
-            atomicAdd(&ccnt[k], 1u);
-            if (k == 0) pm0 |= 1ull << (4 * v + u);
-          }
-      }
-      __syncthreads();
+      const uint32_t per = FHASH_MAXP / npass;
       bool over = false;
-      for (uint32_t i = 0; i < npass; ++i) over = over || ccnt[i] > FHASH_PASS;
+      for (uint32_t p = 0; p < npass; ++p) {
+        uint32_t n = 0;
+        for (uint32_t i = 0; i < per; ++i) n += fcnt[p * per + i];
+        over = over || n > FHASH_PASS;
+      }
       hashed = !over;
     }
     if (hashed) {
@@ -1104,13 +1105,13 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
         // order does not matter here: ranks come from the offsets), so each
         // thread then handles at most two entries -- a wave runs two probe
         // loops, not one per round and lane that holds a candidate
-        // (the last pass takes what is left, pass 0 what the counting sweep
-        // found: no class sweep of their own)
+        // (the last pass takes what is left, and of two passes the first is
+        // pmh: no class sweep of their own)
         uint64_t pm = 0;
         if (pass + 1 == npass) {
           pm = left;
-        } else if (pass == 0) {
-          pm = pm0;
+        } else if (pass == 0 && npass == 2) {
+          pm = pmh;
         } else {
 #pragma unroll
           for (int v = 0; v < FKV; ++v) {
