@@ -33,6 +33,25 @@ $(LIB): $(HIP_OBJS) $(C_OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# The test library: the product with its fault-injection knobs compiled in
+# (-DPPTK_RX_TEST_HOOKS: a rate-limiter workgroup held past its barrier
+# deadline, a stalled communicator warm-up).  Only the failure-path tests load
+# it; the product library never reads those knobs.
+HOOKS_LIB := tests/hooks/libpptkrx_hooks.so
+HOOKS_SRCS := pptk_amd/csrc/rx_permit.hip pptk_amd/csrc/rx_comm.hip
+HOOKS_OBJS := $(patsubst pptk_amd/csrc/%.hip,$(OBJDIR)/hooks/%.o,$(HOOKS_SRCS))
+
+$(OBJDIR)/hooks/%.o: pptk_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DPPTK_RX_TEST_HOOKS -c $< -o $@
+
+$(HOOKS_LIB): $(filter-out $(OBJDIR)/rx_permit.o $(OBJDIR)/rx_comm.o,$(HIP_OBJS)) $(HOOKS_OBJS) $(C_OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl
+
+hooks: $(HOOKS_LIB)
+all: $(HOOKS_LIB)
+
 # A/B builds of the product library with extra defines, e.g.
 #   make abvariant NAME=full DEFS=-DPPTK_RX_FULL_UNROLL
 abvariant:

@@ -245,62 +245,24 @@ def ring_buffers(ctx, b, n, dev, compact):
     return ring.recs, report
 
 
-def placed_gather(ctx, b, recs, kw, n_total, ws, rank, dev, ncand=8, steps=4):
-    """The two gather buffers, placed.  The all-gather lands (ws - 1) shards
-    of hashes in this GPU's HBM while the next batch streams its frames, and
-    the kernel writes its own hashes there: what those writes cost depends
-    on where the buffer sits, as for the records (one GPU: 4.62 vs 5.19 ms
-    per C1500 batch with 940 MB of gather writes beside it, and 4.20 vs 4.72
-    ms for the kernel's own 128 MB of hashes).  The two
-    double-buffered gather buffers are the two halves of one placed region
-    (placements come in runs of several GB, so both halves share the
-    region's class).  Per candidate region (allocated 4 GB apart): batches
-    with their hashes into each half's own slice in turn, and beside each a
-    device copy of the bytes the gather would land into the rest of that
-    half; the fastest region is kept.  Rank-local (no collective).
-    Returns ([GatherBuffer, GatherBuffer], report)."""
-    import torch
+def placed_gather(ctx, b, recs, kw, n_total, ws, rank, dev):
+    """The two gather buffers, placed by the library (pptk_rx_gather_alloc,
+    include/pptk_rx.h): the all-gather lands (ws - 1) shards of hashes in
+    this GPU's HBM while the next batch streams its frames, and the kernel
+    writes its own hashes into its slice; what those writes cost depends on
+    where the buffer sits, as for the records.  The
+    library probes candidate regions with this batch and a device copy of
+    the bytes the gather would land beside each launch, and keeps the
+    fastest -- the same call a C application makes (examples/rx_multigpu.c).
+    Rank-local (no collective).  Returns ([GatherBuffer, GatherBuffer],
+    report)."""
     from pptk_amd.shard import GatherBuffer, shard_range
     first, count, per = shard_range(n_total, ws, rank)
-    nb = ws * per * 8
-    free, _ = torch.cuda.mem_get_info(dev)
-    while ncand > 1 and ncand * (2 * nb + (4 << 30)) > 0.5 * free:
-        ncand -= 1
-    hold = []
-    cands = _spaced(dev, ncand, 2 * nb, 4 << 30, hold)
-    lo, hi = rank * per * 8, (rank + 1) * per * 8
-    src = torch.zeros(max(lo, nb - hi, 1), dtype=torch.uint8, device=dev)
-    main = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev)
-    ms = []
-    for c in cands:
-        halves = [c[:nb], c[nb:]]
-        for k in range(steps + 2):
-            if k == 2:
-                torch.cuda.synchronize(dev)
-                t0 = time.perf_counter()
-            h = halves[k & 1]
-            ctx.batch_device(b["frames"], count, recs=recs,
-                             hash_out=h[lo:hi].view(torch.int64)[:count], **kw)
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                if lo:
-                    h[:lo].copy_(src[:lo])
-                if nb > hi:
-                    h[hi:].copy_(src[:nb - hi])
-        torch.cuda.synchronize(dev)
-        ms.append(round((time.perf_counter() - t0) / steps * 1e3, 4))
-    best = min(range(ncand), key=lambda i: ms[i])
-    gbs = [GatherBuffer(n_total, ws, rank, dev, out=cands[best][k * nb:(k + 1) * nb])
-           for k in range(2)]
-    for g in gbs:
-        g.out.zero_()
-    del hold, cands, src
-    freed, at = release(dev)
-    return gbs, {"candidates": ncand, "candidate_ms": ms, "chosen": best,
-                 "freed_bytes": freed, "_freed_at": at}
+    g = ctx.gather_alloc(b["frames"], count, per, ws, rank, recs=recs, **kw)
+    gbs = [GatherBuffer(n_total, ws, rank, dev, out=g.out[k]) for k in range(2)]
+    rep = dict(g.report)
+    rep["_freed_at"] = time.perf_counter()
+    return gbs, rep
 
 
 def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SETTLE_S,
@@ -515,6 +477,109 @@ def validate_line(line):
     if not isinstance(prk, list) or len(prk) != ws:
         bad.append("per_rank_kernel_ms does not list every rank")
     return bad
+
+
+LINE_MAX_CHARS = 4000     # the stdout line must fit the driver's stored tail whole
+
+
+def _cfg_entry(sec):
+    """One config's entry of the compact line."""
+    if not sec:
+        return None
+    r = sec.get("roofline") or {}
+    e = {"mpkts": sec.get("value"), "kernel_ms": sec.get("kernel_ms"), "frac": r.get("frac"),
+         "variant": sec.get("kernel_variant")}
+    if r.get("traffic"):
+        e["traffic"] = r["traffic"]
+    if r.get("mix_sol_frac"):
+        e["sol_frac"] = r["mix_sol_frac"]
+    o = sec.get("oracle_sample")
+    if o:
+        e["oracle_mismatches"] = o.get("mismatches")
+    fb = sec.get("full_batch_check")
+    if fb:
+        e["verdicts_ok"] = bool(fb.get("parsed") and fb.get("ip_verdicts") and fb.get("l4_verdicts"))
+    return e
+
+
+def compact_line(full, detail_path=None):
+    """The printed JSON line: the contract keys, the primary roofline and
+    CPU baseline, and one compact entry per BASELINE config (C1500, C64,
+    CMIX with M6 beside it, IMIX, JMIX; compact-record runs), the end-to-end
+    rates, the batch ops and, with N > 1, the all-gather -- every number the
+    driver should keep, under LINE_MAX_CHARS so the stored stdout tail holds
+    it whole.  Everything else (placement reports, box probes, workloads) is
+    in the full result at `detail_path` and on stderr."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
+    line = {k: full.get(k) for k in keep}
+    c = full.get("config") or {}
+    line["config"] = {k: c.get(k) for k in ("workload", "frames_per_gpu", "global_frames",
+                                             "parallelism", "rccl_ranks")}
+    r = full.get("roofline") or {}
+    line["roofline"] = {k: r.get(k) for k in (
+        "bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms", "kernel_variant",
+        "algorithmic_bytes_per_launch", "frac_plain_alloc", "mix_sol_frac") if k in r}
+    src = r.get("traffic_source") or ""
+    line["roofline"]["traffic_source"] = "live rocprofv3 PMC" if src.startswith("live") else src
+    cpu = full.get("cpu_baseline")
+    if cpu:
+        line["cpu_baseline"] = {k: cpu.get(k) for k in ("value", "unit", "cores", "kind",
+                                                        "single_thread_mpkts", "cpu_model")}
+        line["cpu_baseline"]["sample"] = "1 M distinct C1500 frames, full path (reference functions)"
+    cfgs = {}
+    cfgs[(c.get("workload") or "c1500").split(":")[0].lower()] = _cfg_entry(
+        {"value": full.get("value"), "kernel_ms": r.get("kernel_ms"),
+         "kernel_variant": r.get("kernel_variant"), "roofline": r,
+         "oracle_sample": (full.get("parity") or {}).get("oracle_sample"),
+         "full_batch_check": (full.get("parity") or {}).get("full_batch")})
+    if full.get("rec32"):
+        cfgs["c1500_rec32"] = _cfg_entry(full["rec32"])
+    for name, sec in (full.get("secondary") or {}).items():
+        cfgs[name] = _cfg_entry(sec)
+        if sec.get("rec32"):
+            cfgs[name + "_rec32"] = _cfg_entry(sec["rec32"])
+        if sec.get("m6"):
+            cfgs[name]["m6_ms"] = sec["m6"]["kernel_ms"]
+            cfgs[name]["m6_frac"] = sec["m6"]["frac"]
+        if sec.get("binned"):
+            cfgs[name]["mixed_call_ms"] = sec["binned"].get("ms_per_batch")
+            cfgs[name]["binned"] = sec["binned"].get("binned_by_plan")
+    line["configs"] = cfgs
+    e2e = full.get("e2e")
+    if e2e:
+        line["e2e"] = ({k: ({kk: v.get(kk) for kk in ("mpkts", "path", "frame_gbs", "of_pcie")}
+                            if isinstance(v, dict) else v)
+                        for k, v in e2e.items() if k != "gather_threads"})
+    ops = {}
+    pm = full.get("permit") or {}
+    for key, sub in (("permit_records_ms", pm), ("permit_keys_ms", pm.get("keys")),
+                     ("permit_keys_denying_ms", pm.get("keys_denying"))):
+        if sub and sub.get("ms_per_batch") is not None:
+            ops[key] = sub["ms_per_batch"]
+    for key, sub in (("tx_ms", full.get("tx")), ("rewrite_ms", full.get("rewrite")),
+                     ("mss_clamp_ms", full.get("mss_clamp"))):
+        if sub:
+            ops[key] = sub.get("kernel_ms")
+    if ops:
+        line["ops"] = ops
+    gat = full.get("allgather")
+    if gat:
+        g = {k: gat.get(k) for k in ("ms", "algbw_gbs", "busbw_gbs", "overlap_loss", "rccl_ranks",
+                                      "bytes_per_rank")}
+        chk = gat.get("gathered_check") or {}
+        g["gathered_check"] = {k: chk.get(k) for k in ("own_slice_equals_records",
+                                                        "sampled_frames_per_rank",
+                                                        "sampled_mismatches")}
+        bp = gat.get("buffer_placement") or {}
+        g["placement"] = {k: bp.get(k) for k in ("alloc", "candidates", "chosen", "chosen_ms",
+                                                  "first_ms")}
+        line["allgather"] = g
+        line["value_no_gather"] = full.get("value_no_gather")
+    line["per_rank_kernel_ms"] = full.get("per_rank_kernel_ms")
+    if detail_path:
+        line["detail"] = detail_path
+    return line
 
 
 def mix_sol(b, recs, n):
@@ -960,6 +1025,115 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
     return out
 
 
+def pcie_ceiling(dev, mb=96, reps=20):
+    """The host-to-device copy ceiling the end-to-end path is bound by:
+    pinned hipMemcpyAsync of mb MB, GB/s (tools/pcie_probe.py's h2d row)."""
+    import torch
+    h = torch.empty(mb << 20, dtype=torch.uint8).pin_memory()
+    d = torch.empty(mb << 20, dtype=torch.uint8, device=dev)
+    d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    return round((mb << 20) * reps / (time.perf_counter() - t0) / 1e9, 2)
+
+
+def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", 1 << 20, False), ("c64", 1 << 22, True))):
+    """End to end, host to host (the north star's "rate
+    including pinned hipMemcpyAsync to and from the GPU"): pptk_rx_batch on
+    borrowed ldp_packet frames in host memory (reference rx loop
+    ldp/ldprecv.c:60-70: frames in a netmap ring, ldp/ldpnetmap.c:163-185),
+    records back in host memory, synchronous, chunks of 65 536 frames
+    pipelined over four streams.  Two paths per config: "staged" (host
+    threads gather the frames into pinned staging, DMA down) and "ring" (the
+    frame area registered once with pptk_rx_register_ring: dense chunks go
+    down as one DMA span, nothing gathered); with `reg` the record array is
+    registered too (records written in place over PCIe, no copy back).
+    Every mode is checked bit-exact against a device-resident launch of the
+    same frames before it is timed.  Reported: the faster path, Mpkt/s,
+    frame GB/s and its fraction of this box's pinned H2D copy rate."""
+    import torch
+    from pptk_amd.records import REC_DTYPE, diff_records
+    from pptk_amd.rx import RxContext, ldp_packets
+    from tools.synth import make_batch
+    threads, _ = _cpu_topology()
+    gt = max(1, min(8, threads))
+    ceil = pcie_ceiling(dev)
+    out = {"pcie_h2d_gbs": ceil, "gather_threads": gt}
+    for cfg, n, reg in cfgs:
+        b = make_batch(cfg, n, dev)
+        stride, flen = b["stride"], b["fixed_len"]
+        ring = b["frames"][: n * stride + 64].cpu().numpy()      # the host "ring"
+        ctx = RxContext(0, KEY, max_batch=65536, max_frame=1518, gather_threads=gt)
+        ref = ctx.batch_device(b["frames"], n, stride=stride, fixed_len=flen)
+        want = ref.cpu().numpy()
+        del b, ref
+        pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
+                           np.full(n, flen, np.uint16))
+        outbuf = np.zeros(n, dtype=REC_DTYPE)           # reused, as an rx loop's array
+        if reg:
+            ctx.register_ring(outbuf)
+        res = {}
+        for mode in ("staged", "ring"):
+            if mode == "ring":
+                ctx.register_ring(ring)
+            got = ctx.batch_host(pkts, out=outbuf)
+            if diff_records(got, want):
+                raise RuntimeError(f"e2e {cfg} {mode}: records differ from the device batch")
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < seconds:
+                ctx.batch_host(pkts, out=outbuf)
+                reps += 1
+            el = (time.perf_counter() - t0) / reps
+            res[mode] = round(n / el / 1e6, 2)
+            if mode == "ring":
+                ctx.unregister_ring(ring)
+        if reg:
+            ctx.unregister_ring(outbuf)
+        ctx.close()
+        best = max(res, key=res.get)
+        gbs = res[best] * flen / 1e3
+        out[cfg] = {"mpkts": res[best], "path": best, "frame_gbs": round(gbs, 2),
+                    "of_pcie": round(gbs / ceil, 3) if ceil else None, "frames": n,
+                    "records": "registered" if reg else "copied", "staged_mpkts": res["staged"],
+                    "ring_mpkts": res["ring"]}
+        del ring, pkts, outbuf, want
+        torch.cuda.empty_cache()
+    return out
+
+
+def forced_ms(ctx, b, recs, n, variant, steps, warmup=3):
+    """Median kernel ms of this batch with the kernel variant forced (e.g.
+    CMIX through M6, the kernel that bins each tile's lanes by length --
+    BASELINE.json configs[3]'s "lanes binned by length" -- beside the
+    autotuned choice); records unchanged (checked), the forcing undone."""
+    import torch
+    from pptk_amd.rx import VARIANTS
+    kw = (dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]) if "off" in b
+          else dict(stride=b["stride"], fixed_len=b["fixed_len"]))
+    want = recs.clone()
+    ctx.set_tuning(VARIANTS.index(variant), -1)
+    try:
+        for _ in range(warmup):
+            ctx.batch_device(b["frames"], n, recs=recs, **kw)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        for a, z in ev:
+            a.record()
+            ctx.batch_device(b["frames"], n, recs=recs, **kw)
+            z.record()
+        torch.cuda.synchronize()
+        assert VARIANTS[ctx.last_variant()] == variant
+    finally:
+        ctx.set_tuning(-1, -1)
+    same = bool(torch.equal(recs, want))
+    del want
+    return round(float(np.median([a.elapsed_time(z) for a, z in ev])), 4), same
+
+
 def gather_bench(ctx, gb, ws, dev, steps):
     """The all-gather of `per` u64 flow hashes per rank alone
     (pptk_rx_allgather_hash): time and bandwidths."""
@@ -1078,6 +1252,11 @@ def main():
                     help="seconds of untimed launches before the warmup steps")
     ap.add_argument("--no-place", action="store_true",
                     help="one record buffer as allocated, no placement probe")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host-to-host (pptk_rx_batch) measurement")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where the full result (every sub-measurement) is written; the "
+                         "stdout line is its compact summary")
     ap.add_argument("--no-live-pmc", action="store_true",
                     help="no same-run rocprofv3 FETCH_SIZE/WRITE_SIZE passes (roofline.traffic "
                          "then comes from the committed summary)")
@@ -1212,6 +1391,13 @@ def main():
             if cfg in ("cmix", "imix", "jmix"):
                 secondary[cfg]["binned"] = binned_bench(ctx, r["_batch"], n, dev, args.steps,
                                                         args.warmup, recs=r["_recs"])
+            if cfg == "cmix" and r["variant"] != "M6":
+                # configs[3] as written, "lanes binned by length": the kernel
+                # that bins each tile's lanes (M6), beside the autotuned shape
+                ms, same = forced_ms(ctx, r["_batch"], r["_recs"], n, "M6", args.steps)
+                secondary[cfg]["m6"] = {"kernel_ms": ms, "same_records": same,
+                                        "frac": round(r["bytes"] / (ms * 1e-3) / 1e9
+                                                      / HBM_PEAK_GBS, 4)}
             if cfg == "c64" and not args.no_rec32:
                 r32 = run_config(cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, None,
                                  check, args.settle, compact=True, batch=r["_batch"], first=first,
@@ -1235,6 +1421,15 @@ def main():
             rewrite = rewrite_bench(ctx, n, dev, rank, args.steps, args.warmup)
             log(f"[rank {rank}] rewrite: {rewrite}")
 
+    # end to end, host to host (rank 0 of a one-GPU run)
+    e2e = None
+    if rank == 0 and ws == 1 and not args.no_secondary and args.only is None and not args.no_e2e:
+        try:
+            e2e = e2e_bench(dev)
+        except Exception as e:          # reported, never fatal to the device-resident line
+            e2e = {"error": f"{type(e).__name__}: {e}"[:200]}
+        log(f"e2e: {e2e}")
+
     # roofline.traffic from this run: rocprofv3 PMC passes over the same
     # workload and kernel shape, in child processes (rank 0 of a one-GPU
     # run; the committed summary is the fallback)
@@ -1257,7 +1452,7 @@ def main():
             log(f"live pmc {cfg}: {t} {info}")
 
     if rank == 0:
-        line = {
+        full = {
             "metric": METRIC,
             "value": round(prim["mpkts"], 1),
             "unit": "Mpkts/s",
@@ -1290,10 +1485,20 @@ def main():
             "tx": tx,
             "rewrite": rewrite,
             "mss_clamp": mss,
+            "e2e": e2e,
         }
+        line = compact_line(full, detail_path=args.detail)
         problems = validate_line(line)
         if problems:
             line["line_problems"] = problems
+        try:
+            if os.path.dirname(args.detail):
+                os.makedirs(os.path.dirname(args.detail), exist_ok=True)
+            with open(args.detail, "w") as f:
+                json.dump(full, f)
+        except OSError as e:
+            log(f"detail not written: {e}")
+        log("full result: " + json.dumps(full))
         print(json.dumps(line), flush=True)
         if problems and dist_on(ws):
             raise SystemExit(f"multi-GPU line failed its checks: {problems}")

@@ -6,11 +6,16 @@
  * BASELINE.json, single-process form; bench.py runs the one-process-per-GPU
  * form).
  *
- * Each thread, like an ldp/ldprecvmt.c:16-67 queue thread: copies its shard
- * of the frame set to its GPU, runs pptk_rx_batch_device with d_hash aimed
- * at its own slice of the gather buffer, then pptk_rx_allgather_hash in
- * place on the same stream, and checks its records and the whole gathered
- * hash array against the expected records of the set file.
+ * Each thread, like an ldp/ldprecvmt.c:16-67 queue thread: takes its device
+ * frame and record rings from pptk_rx_ring_alloc and its two gather buffers
+ * from pptk_rx_gather_alloc (both placed by the library's probe: what the
+ * record, hash and gather writes cost beside the frame stream depends on
+ * where the buffers sit, DESIGN.md sections 7-8; each rank prints the
+ * placement it got), copies its shard of the frame set into the frame ring,
+ * runs pptk_rx_batch_device with d_hash aimed at its own slice of gather
+ * buffer r % 2, then pptk_rx_allgather_hash in place on the same stream, and
+ * checks its records and the whole gathered hash array against the expected
+ * records of the set file.
  *
  * Failure containment.  The reference's queue threads share nothing
  * (ldp/ldprecvmt.c:174-182), so one failing thread cannot stall the others;
@@ -109,13 +114,19 @@ static void *thrfn(void *arg)
   const struct rxq_set *s = t->set;
   const uint64_t n = s->h.n;
   uint64_t first, count, per;
-  uint8_t *d_frames = NULL;
   uint64_t *d_off = NULL, *d_out = NULL, *h_off = NULL, *h_out = NULL;
   uint16_t *d_len = NULL;
-  struct pptk_rx_rec *d_recs = NULL, *h_recs = NULL;
+  struct pptk_rx_rec *h_recs = NULL;
   hipStream_t st = NULL;
   uint64_t lo = 0, hi = 0;
   struct pptk_rx_dev_batch b;
+  struct pptk_rx_ring ring;
+  struct pptk_rx_ring_spec rs;
+  struct pptk_rx_gather gat;
+  struct pptk_rx_gather_spec gs;
+
+  memset(&ring, 0, sizeof(ring));
+  memset(&gat, 0, sizeof(gat));
 
   if (g_join_threads) {   /* collective: every rank's thread joins */
     if (t->rank == g_fail_rank) {
@@ -141,12 +152,16 @@ static void *thrfn(void *arg)
   }
   CHECK_HIP(hipSetDevice(t->device));
   CHECK_HIP(hipStreamCreate(&st));
-  CHECK_HIP(hipMalloc((void **)&d_frames, hi - lo + 64));
+  /* the frame and record rings of this queue, placed by the library */
+  memset(&rs, 0, sizeof(rs));
+  rs.frame_bytes = hi - lo + 64;
+  rs.nrec = count ? count : 1;
+  rs.rec_bytes = sizeof(struct pptk_rx_rec);
+  rs.probe_len = rs.frame_bytes >= 1500 ? 0 : (uint32_t)rs.frame_bytes;
+  if ((t->rc = pptk_rx_ring_alloc(t->ctx, &rs, &ring, st)) != 0)
+    goto out;
   CHECK_HIP(hipMalloc((void **)&d_off, count * 8 + 8));
   CHECK_HIP(hipMalloc((void **)&d_len, count * 2 + 2));
-  CHECK_HIP(hipMalloc((void **)&d_recs, count * sizeof(struct pptk_rx_rec) + 64));
-  CHECK_HIP(hipMalloc((void **)&d_out, per * (uint64_t)t->nranks * 8 + 8));
-  CHECK_HIP(hipMemset(d_out, 0, per * (uint64_t)t->nranks * 8 + 8));
   h_off = malloc(count * 8 + 8);
   h_out = malloc(per * (uint64_t)t->nranks * 8 + 8);
   h_recs = malloc(count * sizeof(struct pptk_rx_rec) + 64);
@@ -156,7 +171,7 @@ static void *thrfn(void *arg)
   }
   for (uint64_t i = 0; i < count; i++)
     h_off[i] = s->off[first + i] - lo;
-  CHECK_HIP(hipMemcpy(d_frames, s->buf + lo, hi - lo + 16, hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(ring.d_frames, s->buf + lo, hi - lo + 16, hipMemcpyHostToDevice));
   CHECK_HIP(hipMemcpy(d_off, h_off, count * 8, hipMemcpyHostToDevice));
   CHECK_HIP(hipMemcpy(d_len, s->len + first, count * 2, hipMemcpyHostToDevice));
   if (!g_join_threads && t->rank == g_fail_rank) {
@@ -165,14 +180,26 @@ static void *thrfn(void *arg)
   }
 
   memset(&b, 0, sizeof(b));
-  b.d_frames = d_frames;
+  b.d_frames = ring.d_frames;
   b.d_off = d_off;
   b.d_len = d_len;
   b.max_len = 65535;
   b.n = count;
-  b.d_recs = d_recs;
-  b.d_hash = d_out + (uint64_t)t->rank * per;   /* this rank's slice: gather in place */
+  b.d_recs = ring.d_recs;
+  /* the two gather buffers, placed by the library with this batch */
+  memset(&gs, 0, sizeof(gs));
+  gs.per_rank = per;
+  gs.nranks = t->nranks;
+  gs.rank = t->rank;
+  if ((t->rc = pptk_rx_gather_alloc(t->ctx, &b, &gs, &gat, st)) != 0)
+    goto out;
+  printf("rank %d: rings placed: pair (%d, %d) of %u x %u candidates, probe %.4f ms "
+         "(plain allocation %.4f ms); gather region %d of %u, probe %.4f ms (plain %.4f ms)\n",
+         t->rank, ring.chosen_frames, ring.chosen_recs, ring.frame_cands, ring.rec_cands,
+         ring.chosen_ms, ring.first_ms, gat.chosen, gat.cands, gat.chosen_ms, gat.first_ms);
   for (int r = 0; r < t->rounds && t->rc == 0; r++) {
+    d_out = gat.d_out[r & 1];   /* double-buffered, as an rx loop overlapping gathers does */
+    b.d_hash = d_out + (uint64_t)t->rank * per;   /* this rank's slice: gather in place */
     if ((t->rc = pptk_rx_batch_device(t->ctx, &b, st)) != 0)
       break;
     if ((t->rc = pptk_rx_allgather_hash(t->ctx, b.d_hash, per, d_out, st)) != 0)
@@ -182,7 +209,7 @@ static void *thrfn(void *arg)
   }
   if (t->rc)
     goto out;
-  CHECK_HIP(hipMemcpy(h_recs, d_recs, count * sizeof(struct pptk_rx_rec), hipMemcpyDeviceToHost));
+  CHECK_HIP(hipMemcpy(h_recs, ring.d_recs, count * sizeof(struct pptk_rx_rec), hipMemcpyDeviceToHost));
   CHECK_HIP(hipMemcpy(h_out, d_out, per * (uint64_t)t->nranks * 8, hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < count; i++)
     if (memcmp(&h_recs[i], &s->want[first + i], sizeof(h_recs[i])) != 0)
@@ -198,11 +225,10 @@ out:
     (void)pptk_rx_comm_sync(t->ctx, st, 0);
     (void)hipStreamDestroy(st);
   }
-  (void)hipFree(d_frames);
+  (void)pptk_rx_ring_free(&ring);
+  (void)pptk_rx_gather_free(&gat);
   (void)hipFree(d_off);
   (void)hipFree(d_len);
-  (void)hipFree(d_recs);
-  (void)hipFree(d_out);
   free(h_off);
   free(h_out);
   free(h_recs);

@@ -290,13 +290,27 @@ int pptk_rx_permit_device(struct pptk_rx_ctx *ctx, const struct pptk_rx_rec *d_r
  * subject (verdict 2, no token touched).  Up to 2^16 buckets and 16 M
  * frames (65 536 per CU) this runs as one persistent launch that reads the
  * keys once (DESIGN.md section 5 "Rate limiter"); beyond, or with
- * PPTK_RX_TUNE_PERMIT_PASSES set, as four launches.  The scratch needs no
- * initialisation; calls that share one scratch buffer must be ordered on
- * one stream (a call overlapping another on the same scratch gives wrong
- * verdicts, bounded by a 2 s spin, never a hang). */
+ * PPTK_RX_TUNE_PERMIT_PASSES set (pptk_rx_set_tuning, or the PPTK_RX_TUNE
+ * environment word), as four launches.  The persistent launch needs all its
+ * workgroups resident at once: the library orders every such launch of a
+ * device behind the previous one, whatever stream or context issued it, so
+ * concurrent calls never starve each other; calls that share one scratch
+ * buffer must still be ordered on one stream.  Should the workgroups not
+ * all become resident within 2 s (e.g. another process's kernels hold the
+ * CUs), the launch aborts: verdicts undefined, the token counts left as
+ * they were before the call (nothing half-updated), and
+ * pptk_rx_permit_status reports -ETIMEDOUT; never a hang.  The scratch
+ * needs no initialisation. */
 int pptk_rx_permit_keys_device(struct pptk_rx_ctx *ctx, const uint32_t *d_keys, uint64_t n,
                                int family, const uint8_t *d_subject, uint32_t *d_tokens,
                                uint8_t *d_verdict, void *d_scratch, void *stream);
+
+/* Whether every pptk_rx_permit_keys_device call on d_scratch since the last
+ * status query completed: 0, or -ETIMEDOUT if one aborted (its verdicts are
+ * undefined and its tokens unchanged: repeat it, e.g. with
+ * PPTK_RX_TUNE_PERMIT_PASSES).  Synchronises `stream` (the stream those
+ * calls ran on).  -EIO on a HIP error. */
+int pptk_rx_permit_status(struct pptk_rx_ctx *ctx, const void *d_scratch, void *stream);
 
 /* The token refill timer (batch_timer_fn, reference iphash/iphash.c:
  * 290-350) for buckets [start, end): tokens = min(tokens + add, initial).
@@ -408,7 +422,9 @@ int pptk_tcp_mss_clamp_device(struct pptk_rx_ctx *ctx, uint8_t *d_frames, const 
  * PPTK_RX_TUNE_SC1_STORES (write-through record stores),
  * PPTK_RX_TUNE_BLOCKED (each wavefront takes a contiguous block of tiles
  * instead of every nwaves-th tile), PPTK_RX_TUNE_PERMIT_PASSES (the rate
- * limiter's four-launch path instead of its fused one-launch path).
+ * limiter's four-launch path instead of its fused one-launch path; a flags
+ * word holding only this bit leaves the receive transform's memory policy
+ * automatic).
  * Variants and flags change speed only: results are identical for every
  * setting on every input.  Any other flag bit is rejected with -EINVAL
  * (PPTK_RX_TUNE in the environment is masked to these bits). */
@@ -590,7 +606,12 @@ int pptk_rx_place_records(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batc
  * frames over it.  Synchronous (uses `stream` for the probe).
  * frame_cands 1..8 (0 = 3), rec_cands 1..16 (0 = 8), reps 1..20 (0 = 3),
  * probe_len 64..1536 (0 = 1500); candidates beyond the first pair are
- * allocated only as far as 60 % of the free device memory.  Freeing the
+ * allocated only as far as budget_bytes (0: 60 % of the free device memory)
+ * allows.  Calls for one device run one at a time (several rx queues of a
+ * GPU, a context each, setting up their rings together: each probe runs
+ * alone and sizes its candidates from what the earlier calls kept; give
+ * each queue a budget so the first ones do not take the memory the later
+ * ones need for their candidates).  Freeing the
  * candidates not kept makes the driver scrub that memory in the background
  * (~20-30 GB/s; batches beside it run up to 9 % slower): with
  * PPTK_RX_RING_SETTLE the call sleeps until it is over (settle_ms), else
@@ -606,6 +627,9 @@ struct pptk_rx_ring_spec {
   uint32_t rec_cands;     /* 0 = 8 */
   uint32_t reps;          /* timed probe launches per pair, 0 = 3 */
   uint32_t flags;         /* PPTK_RX_RING_SETTLE */
+  uint64_t budget_bytes;  /* device memory the call may hold at once (candidates
+                             and spacers included), 0 = 60 % of the free memory */
+  uint64_t reserved;      /* 0 */
 };
 struct pptk_rx_ring {
   uint8_t *d_frames;      /* frame_bytes (+ 64 readable) */
@@ -630,6 +654,50 @@ int pptk_rx_ring_alloc(struct pptk_rx_ctx *ctx, const struct pptk_rx_ring_spec *
 /* Frees both rings (on ring->device; the context need not exist any more)
  * and zeroes *ring.  Every batch using them must have completed. */
 int pptk_rx_ring_free(struct pptk_rx_ring *ring);
+
+/* The multi-GPU gather buffers, placed by the library like the rings: the
+ * two (double-buffered) destinations of pptk_rx_allgather_hash for this
+ * rank, nranks * per_rank u64 each, zeroed.  Where they sit decides what the
+ * gather's writes -- the kernel's own hashes into the rank's slice and the
+ * (nranks - 1) shards the collective lands while the next batch streams --
+ * cost beside the frame stream.  Candidate regions
+ * (each holding both buffers) are allocated apart; on each, `b` (this
+ * rank's batch: frames, records, geometry; b->d_hash is replaced by each
+ * buffer's slice in turn) runs reps + 2 times with a device copy of the
+ * bytes the gather would land beside every launch on a second stream; the
+ * fastest region is kept, everything else freed.  Synchronous; uses
+ * `stream`.  Call after the rings are placed (the probe runs on them).
+ * cands 1..16 (0 = 8), reps 1..20 (0 = 4); candidates as far as
+ * budget_bytes (0: 50 % of the free memory) allows.  b->n <= per_rank.
+ * Release with pptk_rx_gather_free. */
+struct pptk_rx_gather_spec {
+  uint64_t per_rank;      /* hashes each rank gathers (pptk_rx_shard_range) */
+  int32_t nranks;
+  int32_t rank;
+  uint32_t cands;         /* candidate regions, 0 = 8 */
+  uint32_t reps;          /* timed probe batches per candidate, 0 = 4 */
+  uint32_t flags;         /* PPTK_RX_RING_SETTLE */
+  uint32_t reserved;      /* 0 */
+  uint64_t budget_bytes;  /* 0 = 50 % of the free memory */
+};
+struct pptk_rx_gather {
+  uint64_t *d_out[2];     /* the two gather buffers; rank r's slice of each
+                             starts at d_out[k] + r * per_rank */
+  uint64_t per_rank;
+  int32_t nranks;
+  int32_t rank;
+  int32_t device;
+  uint32_t cands;         /* candidate regions probed */
+  int32_t chosen;         /* the region kept */
+  float chosen_ms;        /* probe ms per batch on the region kept */
+  float first_ms;         /* ... on candidate 0: a plain allocation */
+  uint32_t settle_ms;
+  uint64_t freed_bytes;
+};
+int pptk_rx_gather_alloc(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *b,
+                         const struct pptk_rx_gather_spec *spec, struct pptk_rx_gather *gather,
+                         void *stream);
+int pptk_rx_gather_free(struct pptk_rx_gather *gather);
 
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);

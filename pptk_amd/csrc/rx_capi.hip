@@ -165,7 +165,8 @@ struct pptk_rx_ctx {
   int ncu = 256;
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
-  int forced_flags = -1;
+  int forced_flags = -1;   // the receive transform's memory policy, -1 automatic
+  bool permit_passes = false;   // PPTK_RX_TUNE_PERMIT_PASSES set by pptk_rx_set_tuning
   int last_variant = -1;
   // pptk_rx_autotune's choice per automatic variant, for fixed-stride [0]
   // and offset-described [1] batches (-1: the automatic variant itself)
@@ -343,10 +344,18 @@ static constexpr uint32_t kTuneMask = PPTK_RX_TUNE_NT_LOADS | PPTK_RX_TUNE_NO_ST
 // ms, CMIX 3.05 -> 2.97 ms); non-temporal frame loads only for fixed-stride
 // batches with the streaming variants (C1500 4.47 -> 4.25 ms; they cost 14 %
 // on C64 and 10 % on offset-described CMIX).  PPTK_RX_TUNE overrides.
-static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
+static long env_tune() {
   static const long tune = env_long("PPTK_RX_TUNE", -1);
-  if (c->forced_flags >= 0) return (uint32_t)c->forced_flags & kTuneMask;
-  if (tune >= 0) return (uint32_t)tune & kTuneMask;
+  return tune;
+}
+
+static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
+  constexpr uint32_t rx_bits = kTuneMask & ~(uint32_t)PPTK_RX_TUNE_PERMIT_PASSES;
+  if (c->forced_flags >= 0) return (uint32_t)c->forced_flags & rx_bits;
+  // (an environment word holding only the rate limiter's bit leaves the
+  // memory policy automatic, as pptk_rx_set_tuning does)
+  const long tune = env_tune();
+  if (tune >= 0 && ((uint32_t)tune & rx_bits)) return (uint32_t)tune & rx_bits;
   const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2 ||
                      variant == RX_L4;
   return (small || gather) ? PPTK_RX_TUNE_NT_STORES
@@ -859,7 +868,11 @@ int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
   if (!c || variant < -1 || variant >= RX_NVARIANTS || flags < -1) return -EINVAL;
   if (flags >= 0 && ((uint32_t)flags & ~kTuneMask)) return -EINVAL;
   c->forced_variant = variant;
-  c->forced_flags = flags;
+  // the rate limiter's bit is its own switch: flags that hold nothing else
+  // leave the receive transform's memory policy automatic
+  const int rx = flags < 0 ? -1 : flags & ~PPTK_RX_TUNE_PERMIT_PASSES;
+  c->forced_flags = flags >= 0 && rx == 0 && (flags & PPTK_RX_TUNE_PERMIT_PASSES) ? -1 : rx;
+  c->permit_passes = flags >= 0 && (flags & PPTK_RX_TUNE_PERMIT_PASSES);
   return 0;
 }
 
@@ -896,8 +909,16 @@ static int permit_common(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs
   a.hash_size = hs;
   a.family = family;
   a.ncu = c->ncu;
-  a.force_passes = c->forced_flags >= 0 && (c->forced_flags & PPTK_RX_TUNE_PERMIT_PASSES) ? 1 : 0;
+  a.force_passes =
+      c->permit_passes || (env_tune() >= 0 && (env_tune() & PPTK_RX_TUNE_PERMIT_PASSES)) ? 1 : 0;
   return hip_err(launch_permit(a, d_scratch, (hipStream_t)stream));
+}
+
+int pptk_rx_permit_status(struct pptk_rx_ctx *c, const void *d_scratch, void *stream) {
+  if (!c || !d_scratch) return -EINVAL;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
+  return permit_status(d_scratch, (hipStream_t)stream);
 }
 
 int pptk_rx_permit_device(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs,

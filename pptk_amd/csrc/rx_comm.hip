@@ -276,10 +276,16 @@ __global__ void warmup_stall_kernel(uint64_t ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+// Compiled in only by the test library (PPTK_RX_TEST_HOOKS,
+// tests/hooks/libpptkrx_hooks.so); the product library never reads it.
 uint32_t warmup_stall_ms() {
+#ifdef PPTK_RX_TEST_HOOKS
   const char *e = getenv("PPTK_RX_COMM_TEST_WARMUP_STALL_MS");
   const long v = e ? atol(e) : 0;
   return v <= 0 ? 0u : (uint32_t)std::min(v, 60000L);
+#else
+  return 0;
+#endif
 }
 
 void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,

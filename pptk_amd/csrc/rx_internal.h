@@ -188,6 +188,9 @@ struct PermitArgs {
 };
 size_t permit_scratch_bytes(uint64_t n, uint32_t hash_size);
 hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t s);
+// 0, or -ETIMEDOUT if a fused launch on this scratch since the last query
+// aborted (synchronises s); -EIO on a HIP error
+int permit_status(const void *scratch, hipStream_t s);
 hipError_t launch_refill(uint32_t *tokens, uint32_t start, uint32_t end, uint32_t add,
                          uint32_t initial, hipStream_t s);
 

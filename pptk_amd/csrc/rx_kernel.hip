@@ -51,6 +51,7 @@ constexpr int IMG_CHUNKS = 8;     // 16-byte chunks parked in LDS per frame
 constexpr int IMG_STRIDE = PPTK_RX_IMG_STRIDE;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // Explicit address spaces for every pointer the per-frame code dereferences:
 // a pointer the compiler cannot place becomes a FLAT access, which counts in
@@ -798,6 +799,13 @@ __device__ __forceinline__ bool lane_fast(const RxKArgs &a, const uint32_t d[16]
   return true;
 }
 
+// How the kernel writes the dense flow-hash array (A/B builds: 0 plain
+// per-lane stores, 1 non-temporal per-lane stores, 2 staged beside the
+// record and stored by flush_records as one run per tile).
+#ifndef PPTK_RX_HASH_MODE
+#define PPTK_RX_HASH_MODE 2
+#endif
+
 // Record of frame `idx`: the optional dense flow-hash word, then the record
 // (64 bytes, or the 32-byte compact projection) either parked in the lane's
 // LDS slot `st` for flush_records (batch order) or stored directly
@@ -805,8 +813,19 @@ __device__ __forceinline__ bool lane_fast(const RxKArgs &a, const uint32_t d[16]
 __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, uint32_t idx,
                                             LDS_AS u32x4 *st, bool stage) {
   const uint32_t *w = o.w;
-  if (a.hash)
-    a.hash[idx] = o.fh;
+  // The dense flow hash (the all-gather's send slice).  Beside the frame
+  // stream, where the memory charges writes by their burst (DESIGN.md 7
+  // "Placement"), it goes out like the records: non-temporal, and (batch
+  // order) parked in the record slot's spare 16 bytes and stored by the
+  // flush as one 512-byte run per tile next to the tile's records.
+  if (a.hash) {
+    if (PPTK_RX_HASH_MODE == 2 && stage && !a.perm)
+      *(LDS_AS uint64_t *)(st + 4) = o.fh;
+    else if (PPTK_RX_HASH_MODE >= 1 && (a.tune & 32u))
+      __builtin_nontemporal_store(o.fh, (GLB_AS uint64_t *)a.hash + idx);
+    else
+      a.hash[idx] = o.fh;
+  }
   if (a.key)   // rate-limiter key: src_bucket (word 14), IPv6 bit 31; ~0 unparsed
     a.key[idx] = !(o.flags & PPTK_RX_F_PARSED) ? 0xffffffffu
                  : (o.flags & PPTK_RX_F_IPV6)  ? (w[14] | 0x80000000u)
@@ -886,6 +905,26 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
         __builtin_nontemporal_store(val, d);
       } else {
         *d = val;
+      }
+    }
+  }
+  // the tile's flow hashes (parked in each record slot's spare 16 bytes):
+  // lanes 0..31 store two records' hashes each, one 512-byte run
+  if (PPTK_RX_HASH_MODE == 2 && a.hash && !scatter && lane < WAVE / 2) {
+    const uint32_t r0 = 2u * (uint32_t)lane;
+    if ((uint64_t)r0 < nrec) {
+      const uint64_t h0 = *(const LDS_AS uint64_t *)(st + r0 * 5 + 4);
+      GLB_AS uint64_t *hd = (GLB_AS uint64_t *)a.hash + tile * (uint64_t)WAVE + r0;
+      if ((uint64_t)r0 + 1 < nrec && ((uintptr_t)hd & 15u) == 0) {
+        const uint64_t h1 = *(const LDS_AS uint64_t *)(st + (r0 + 1) * 5 + 4);
+        const u64x2 v = {h0, h1};
+        if (a.tune & 32u)
+          __builtin_nontemporal_store(v, (GLB_AS u64x2 *)hd);
+        else
+          *(GLB_AS u64x2 *)hd = v;
+      } else {
+        hd[0] = h0;
+        if ((uint64_t)r0 + 1 < nrec) hd[1] = *(const LDS_AS uint64_t *)(st + (r0 + 1) * 5 + 4);
       }
     }
   }

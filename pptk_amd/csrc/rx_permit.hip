@@ -51,12 +51,17 @@
 //   V. verdicts in frame order from the dense keys and lim[].
 // 16 M frames, 2^16 buckets: the histogram table is 32 MB, the passes read
 // the keys twice -- no 64 MB x (2 passes x 3 arrays) radix sort.
+#include <errno.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <random>
+#include <unordered_map>
+#include <utility>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -444,9 +449,17 @@ __global__ __launch_bounds__(HT) void permit_verdicts_tab(PermitArgs a, const ui
 // one-workgroup-per-CU row): no L2 write-back fences.  Co-residency: the
 // grid is at most one workgroup per CU and each needs > 80 KB of LDS, so no
 // CU holds two; a workgroup not yet resident (a CU busy with another
-// stream's kernel) only delays the others.  Every spin is bounded
-// (FUSED_SPIN_TICKS): a barrier that times out marks a status word
-// (PermitFused::out[1]) instead of hanging the GPU.
+// stream's kernel) only delays the others.  Two fused launches on two
+// streams could each hold part of the CUs and wait for each other's; the
+// host orders every fused launch of a device behind the previous one
+// (launch_permit), so within a process that cannot happen.  Every spin is
+// still bounded (FUSED_SPIN_TICKS, e.g. another process's kernels holding
+// the CUs): a workgroup whose barrier times out ABORTS the launch -- it
+// publishes an abort word that every other workgroup's barrier also stops
+// at -- and marks the status word (PermitFused::out[1], read by
+// pptk_rx_permit_status).  The token counts are written only after the
+// second barrier has passed, so an aborted launch leaves the tokens as they
+// were (the caller repeats the call), never half-updated.
 constexpr int FT = 1024;                  // threads per workgroup
 constexpr int FKV = 16;                   // 16-byte key loads per thread (64 frames)
 constexpr int FKB = 4;                    // of them per batch (two batches in flight)
@@ -469,10 +482,14 @@ struct PermitFused {
   uint32_t *novf;    // nblk
   uint32_t *need;    // hash_size
   uint32_t *code;    // ceil(hash_size / 2) words of u16 pairs
-  uint64_t *arrive;  // FMAXBLK: workgroup c's barrier generation (nonce + k)
-  uint64_t *out;     // [1] = nonce | 1: a barrier timed out (status; [0] unused)
+  uint32_t *ntok;    // hash_size: the new token counts, until the commit
+  uint64_t *arrive;  // FMAXBLK: workgroup c's barrier generation (nonce + k, or nonce | 4: abort)
+  uint64_t *out;     // [1] = nonce | 1: the launch aborted (status; [0] unused)
   uint32_t *stamps;  // FSTAMPS x FMAXBLK phase timestamps (tools/permit_run.py)
-  uint64_t nonce;    // this launch's, low two bits clear (never 0 or ~0)
+  uint64_t nonce;    // this launch's, low three bits clear (never 0)
+  uint64_t spin_ticks;   // a barrier's bound (100 MHz ticks)
+  uint64_t stall_ticks;  // test builds: hold the last workgroup this long ...
+  uint32_t stall_at;     // ... before barrier stall_at (1, 2; 0 = never)
   uint32_t nblk, seg, nwords;
 };
 constexpr int FSTAMPS = 12;
@@ -496,43 +513,64 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
 // arrive[c], and wave 0 polls all nblk words (sc1, bounded) until each holds
 // N + k or later.  Nothing needs zeroing between launches: a word left by
 // another launch (or garbage) never matches this launch's nonce, so there is
-// no memset before each launch.  Returns whether some workgroup raised its
+// no memset before each launch.  Returns 1 if some workgroup raised its
 // flag -- phase 2's "a bucket ran out", carried by the arrival words rather
 // than by one word every workgroup would store to (write-through stores to
-// one address are served one after another: 10 us for 256 of them).
-__device__ __forceinline__ bool fused_barrier(const PermitFused &f, uint32_t c, uint64_t k,
-                                              bool flag = false) {
-  __shared__ uint32_t any_flag;
+// one address are served one after another: 10 us for 256 of them) -- else
+// 0; or -1: the launch aborted.  A workgroup whose wait exceeds
+// f.spin_ticks, or that sees another's abort word (N | 4), publishes its own
+// abort word and the status, and its caller returns at once: once any
+// workgroup has given up, every barrier still waiting ends in an abort, and
+// a workgroup that arrives later (it was not resident) sees the abort words.
+__device__ __forceinline__ int fused_barrier(const PermitFused &f, uint32_t c, uint64_t k,
+                                             bool flag = false) {
+  __shared__ int res;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < 64) {
     if (threadIdx.x == 0) st_sc1(f.arrive + c, f.nonce + k + (flag ? 1u : 0u));
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-      bool ok = true, fl = false;
+      bool ok = true, fl = false, ab = false;
       for (uint32_t i = threadIdx.x; i < f.nblk; i += 64) {
         const uint64_t x = ld_sc1(f.arrive + i);
-        ok = ok && (x & ~3ull) == f.nonce && (x & 3ull) >= k;
-        fl = fl || (x & 3ull) == 3ull;
+        const bool ours = (x & ~7ull) == f.nonce;
+        ok = ok && ours && (x & 3ull) >= k;
+        fl = fl || (ours && (x & 3ull) == 3ull);
+        ab = ab || (ours && (x & 4ull) != 0);
       }
-      if (__all(ok)) {
-        if (threadIdx.x == 0) any_flag = 0;
+      const bool give_up = __any(ab) || __builtin_amdgcn_s_memrealtime() - t0 > f.spin_ticks;
+      if (!give_up && __all(ok)) {
+        if (threadIdx.x == 0) res = 0;
         __builtin_amdgcn_wave_barrier();
-        if (__any(fl) && threadIdx.x == 0) any_flag = 1;
+        if (__any(fl) && threadIdx.x == 0) res = 1;
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > FUSED_SPIN_TICKS) {
+      if (give_up) {
         if (threadIdx.x == 0) {
+          st_sc1(f.arrive + c, f.nonce | 4u);
           st_sc1(f.out + 1, f.nonce | 1u);
-          any_flag = 1;   // (timed out: take the full path)
+          res = -1;
         }
         break;
       }
+      __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
-  return any_flag != 0;
+  return res;
+}
+
+// Test builds (PPTK_RX_TEST_HOOKS) hold the last workgroup before barrier
+// f.stall_at for f.stall_ticks, so that the others' barrier times out (the
+// fault-injection test of the abort path); a product build never sets it.
+__device__ __forceinline__ void fused_stall(const PermitFused &f, uint32_t c, uint32_t k) {
+  if (f.stall_ticks == 0 || f.stall_at != k || c + 1 != f.nblk) return;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < f.stall_ticks) __builtin_amdgcn_s_sleep(127);
+  }
+  __syncthreads();
 }
 
 // Subject keys of frames i .. i + 3 of the segment [.., hi).
@@ -760,24 +798,29 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
 #ifdef PPTK_PERMIT_SPEC_EARLY   // (A/B: the speculative verdicts before the table loads)
   put_spec();
 #endif
-  fused_barrier(f, c, 1);
+  fused_stall(f, c, 1);
+  if (fused_barrier(f, c, 1) < 0) return;   // aborted: nothing written but scratch
   FSTAMP(3);
 
   // ---- phase 2: per bucket down its column ---------------------------------
   // Workgroup c takes a range of table words (4 buckets each); its threads
   // are 64 word lanes x 16 row slices (up to 16 rows each, all loads in
   // flight), so a bucket's column is summed by 16 threads at once.
+  // The new token counts are committed only after the second barrier (an
+  // aborted launch leaves the tokens untouched): slice 0 parks those of its
+  // last word batch in LDS (tokl, no longer read), earlier batches (small
+  // batches: few segments, many words each) go through f.ntok.
   {
+    const uint32_t wpb = (f.nwords + f.nblk - 1) / f.nblk;
+    const uint32_t wlo = min(f.nwords, c * wpb), whi = min(f.nwords, wlo + wpb);
+    const uint32_t wl = tid & 63, s = tid >> 6;
     // some bucket of this workgroup's words ran out: one flag store per
     // workgroup, not one per word (thousands of write-through stores to one
     // address, all waited for by the barrier)
     if (tid == 0) out_l = 0;
     uint32_t *const cst = p23;          // c* found per (word lane, bucket)
     uint32_t *const tokl = p23 + 256;   // the tokens before the batch
-    const uint32_t wpb = (f.nwords + f.nblk - 1) / f.nblk;
-    const uint32_t wlo = min(f.nwords, c * wpb), whi = min(f.nwords, wlo + wpb);
     const uint32_t rs = (f.nblk + FSL - 1) / FSL;          // rows per slice (<= 16)
-    const uint32_t wl = tid & 63, s = tid >> 6;
     uint32_t *part = list;                                  // [FSL][64][4]
     for (uint32_t w0 = wlo; w0 < whi; w0 += 64) {
       const uint32_t w = w0 + wl;
@@ -885,13 +928,21 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       }
       __syncthreads();
       if (s == 0 && on) {   // code pairs and the new token counts
-        uint32_t cd[4];
+        uint32_t cd[4], ntk[4];
+        const bool last = w0 + 64 >= whi;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t b = 4 * w + q;
           const uint32_t t = tokl[wl * 4 + q];
           cd[q] = tot[q] <= t ? CODE_ALL : t == 0 ? CODE_NONE : cst[wl * 4 + q];
-          if (b < a.hash_size) a.tokens[b] = t > tot[q] ? t - tot[q] : 0u;
+          const uint32_t nt = t > tot[q] ? t - tot[q] : 0u;
+          if (!last && b < a.hash_size) st_sc1(f.ntok + b, nt);
+          ntk[q] = nt;
+        }
+        // (every read of tokl in this batch is behind the barrier above)
+        if (last) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tokl[wl * 4 + q] = ntk[q];
         }
         for (uint32_t r = 0; r < FCREPL; ++r) {
           uint32_t *const cr = f.code + r * ((words + 63u) & ~63u);
@@ -911,8 +962,26 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   }
   FSTAMP(4);
   __syncthreads();
-  const bool any_out = fused_barrier(f, c, 2, out_l != 0);
+  fused_stall(f, c, 2);
+  const int b2 = fused_barrier(f, c, 2, out_l != 0);
+  if (b2 < 0) return;   // aborted: the tokens stay as they were
   FSTAMP(5);
+  // every workgroup is past phase 2: commit this one's token counts
+  if (tid < 64) {
+    const uint32_t wpb = (f.nwords + f.nblk - 1) / f.nblk;
+    const uint32_t wlo = min(f.nwords, c * wpb), whi = min(f.nwords, wlo + wpb);
+    for (uint32_t w0 = wlo; w0 < whi; w0 += 64) {
+      const uint32_t w = w0 + tid;
+      if (w >= whi) break;
+      const bool last = w0 + 64 >= whi;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t b = 4 * w + q;
+        if (b < a.hash_size) a.tokens[b] = last ? p23[256 + tid * 4 + q] : ld_sc1(f.ntok + b);
+      }
+    }
+  }
+  const bool any_out = b2 > 0;
   // no bucket ran out: the speculative verdicts stand
   if (!any_out) {
     FSTAMP(6);
@@ -1531,26 +1600,68 @@ void fused_layout(uint32_t nblk, uint32_t seg, uint32_t hash_size, void *base, P
   f.novf = take((size_t)nblk * 4);
   f.need = take((size_t)hash_size * 4);
   f.code = take((size_t)FCREPL * ((((hash_size + 1) / 2) + 63) & ~63u) * 4);
+  f.ntok = take((size_t)hash_size * 4);
   total = off;
 }
+// (f.out sits at this offset of the scratch for every geometry)
+constexpr size_t kFusedOutOff = (FMAXBLK * 8 + 255) / 256 * 256;
 
-// A launch's barrier nonce: distinct per launch in this process, random
-// across processes (a stale word in a reused scratch buffer never matches),
-// low two bits clear for the barrier generation, never 0 or ~0.
-uint64_t fused_nonce() {
-  static const uint64_t seed = [] {
+// Barrier nonces: base + 8 k for the k-th fused launch of this process
+// (distinct per launch; the base is random, so a word another process left
+// in a reused scratch buffer never matches), low three bits clear for the
+// barrier generation and the abort bit.
+uint64_t nonce_base() {
+  static const uint64_t base = [] {
     std::random_device rd;
-    return ((uint64_t)rd() << 32 ^ rd()) ^
-           (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
-  }();
-  static std::atomic<uint64_t> ctr{0};
-  for (;;) {
-    uint64_t z = seed + 0x9e3779b97f4a7c15ull * (ctr.fetch_add(1) + 1);
+    uint64_t z = ((uint64_t)rd() << 32 ^ rd()) ^
+                 (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    z = (z ^ (z >> 31)) & ~3ull;
-    if (z != 0 && z != (~0ull & ~3ull)) return z;
+    return (z ^ (z >> 31)) & ~7ull;
+  }();
+  return base;
+}
+std::atomic<uint64_t> g_nonce_ctr{1};
+uint64_t nonce_of(uint64_t k) { return nonce_base() + 8 * k; }
+
+// Per scratch buffer: the first launch counter since its status was last
+// read (pptk_rx_permit_status reports whether any launch since then
+// aborted).  Small: one entry per scratch buffer in use.
+std::mutex g_status_mu;
+std::unordered_map<const void *, std::pair<uint64_t, uint64_t>> g_status;   // first, last k
+
+// The previous fused launch of each device, which the next one on another
+// stream waits for: two fused grids running at once could split the CUs
+// between them and each wait at its barrier for workgroups that cannot
+// become resident.  An event per device, recorded after every
+// fused launch (a marker on the same stream; no host wait).
+struct FusedOrder {
+  std::mutex mu;
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
+  bool any = false;
+};
+FusedOrder g_order[64];
+
+// Test builds only (PPTK_RX_TEST_HOOKS): fault injection for the abort path.
+void test_hooks(PermitFused &f) {
+#ifdef PPTK_RX_TEST_HOOKS
+  // (read at every launch: a test sets and clears them between calls)
+  auto knob = [](const char *name, long dflt) {
+    const char *e = getenv(name);
+    return e ? atol(e) : dflt;
+  };
+  const long stall_ms = knob("PPTK_RX_TEST_PERMIT_STALL_MS", 0);
+  const long stall_at = knob("PPTK_RX_TEST_PERMIT_STALL_AT", 1);
+  const long spin_ms = knob("PPTK_RX_TEST_PERMIT_SPIN_MS", 0);
+  if (spin_ms > 0) f.spin_ticks = (uint64_t)spin_ms * 100000ull;
+  if (stall_ms > 0) {
+    f.stall_ticks = (uint64_t)std::min(stall_ms, 10000l) * 100000ull;
+    f.stall_at = (uint32_t)stall_at;
   }
+#else
+  (void)f;
+#endif
 }
 
 // The fused kernel fits one workgroup per CU (its registers and 150 KB of
@@ -1592,13 +1703,42 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   // (records: the four passes -- their 1 GB read dominates, and the fused
   // kernel's records loads, one round in flight for its register budget,
   // measured slower: 0.351 vs 0.238 ms per 16 M records)
-  if (!a.force_passes && a.keys_in && fused_geom(a.n, a.hash_size, a.ncu, g) && fused_fits()) {
-    PermitFused f;
+  int dev = -1;
+  if (!a.force_passes && a.keys_in && fused_geom(a.n, a.hash_size, a.ncu, g) && fused_fits() &&
+      hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+    PermitFused f{};
     size_t total = 0;
     fused_layout(g.nblk, g.seg, a.hash_size, scratch, f, total);
-    f.nonce = fused_nonce();
+    f.spin_ticks = FUSED_SPIN_TICKS;
+    test_hooks(f);
+    FusedOrder &o = g_order[dev];
+    std::lock_guard<std::mutex> lk(o.mu);
+    hipError_t e = hipSuccess;
+    // (a device-scope release is all the stream wait needs: no system-scope
+    // fence -- an L2 write-back -- behind every launch)
+    if (!o.ev && hipEventCreateWithFlags(&o.ev, hipEventDisableTiming |
+                                                    hipEventDisableSystemFence) != hipSuccess &&
+        (e = hipEventCreateWithFlags(&o.ev, hipEventDisableTiming)) != hipSuccess)
+      return e;
+#ifndef PPTK_PERMIT_NO_ORDER   // (A/B: the launch order's cost)
+    if (o.any && o.last != st && (e = hipStreamWaitEvent(st, o.ev, 0)) != hipSuccess) return e;
+#endif
+    const uint64_t k = g_nonce_ctr.fetch_add(1);
+    f.nonce = nonce_of(k);
+    {
+      std::lock_guard<std::mutex> sl(g_status_mu);
+      auto it = g_status.find(scratch);
+      if (it == g_status.end()) g_status.emplace(scratch, std::make_pair(k, k));
+      else it->second.second = k;
+    }
     hipLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, a, f);
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+#ifndef PPTK_PERMIT_NO_ORDER
+    if ((e = hipEventRecord(o.ev, st)) != hipSuccess) return e;
+#endif
+    o.last = st;
+    o.any = true;
+    return hipSuccess;
   }
   if (a.hash_size <= HMAX && (a.n + HB - 1) / HB <= MAX_BLOCKS) {
     HistScratch h;
@@ -1632,6 +1772,25 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
   hipLaunchKernelGGL(permit_consume, dim3(blocks(a.hash_size)), dim3(PT), 0, st, a, s.first,
                      s.end);
   return hipGetLastError();
+}
+
+int permit_status(const void *scratch, hipStream_t st) {
+  std::pair<uint64_t, uint64_t> r;
+  {
+    std::lock_guard<std::mutex> sl(g_status_mu);
+    auto it = g_status.find(scratch);
+    if (it == g_status.end()) return 0;   // no fused launch on it since the last query
+    r = it->second;
+    g_status.erase(it);
+  }
+  if (hipStreamSynchronize(st) != hipSuccess) return -EIO;
+  uint64_t w = 0;
+  if (hipMemcpy(&w, (const uint8_t *)scratch + kFusedOutOff + 8, 8, hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return -EIO;
+  if (!(w & 1u)) return 0;
+  const uint64_t k = ((w & ~7ull) - nonce_base()) / 8;
+  return k >= r.first && k <= r.second ? -ETIMEDOUT : 0;
 }
 
 hipError_t launch_refill(uint32_t *tokens, uint32_t start, uint32_t end, uint32_t add,

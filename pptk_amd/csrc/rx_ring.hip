@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -95,6 +96,20 @@ void free_all(std::vector<void *> &v) {
   v.clear();
 }
 
+// One placement probe at a time per device: several rx queues of one GPU
+// (a context each, reference ldp/ldprecvmt.c:16-67) setting up their rings
+// at once would otherwise size their candidate sets from the same free
+// memory, then fail each other's allocations and time their probes beside
+// each other's.  Each call sees the memory the previous ones kept.
+std::mutex g_place_mu[64];
+std::mutex &place_mutex(int dev) { return g_place_mu[(unsigned)dev % 64u]; }
+
+// The memory a call's candidates (and spacers) may take beyond the pair it
+// keeps: `budget` if given, else `frac` of the device's free memory.
+double cand_budget(uint64_t budget, size_t free_b, double frac) {
+  return budget ? (double)std::min<uint64_t>(budget, free_b) : frac * (double)free_b;
+}
+
 }  // namespace
 
 extern "C" {
@@ -110,7 +125,7 @@ int pptk_rx_ring_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_ring_spec *sp
   const uint32_t reps = sp->reps ? sp->reps : 3;
   if ((rb != 64 && rb != 32) || sp->frame_bytes == 0 || sp->nrec == 0 || plen < 64 ||
       plen > 1536 || nf0 > 8 || nr0 > 16 || reps > 20 || sp->nrec > 0xffffffffull ||
-      (sp->flags & ~(uint32_t)PPTK_RX_RING_SETTLE))
+      (sp->flags & ~(uint32_t)PPTK_RX_RING_SETTLE) || sp->reserved)
     return -EINVAL;
   // the probe batch: fixed-stride frames of probe_len bytes over the frame
   // ring (up to nrec of them)
@@ -118,6 +133,7 @@ int pptk_rx_ring_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_ring_spec *sp
   if (n == 0) return -EINVAL;
   DeviceScope dg(ctx_device(c));
   if (!dg.ok) return -EIO;
+  std::lock_guard<std::mutex> plk(place_mutex(ctx_device(c)));
   const hipStream_t s = (hipStream_t)stream;
   // The frame ring is readable 64 bytes past its end (the kernels' 16-byte
   // chunk reads of a last frame, pptk_rx.h "Frames").
@@ -128,13 +144,15 @@ int pptk_rx_ring_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_ring_spec *sp
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return -EIO;
   if (fbytes + rbytes > free_b) return -ENOMEM;
-  // candidates beyond the first pair only as far as 60 % of the free memory
+  // candidates beyond the first pair only as far as the budget (default
+  // 60 % of the free memory) allows
   uint32_t nf = nf0, nr = nr0;
   auto need = [&](uint32_t f, uint32_t r) {
     return (f - 1) * (fbytes + spacer_f) + r * (rbytes + spacer_r) + fbytes;
   };
-  while (nf > 1 && (double)need(nf, nr) > 0.6 * (double)free_b) --nf;
-  while (nr > 1 && (double)need(nf, nr) > 0.6 * (double)free_b) --nr;
+  const double budget = cand_budget(sp->budget_bytes, free_b, 0.6);
+  while (nf > 1 && (double)need(nf, nr) > budget) --nf;
+  while (nr > 1 && (double)need(nf, nr) > budget) --nr;
 
   std::vector<void *> spacers, fc, rc;
   uint64_t allocated = 0;
@@ -232,6 +250,146 @@ int pptk_rx_ring_free(struct pptk_rx_ring *r) {
   if (r->d_frames) (void)hipFree(r->d_frames);
   if (r->d_recs) (void)hipFree(r->d_recs);
   memset(r, 0, sizeof(*r));
+  return 0;
+}
+
+// The multi-GPU gather buffers, placed.  Per batch the all-gather lands
+// (nranks - 1) shards of hashes in this GPU's HBM while the next batch
+// streams its frames, and the kernel writes its own hashes into its slice:
+// what those writes cost beside the frame stream depends on where the
+// buffer sits, as for the records (one GPU, C1500: 4.62 vs 5.19 ms per
+// batch with 940 MB of emulated gather writes beside it).  The
+// two double-buffered gather buffers are the two halves of one region
+// (placements come in runs of several GB, so both halves share the
+// region's class).  Per candidate region (allocated behind spacers): the
+// caller's batch is run with its hashes into each half's own slice in turn
+// and, beside each launch on a second stream, a device copy of the bytes
+// the gather would land in the rest of that half; the fastest region is
+// kept, the rest freed.
+int pptk_rx_gather_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,
+                         const struct pptk_rx_gather_spec *sp, struct pptk_rx_gather *out,
+                         void *stream) {
+  if (!c || !b || !sp || !out) return -EINVAL;
+  memset(out, 0, sizeof(*out));
+  const uint32_t ncand0 = sp->cands ? sp->cands : 8;
+  const uint32_t reps = sp->reps ? sp->reps : 4;
+  if (sp->nranks < 1 || sp->rank < 0 || sp->rank >= sp->nranks || sp->per_rank == 0 ||
+      b->n > sp->per_rank || ncand0 > 16 || reps > 20 || sp->reserved ||
+      (sp->flags & ~(uint32_t)PPTK_RX_RING_SETTLE) ||
+      sp->per_rank > (1ull << 40) / (uint64_t)sp->nranks)
+    return -EINVAL;
+  DeviceScope dg(ctx_device(c));
+  if (!dg.ok) return -EIO;
+  std::lock_guard<std::mutex> plk(place_mutex(ctx_device(c)));
+  const hipStream_t s = (hipStream_t)stream;
+  const uint64_t nb = (uint64_t)sp->nranks * sp->per_rank * 8;   // one gather buffer
+  const uint64_t lo = (uint64_t)sp->rank * sp->per_rank * 8, hi = lo + sp->per_rank * 8;
+  const uint64_t spacer = std::min<uint64_t>(4 * kGiB, std::max<uint64_t>(256ull << 20, 4 * nb));
+  const uint64_t srcb = std::max<uint64_t>(std::max(lo, nb - hi), 16);
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return -EIO;
+  if (2 * nb + srcb > free_b) return -ENOMEM;
+  uint32_t nc = ncand0;
+  const double budget = cand_budget(sp->budget_bytes, free_b, 0.5);
+  while (nc > 1 && (double)(nc * (2 * nb + spacer) + srcb) > budget) --nc;
+
+  std::vector<void *> spacers, cands;
+  void *src = nullptr;
+  auto alloc = [](uint64_t bytes, std::vector<void *> &into) {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    into.push_back(p);
+    return true;
+  };
+  for (uint32_t k = 0; k < nc; ++k)
+    if ((k > 0 && !alloc(spacer, spacers)) || !alloc(2 * nb, cands)) break;
+  hipStream_t side = nullptr;
+  hipEvent_t ev = nullptr;
+  int err = 0;
+  if (cands.empty() || hipMalloc(&src, srcb) != hipSuccess) err = -ENOMEM;
+  if (!err && (hipMemsetAsync(src, 0, srcb, s) != hipSuccess ||
+               hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess ||
+               hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess))
+    err = -EIO;
+  nc = (uint32_t)cands.size();
+  std::vector<float> ms(nc, 0.f);
+  for (uint32_t k = 0; k < nc && !err; ++k) {
+    std::chrono::steady_clock::time_point t0;
+    for (uint32_t r = 0; r < reps + 2 && !err; ++r) {
+      if (r == 2) {   // two untimed warm-up batches per candidate
+        if (hipStreamSynchronize(s) != hipSuccess || hipStreamSynchronize(side) != hipSuccess) {
+          err = -EIO;
+          break;
+        }
+      }
+      if (r == 2) t0 = std::chrono::steady_clock::now();
+      uint8_t *half = (uint8_t *)cands[k] + (r & 1) * nb;
+      pptk_rx_dev_batch bb = *b;
+      bb.d_hash = (uint64_t *)(half + lo);
+      if ((err = pptk_rx_batch_device(c, &bb, stream)) != 0) break;
+      if (hipEventRecord(ev, s) != hipSuccess || hipStreamWaitEvent(side, ev, 0) != hipSuccess ||
+          (lo && hipMemcpyAsync(half, src, lo, hipMemcpyDeviceToDevice, side) != hipSuccess) ||
+          (nb > hi &&
+           hipMemcpyAsync(half + hi, src, nb - hi, hipMemcpyDeviceToDevice, side) != hipSuccess))
+        err = -EIO;
+      if (r == reps + 1 && !err) {
+        if (hipStreamSynchronize(s) != hipSuccess || hipStreamSynchronize(side) != hipSuccess)
+          err = -EIO;
+        ms[k] = (float)(std::chrono::duration<double, std::milli>(
+                            std::chrono::steady_clock::now() - t0).count() / reps);
+      }
+    }
+  }
+  if (side) {
+    (void)hipStreamSynchronize(side);
+    (void)hipStreamDestroy(side);
+  }
+  (void)hipStreamSynchronize(s);
+  if (ev) (void)hipEventDestroy(ev);
+  if (src) (void)hipFree(src);
+  if (err) {
+    free_all(spacers);
+    free_all(cands);
+    return err;
+  }
+  const uint32_t best = (uint32_t)(std::min_element(ms.begin(), ms.end()) - ms.begin());
+  void *keep = cands[best];
+  cands[best] = nullptr;
+  uint64_t freed = (uint64_t)spacers.size() * spacer + (uint64_t)(nc - 1) * 2 * nb + srcb;
+  free_all(spacers);
+  free_all(cands);
+  // the buffers start zeroed (the padding past the last rank's frames too)
+  if (hipMemsetAsync(keep, 0, 2 * nb, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipFree(keep);
+    return -EIO;
+  }
+  out->d_out[0] = (uint64_t *)keep;
+  out->d_out[1] = (uint64_t *)((uint8_t *)keep + nb);
+  out->per_rank = sp->per_rank;
+  out->nranks = sp->nranks;
+  out->rank = sp->rank;
+  out->device = ctx_device(c);
+  out->cands = nc;
+  out->chosen = (int32_t)best;
+  out->chosen_ms = ms[best];
+  out->first_ms = ms[0];
+  out->freed_bytes = freed;
+  if (sp->flags & PPTK_RX_RING_SETTLE) {
+    const double sec = (double)freed / kScrubBytesPerS;
+    std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(sec * 1e6)));
+    out->settle_ms = (uint32_t)(sec * 1e3);
+  }
+  return 0;
+}
+
+int pptk_rx_gather_free(struct pptk_rx_gather *g) {
+  if (!g) return -EINVAL;
+  DeviceScope dg(g->device);
+  if (g->d_out[0]) (void)hipFree(g->d_out[0]);
+  memset(g, 0, sizeof(*g));
   return 0;
 }
 

@@ -39,7 +39,28 @@ class RxRingSpec(ctypes.Structure):
     _fields_ = [("frame_bytes", ctypes.c_uint64), ("nrec", ctypes.c_uint64),
                 ("rec_bytes", ctypes.c_uint32), ("probe_len", ctypes.c_uint32),
                 ("frame_cands", ctypes.c_uint32), ("rec_cands", ctypes.c_uint32),
-                ("reps", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("reps", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("budget_bytes", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
+
+
+class RxGatherSpec(ctypes.Structure):
+    """struct pptk_rx_gather_spec (include/pptk_rx.h)."""
+    _fields_ = [("per_rank", ctypes.c_uint64), ("nranks", ctypes.c_int32),
+                ("rank", ctypes.c_int32), ("cands", ctypes.c_uint32), ("reps", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("budget_bytes", ctypes.c_uint64)]
+
+
+class RxGatherC(ctypes.Structure):
+    """struct pptk_rx_gather."""
+    _fields_ = [("d_out", ctypes.c_void_p * 2), ("per_rank", ctypes.c_uint64),
+                ("nranks", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("cands", ctypes.c_uint32), ("chosen", ctypes.c_int32),
+                ("chosen_ms", ctypes.c_float), ("first_ms", ctypes.c_float),
+                ("settle_ms", ctypes.c_uint32), ("freed_bytes", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(RxGatherSpec) == 40 and ctypes.sizeof(RxGatherC) == 64
 
 
 class RxRingC(ctypes.Structure):
@@ -82,6 +103,39 @@ class _DevMem:
                                          "data": (ptr, False), "version": 3, "strides": None}
 
 
+class _GatherOwner:
+    """Frees a pptk_rx_gather when the last tensor over it is gone."""
+
+    def __init__(self, L, g):
+        self.L, self.g = L, g
+
+    def __del__(self):
+        try:
+            if self.g is not None:
+                self.L.pptk_rx_gather_free(ctypes.byref(self.g))
+        except Exception:
+            pass
+        self.g = None
+
+
+class DeviceGather:
+    """Library-placed gather buffers (pptk_rx_gather_alloc): .out[0], .out[1]
+    (torch int64, nranks * per_rank each) and the probe .report; freed once
+    no tensor over them is referenced."""
+
+    def __init__(self, ctx, g):
+        import torch
+        dev = torch.device("cuda", ctx.device)
+        own = _GatherOwner(ctx._L, g)
+        nb = g.nranks * g.per_rank * 8
+        self.out = [torch.as_tensor(_DevMem(own, g.d_out[k], nb), device=dev).view(torch.int64)
+                    for k in range(2)]
+        self.report = {"candidates": g.cands, "chosen": g.chosen,
+                       "chosen_ms": round(g.chosen_ms, 4), "first_ms": round(g.first_ms, 4),
+                       "freed_bytes": g.freed_bytes, "settle_ms": g.settle_ms,
+                       "alloc": "pptk_rx_gather_alloc"}
+
+
 class DeviceRing:
     """Library-owned placed device rings (pptk_rx_ring_alloc): .frames (torch
     uint8, frame_bytes + 64), .recs (torch uint8 (nrec, rec_bytes)) and the
@@ -118,10 +172,11 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
            "pptk_rx_permit_scratch_bytes", "pptk_rx_permit_device", "pptk_rx_permit_keys_device",
-           "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_set_side_buffer",
+           "pptk_rx_permit_status", "pptk_rx_tokens_refill_device", "pptk_tx_cksum_device", "pptk_tx_set_side_buffer",
            "pptk_tx_rewrite_device",
            "pptk_tcp_mss_clamp_device", "pptk_rx_autotune", "pptk_rx_place_records",
            "pptk_rx_place_buffers", "pptk_rx_ring_alloc", "pptk_rx_ring_free",
+           "pptk_rx_gather_alloc", "pptk_rx_gather_free",
            # multi-GPU (RCCL)
            "pptk_rx_device_count", "pptk_rx_comm_uid", "pptk_rx_comm_create",
            "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
@@ -196,6 +251,13 @@ def lib(path=None):
             L.pptk_rx_ring_alloc.restype = ctypes.c_int
             L.pptk_rx_ring_free.argtypes = [ctypes.POINTER(RxRingC)]
             L.pptk_rx_ring_free.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_gather_alloc"):         # absent from older A/B builds
+            L.pptk_rx_gather_alloc.argtypes = [vp, ctypes.POINTER(RxDevBatch),
+                                               ctypes.POINTER(RxGatherSpec),
+                                               ctypes.POINTER(RxGatherC), vp]
+            L.pptk_rx_gather_alloc.restype = ctypes.c_int
+            L.pptk_rx_gather_free.argtypes = [ctypes.POINTER(RxGatherC)]
+            L.pptk_rx_gather_free.restype = ctypes.c_int
         if hasattr(L, "pptk_tcp_mss_clamp_device"):    # absent from older A/B builds
             L.pptk_tcp_mss_clamp_device.argtypes = [vp, vp, vp, vp, ctypes.c_uint64,
                                                     ctypes.c_uint32, ctypes.c_uint64,
@@ -214,6 +276,9 @@ def lib(path=None):
             L.pptk_rx_tokens_refill_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32,
                                                        ctypes.c_uint32, ctypes.c_uint32, vp]
             L.pptk_rx_tokens_refill_device.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_permit_status"):        # absent from older A/B builds
+            L.pptk_rx_permit_status.argtypes = [vp, vp, vp]
+            L.pptk_rx_permit_status.restype = ctypes.c_int
         if hasattr(L, "pptk_rx_batch_device_mixed"):   # absent from older A/B builds
             L.pptk_rx_batch_device_mixed.argtypes = [vp, ctypes.POINTER(RxDevBatch), vp, vp, vp]
             L.pptk_rx_batch_device_mixed.restype = ctypes.c_int
@@ -413,12 +478,12 @@ class RxContext:
         return bf.value, br.value, [round(x, 4) for x in ms[:nf * nr]]
 
     def ring_alloc(self, frame_bytes, nrec, rec_bytes=64, probe_len=0, frame_cands=0,
-                   rec_cands=0, reps=0, settle=False, stream=None):
+                   rec_cands=0, reps=0, settle=False, stream=None, budget_bytes=0):
         """pptk_rx_ring_alloc: placed device frame and record rings (a
         DeviceRing; its .report carries the probe)."""
         import torch
         spec = RxRingSpec(frame_bytes, nrec, rec_bytes, probe_len, frame_cands, rec_cands, reps,
-                          RING_SETTLE if settle else 0)
+                          RING_SETTLE if settle else 0, budget_bytes, 0)
         ring = RxRingC()
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         rc = self._L.pptk_rx_ring_alloc(self._ctx, ctypes.byref(spec), ctypes.byref(ring),
@@ -426,6 +491,30 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_ring_alloc failed ({rc})")
         return DeviceRing(self, ring)
+
+    def gather_alloc(self, frames, n, per_rank, nranks, rank, off=None, lens=None, stride=0,
+                     fixed_len=0, max_len=0, recs=None, compact=False, cands=0, reps=0,
+                     settle=False, budget_bytes=0, stream=None):
+        """pptk_rx_gather_alloc: this rank's two gather buffers, placed by a
+        probe that runs the batch (frames/recs as for batch_device) with its
+        hashes into each candidate; a DeviceGather."""
+        import torch
+        rb = 32 if compact else 64
+        if recs is None:
+            recs = torch.empty((n, rb), dtype=torch.uint8, device=frames.device)
+        b = RxDevBatch(frames.data_ptr(), None if off is None else off.data_ptr(),
+                       None if lens is None else lens.data_ptr(), None, stride, fixed_len,
+                       max_len, n, None if compact else recs.data_ptr(), None,
+                       recs.data_ptr() if compact else None)
+        spec = RxGatherSpec(per_rank, nranks, rank, cands, reps, RING_SETTLE if settle else 0, 0,
+                            budget_bytes)
+        g = RxGatherC()
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        rc = self._L.pptk_rx_gather_alloc(self._ctx, ctypes.byref(b), ctypes.byref(spec),
+                                          ctypes.byref(g), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_gather_alloc failed ({rc})")
+        return DeviceGather(self, g)
 
     def tuned_variant(self, frames, n, off=None, lens=None, stride=0, fixed_len=0, max_len=0,
                       compact=False):
@@ -499,6 +588,14 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_permit_keys_device failed ({rc})")
         return verdict
+
+    def permit_status(self, scratch, stream=None):
+        """pptk_rx_permit_status: 0, or -ETIMEDOUT if a permit_keys_device
+        call on `scratch` since the last query aborted (synchronises the
+        stream)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(scratch.device)
+        return self._L.pptk_rx_permit_status(self._ctx, _dp(scratch), ctypes.c_void_p(s.cuda_stream))
 
     def tokens_refill_device(self, tokens, start, end, add, initial, stream=None):
         import torch

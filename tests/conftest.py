@@ -10,6 +10,9 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 GOLDEN_SETS = ("edge", "fuzz", "c64", "c1500", "cmix", "icmp", "frag")
+# the product library built with -DPPTK_RX_TEST_HOOKS (Makefile "hooks"):
+# the fault-injection knobs of the failure-path tests exist only there
+HOOKS_LIB = os.path.join(ROOT, "tests", "hooks", "libpptkrx_hooks.so")
 
 
 def pytest_configure(config):

@@ -356,19 +356,80 @@ def test_comm_warmup_gather_stall_is_bounded(dev, monkeypatch):
     stream, so the wait below is the stall, not a hang); the same context
     then builds a communicator that gathers the golden hashes."""
     import time
+    from conftest import HOOKS_LIB
     from pptk_amd.rx import RxContext, comm_uid
     z = load_golden("fuzz")
     b4, b6, hs = (int(x) for x in z["iphash"])
-    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_frame=65535, comm_timeout_ms=1500)
+    # (the knob exists only in the test build of the library)
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_frame=65535, comm_timeout_ms=1500,
+                    lib_path=HOOKS_LIB)
     monkeypatch.setenv("PPTK_RX_COMM_TEST_WARMUP_STALL_MS", "4000")
-    rc, took = _timed_create(ctx, 1, 0, comm_uid())
+    rc, took = _timed_create(ctx, 1, 0, comm_uid(lib_path=HOOKS_LIB))
     assert rc == -ETIMEDOUT and 1.2 < took < 3.5, (rc, took)
     monkeypatch.delenv("PPTK_RX_COMM_TEST_WARMUP_STALL_MS")
     t0 = time.monotonic()
     torch.cuda.synchronize()
     assert time.monotonic() - t0 < 15
     time.sleep(1.0)          # (the helper frees its buffers after the drain)
-    ctx.comm_create(1, 0, comm_uid())
+    ctx.comm_create(1, 0, comm_uid(lib_path=HOOKS_LIB))
     got, _ = _gather_set(ctx, z, dev)
     assert np.array_equal(got, as_records(z["recs"])["flow_hash"])
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", ["cmix", "c1500"])
+def test_placed_gather_buffers_gather_golden(dev, name):
+    """pptk_rx_gather_alloc: the library places this rank's two gather
+    buffers by running the batch into each candidate region (as the
+    multi-GPU bench and examples/rx_multigpu.c now take them); on a one-rank
+    communicator the kernel writes the rank's hashes into each buffer's
+    slice and the in-place all-gather leaves the golden flow hashes, in both
+    buffers; the padding past the frames stays zero; the report is
+    consistent; the memory comes back when the buffers go."""
+    import gc
+    from pptk_amd.rx import comm_uid, shard_range
+    from pptk_amd.shard import GatherBuffer
+    z = load_golden(name)
+    ctx = _ctx(z)
+    ctx.comm_create(1, 0, comm_uid())
+    n = len(z["off"])
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    kw = dict(off=off, lens=lens, max_len=int(z["len"].max()))
+    n_total = n + 5                       # padded shard: 5 slots no frame fills
+    first, count, per = shard_range(n_total, 1, 0)
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(dev)
+    g = ctx.gather_alloc(frames, n, per, 1, 0, cands=3, reps=2, **kw)
+    rep = g.report
+    assert rep["candidates"] == 3 and 0 <= rep["chosen"] < 3 and rep["chosen_ms"] > 0
+    assert rep["freed_bytes"] > 0
+    want = as_records(z["recs"])["flow_hash"]
+    for k in range(2):
+        gb = GatherBuffer(n_total, 1, 0, dev, out=g.out[k])
+        assert int(gb.out.abs().sum().item()) == 0          # zeroed
+        recs = ctx.batch_device(frames, n, hash_out=gb.local[:n], **kw)
+        got = gb.gather(ctx).cpu().numpy().view(np.uint64)
+        torch.cuda.synchronize()
+        assert np.array_equal(got[:n], want), k
+        assert (got[n:] == 0).all()
+        assert np.array_equal(as_records(recs.cpu().numpy().reshape(-1))["flow_hash"], want)
+    del g, gb
+    gc.collect()
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info(dev)
+    assert free1 >= free0 - (64 << 20)
+    ctx.close()
+
+
+def test_gather_alloc_rejects(dev):
+    """Bad gather specs: -EINVAL before anything is allocated."""
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    frames = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    for args in ((10, 0, 0), (10, 2, 2), (10, 1, -1), (0, 1, 0), (5, 1, 0)):   # (per, nranks, rank)
+        with pytest.raises(OSError) as e:
+            ctx.gather_alloc(frames, 10, *args, stride=64, fixed_len=64)
+        assert e.value.errno == EINVAL, args
     ctx.close()

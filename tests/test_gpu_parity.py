@@ -1012,6 +1012,65 @@ def test_ring_alloc(compact, dev):
     ctx.close()
 
 
+def test_ring_alloc_two_queues_on_one_gpu(dev):
+    """Two rx queues of one GPU, a context each (reference ldp/ldprecvmt.c:
+    16-67), set up their rings at the same time from two threads, each with
+    a memory budget: the library runs the two placement probes one after the
+    other (so neither sizes its candidates from memory the other is holding,
+    nor times its probe beside the other's), both calls succeed with more
+    than one candidate pair, and both rings give the golden records."""
+    import threading
+    z = load_golden("cmix")
+    n = len(z["off"])
+    ctxs = [_ctx(z), _ctx(z)]
+    fbytes = max(z["buf"].size, 1500 * 4096)
+    rings, errs = [None, None], []
+
+    def setup(k):
+        try:
+            rings[k] = ctxs[k].ring_alloc(fbytes, n, 64, frame_cands=2, rec_cands=4, reps=2,
+                                          budget_bytes=12 << 30,
+                                          stream=torch.cuda.Stream(dev))
+        except Exception as e:          # (reported below)
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=setup, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errs, errs
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    for ctx, ring in zip(ctxs, rings):
+        rep = ring.report
+        assert rep["frame_cands"] * rep["rec_cands"] > 1, rep
+        ring.frames[:z["buf"].size].copy_(torch.from_numpy(z["buf"]).to(dev))
+        ctx.batch_device(ring.frames, n, off=off, lens=lens, max_len=1500, recs=ring.recs)
+        torch.cuda.synchronize()
+        d = diff_records(ring.recs.cpu().numpy().reshape(-1), z["recs"])
+        assert not d, d
+    assert rings[0].frames.data_ptr() != rings[1].frames.data_ptr()
+    del rings
+    for ctx in ctxs:
+        ctx.close()
+
+
+def test_ring_alloc_budget_limits_candidates(dev):
+    """A budget smaller than the default candidate set: fewer candidates
+    are probed (the spacers and candidates must fit in it), the ring is
+    still returned and correct in size."""
+    z = load_golden("edge")
+    ctx = _ctx(z)
+    fbytes = 1500 * 4096
+    ring = ctx.ring_alloc(fbytes, 4096, 64, budget_bytes=3 << 30)
+    rep = ring.report
+    assert rep["frame_cands"] * rep["rec_cands"] < 3 * 8, rep
+    assert ring.frames.numel() == fbytes + 64 and tuple(ring.recs.shape) == (4096, 64)
+    del ring
+    ctx.close()
+
+
 def test_ring_alloc_rejects(dev):
     """Bad ring specs are -EINVAL before anything is allocated."""
     z = load_golden("edge")

@@ -375,3 +375,97 @@ def test_permit_keys_out_of_range_are_not_subjects(dev):
     torch.cuda.synchronize()
     assert np.array_equal(v.cpu().numpy(), v_want)
     assert np.array_equal(tokt.cpu().numpy().view(np.uint32), t_want)
+
+
+ETIMEDOUT = 110
+
+
+def _keys_case(n, hs, seed):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, hs, n).astype(np.int64)
+    k[rng.random(n) < 0.02] = -1
+    tok = rng.integers(0, 2 * n // hs, hs).astype(np.uint32)     # ~half denied
+    keys = np.where(k >= 0, k, 0xFFFFFFFF).astype(np.uint32)
+    return k, tok, keys
+
+
+def test_permit_keys_two_contexts_two_streams_at_once(dev):
+    """Two rx queues on one GPU (a context each, as ldp/ldprecvmt.c:16-67
+    runs one thread per queue) issue the rate limiter on two streams at the
+    same time, four batches each with their own token arrays.  The fused
+    launches need every workgroup resident; two of them at once could split
+    the CUs and each wait for the other's: the library orders
+    them, so both chains equal the frame-by-frame semantics, no launch
+    aborts (status 0 on both scratch buffers) and nothing waits out the
+    2 s barrier bound."""
+    import time
+    n, hs, reps = 1 << 22, 1 << 16, 4
+    cases = [_keys_case(n, hs, 91 + i) for i in range(2)]
+    want = []
+    for k, tok, _ in cases:
+        t, vs = tok, []
+        for _ in range(reps):
+            v, t = _np_permit(k, hs, t)
+            vs.append(v)
+        want.append((vs, t))
+    ctxs = [_ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+            for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    keys = [torch.from_numpy(c[2].view(np.int32)).to(dev) for c in cases]
+    toks = [torch.from_numpy(c[1].view(np.int32).copy()).to(dev) for c in cases]
+    scratch = [torch.empty(ctxs[0]._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8,
+                           device=dev) for _ in range(2)]
+    verdicts = [[torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(reps)]
+                for _ in range(2)]
+    torch.cuda.synchronize()
+    t0 = time.monotonic()
+    for r in range(reps):
+        for i in range(2):
+            ctxs[i].permit_keys_device(keys[i], 4, toks[i], verdict=verdicts[i][r],
+                                       scratch=scratch[i], stream=streams[i])
+    torch.cuda.synchronize()
+    took = time.monotonic() - t0
+    for i in range(2):
+        assert ctxs[i].permit_status(scratch[i], stream=streams[i]) == 0
+        for r in range(reps):
+            assert np.array_equal(verdicts[i][r].cpu().numpy(), want[i][0][r]), (i, r)
+        assert np.array_equal(toks[i].cpu().numpy().view(np.uint32), want[i][1]), i
+    assert took < 1.5, took
+
+
+@pytest.mark.parametrize("stall_at", [1, 2])
+def test_permit_fused_abort_leaves_tokens_and_reports(dev, monkeypatch, stall_at):
+    """Fault injection (the test build of the library, PPTK_RX_TEST_HOOKS):
+    one workgroup of the fused launch is held 600 ms before grid barrier
+    `stall_at` while the others' barrier gives up after 200 ms.  The launch
+    aborts: pptk_rx_permit_status reports -ETIMEDOUT and the token array is
+    exactly as before the call (the commit comes after the last barrier).
+    The same call repeated without the stall gives the frame-by-frame
+    verdicts and tokens, and status 0."""
+    from conftest import HOOKS_LIB
+    from pptk_amd.rx import RxContext
+    if _PATH[0] == "passes":
+        pytest.skip("the four-launch path has no grid barrier")
+    n, hs = 1 << 20, 1 << 16
+    k, tok_h, keys_h = _keys_case(n, hs, 97)
+    v_want, t_want = _np_permit(k, hs, tok_h)
+    ctx = RxContext(0, bytes(range(1, 17)), 24, 48, hs, lib_path=HOOKS_LIB)
+    keys = torch.from_numpy(keys_h.view(np.int32)).to(dev)
+    tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
+    scratch = torch.empty(ctx._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8,
+                          device=dev)
+    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_MS", "600")
+    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_SPIN_MS", "200")
+    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_AT", str(stall_at))
+    ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
+    assert ctx.permit_status(scratch) == -ETIMEDOUT
+    assert np.array_equal(tok.cpu().numpy().view(np.uint32), tok_h)
+    for name in ("PPTK_RX_TEST_PERMIT_STALL_MS", "PPTK_RX_TEST_PERMIT_SPIN_MS",
+                 "PPTK_RX_TEST_PERMIT_STALL_AT"):
+        monkeypatch.delenv(name)
+    assert ctx.permit_status(scratch) == 0          # (queried: nothing since)
+    v = ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
+    assert ctx.permit_status(scratch) == 0
+    assert np.array_equal(v.cpu().numpy(), v_want)
+    assert np.array_equal(tok.cpu().numpy().view(np.uint32), t_want)
+    ctx.close()

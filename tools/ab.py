@@ -4,8 +4,10 @@ on one batch.
     python tools/ab.py c1500 3:1 3:0 6:1 ...        (variant:flags pairs)
     AB_LIBS=old=build/ab_old/libpptkrx.so python tools/ab.py cmix 3:33 old:3:33
 
-A setting is [lib:]variant:flags[:c][:m]; variant or flags -1 = automatic
-choice; a trailing :c writes compact 32-byte records, :m runs that setting
+A setting is [lib:]variant:flags[:c][:m][:h]; variant or flags -1 = automatic
+choice; a trailing :h also writes the dense flow-hash array (the multi-GPU
+all-gather's send slice, into one buffer allocated after the records);
+a trailing :c writes compact 32-byte records, :m runs that setting
 through pptk_rx_batch_device_mixed (mixed batches; as AB_MIXED=1 does for all);
 lib names come from AB_LIBS (name=path,...), default = pptk_amd/libpptkrx.so.
 Generates the batch once, then times every setting in interleaved rounds
@@ -27,8 +29,11 @@ sys.path.insert(0, ROOT)
 
 
 def parse_setting(a):
-    """[lib:]variant:flags[:c][:m] -> (lib, variant, flags, compact, mixed)."""
+    """[lib:]variant:flags[:c][:m][:h] -> (lib, variant, flags, compact, mixed, hash)."""
     p = a.split(":")
+    hsh = p[-1] == "h"
+    if hsh:
+        p = p[:-1]
     mixed = p[-1] == "m"
     if mixed:
         p = p[:-1]
@@ -36,8 +41,8 @@ def parse_setting(a):
     if compact:
         p = p[:-1]
     if len(p) == 2:
-        return ("", int(p[0]), int(p[1]), compact, mixed)
-    return (p[0], int(p[1]), int(p[2]), compact, mixed)
+        return ("", int(p[0]), int(p[1]), compact, mixed, hsh)
+    return (p[0], int(p[1]), int(p[2]), compact, mixed, hsh)
 
 
 def main():
@@ -77,7 +82,10 @@ def main():
         scratch = torch.empty(ctxs[""]._L.pptk_rx_bin_scratch_bytes(n), dtype=torch.uint8,
                               device=dev)
 
-    def launch(ctx, compact, mix=False):
+    hbuf = (torch.empty(n, dtype=torch.int64, device=dev) if any(st[5] for st in settings)
+            else None)
+
+    def launch(ctx, compact, mix=False, hsh=False):
         recs = recs32 if compact else recs64
         if (mixed or mix) and "off" in b:
             ctx.batch_device_mixed(b["frames"], n, b["off"], b["lens"], recs=recs64,
@@ -86,7 +94,8 @@ def main():
             ctx.batch_device(b["frames"], n, recs=recs, perm=ctx.bin_device(b["lens"], n),
                              compact=compact, **kw)
         else:
-            ctx.batch_device(b["frames"], n, recs=recs, compact=compact, **kw)
+            ctx.batch_device(b["frames"], n, recs=recs, compact=compact,
+                             hash_out=hbuf if hsh else None, **kw)
 
     ref = {}
     times = {s: [] for s in settings}
@@ -95,17 +104,19 @@ def main():
         for s in settings:
             ctx = ctxs[s[0]]
             ctx.set_tuning(s[1], s[2])
-            launch(ctx, s[3], s[4])
+            launch(ctx, s[3], s[4], s[5])
             torch.cuda.synchronize()
             if s not in same:       # every setting must give the same records
                 r = recs32 if s[3] else recs64
                 if s[3] not in ref:
                     ref[s[3]] = r.clone()
                 same[s] = bool(torch.equal(r, ref[s[3]]))
+                if s[5] and not s[3]:     # the dense hashes equal the records' flow_hash
+                    same[s] = same[s] and bool(torch.equal(hbuf, r.view(torch.int64)[:, 0]))
             for _ in range(reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                launch(ctx, s[3], s[4])
+                launch(ctx, s[3], s[4], s[5])
                 e1.record()
                 torch.cuda.synchronize()
                 times[s].append(e0.elapsed_time(e1))
@@ -121,7 +132,7 @@ def main():
     for s, t in times.items():
         ms = float(np.median(t))
         key = ":".join(str(x) for x in s[:3] if x != "") + (":c" if s[3] else "") + \
-            (":m" if s[4] else "")
+            (":m" if s[4] else "") + (":h" if s[5] else "")
         out[key] = {"ms": round(ms, 4), "gbs": round(b["bytes"] / ms / 1e6, 1),
                     "mpkts": round(n / ms / 1e3, 1), "same_records": same[s]}
     print(json.dumps(out))
