@@ -301,6 +301,13 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
         recs = torch.empty((n, 32 if compact else 64), dtype=torch.uint8, device=dev)
     gplace = None
     if isinstance(gbs, str):          # "place": the gather buffers, placed
+        # (after the scrub of what the ring placement freed: beside it every
+        # candidate runs slow alike and the probe cannot tell them apart)
+        if placement and "_freed_at" in placement:
+            wait = placement["_freed_at"] + placement["freed_bytes"] / SCRUB_BYTES_PER_S \
+                - time.perf_counter()
+            if wait > 0:
+                time.sleep(wait)
         gbs, gplace = placed_gather(ctx, b, recs, kw, n_gather_total, ws, rank, dev)
     if autotune:
         # pick this GPU's fastest interchangeable kernel shape for the batch
@@ -572,7 +579,7 @@ def compact_line(full, detail_path=None):
                                                         "sampled_frames_per_rank",
                                                         "sampled_mismatches")}
         bp = gat.get("buffer_placement") or {}
-        g["placement"] = {k: bp.get(k) for k in ("alloc", "candidates", "chosen", "chosen_ms",
+        g["placement"] = {k: bp.get(k) for k in ("alloc", "candidates", "chosen", "chosen_ms", "candidate_ms",
                                                   "first_ms")}
         line["allgather"] = g
         line["value_no_gather"] = full.get("value_no_gather")

@@ -661,13 +661,18 @@ int pptk_rx_ring_free(struct pptk_rx_ring *ring);
  * gather's writes -- the kernel's own hashes into the rank's slice and the
  * (nranks - 1) shards the collective lands while the next batch streams --
  * cost beside the frame stream.  Candidate regions
- * (each holding both buffers) are allocated apart; on each, `b` (this
- * rank's batch: frames, records, geometry; b->d_hash is replaced by each
- * buffer's slice in turn) runs reps + 2 times with a device copy of the
- * bytes the gather would land beside every launch on a second stream; the
- * fastest region is kept, everything else freed.  Synchronous; uses
- * `stream`.  Call after the rings are placed (the probe runs on them).
- * cands 1..16 (0 = 8), reps 1..20 (0 = 4); candidates as far as
+ * (each holding both buffers) are allocated apart; `b` (this rank's batch:
+ * frames, records, geometry; b->d_hash is replaced by each buffer's slice in
+ * turn) runs ~300 ms to warm the clocks, then `reps` rounds over the
+ * candidates, each launch followed, on a second stream, by a device copy of
+ * the bytes the gather would land (beside the next launch, as in an rx loop);
+ * the region whose launches have the lowest median kernel time is kept,
+ * everything else freed.  Synchronous; uses
+ * `stream`.  Call after the rings are placed (the probe runs on them) and
+ * after the scrub of what their placement freed is over
+ * (PPTK_RX_RING_SETTLE): batches beside the scrub run up to 20 % slower on
+ * every candidate alike, which hides the differences the probe looks for.
+ * cands 1..16 (0 = 8), reps 1..20 (0 = 5); candidates as far as
  * budget_bytes (0: 50 % of the free memory) allows.  b->n <= per_rank.
  * Release with pptk_rx_gather_free. */
 struct pptk_rx_gather_spec {
@@ -675,7 +680,7 @@ struct pptk_rx_gather_spec {
   int32_t nranks;
   int32_t rank;
   uint32_t cands;         /* candidate regions, 0 = 8 */
-  uint32_t reps;          /* timed probe batches per candidate, 0 = 4 */
+  uint32_t reps;          /* rounds over the candidates (two timed batches each), 0 = 5 */
   uint32_t flags;         /* PPTK_RX_RING_SETTLE */
   uint32_t reserved;      /* 0 */
   uint64_t budget_bytes;  /* 0 = 50 % of the free memory */
@@ -689,10 +694,11 @@ struct pptk_rx_gather {
   int32_t device;
   uint32_t cands;         /* candidate regions probed */
   int32_t chosen;         /* the region kept */
-  float chosen_ms;        /* probe ms per batch on the region kept */
+  float chosen_ms;        /* median probe kernel ms on the region kept */
   float first_ms;         /* ... on candidate 0: a plain allocation */
   uint32_t settle_ms;
   uint64_t freed_bytes;
+  float cand_ms[16];      /* median probe kernel ms of every candidate probed */
 };
 int pptk_rx_gather_alloc(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batch *b,
                          const struct pptk_rx_gather_spec *spec, struct pptk_rx_gather *gather,

@@ -540,6 +540,7 @@ void comm_release(pptk_rx_ctx *c) {
     if (const Rccl *R = rccl()) teardown(R, m, ctx_comm_timeout_ms(c));
   std::lock_guard<std::mutex> g(g_slots);
   set_comm(c, nullptr);
+  { std::lock_guard<std::mutex> gm(m->mu); }   // (an abort still inside RCCL ends first)
   delete m;
 }
 
@@ -634,7 +635,7 @@ int pptk_rx_comm_destroy(struct pptk_rx_ctx *c) {
 
 int pptk_rx_comm_abort(struct pptk_rx_ctx *c) {
   if (!c) return -EINVAL;
-  std::lock_guard<std::mutex> g(g_slots);
+  std::unique_lock<std::mutex> g(g_slots);
   RxComm *m = comm_of(c);
   if (!m) {   // nothing to cancel yet: the context's next creation is
     m = new (std::nothrow) RxComm();
@@ -643,7 +644,7 @@ int pptk_rx_comm_abort(struct pptk_rx_ctx *c) {
     set_comm(c, m);
     return 0;
   }
-  std::lock_guard<std::mutex> gm(m->mu);
+  std::unique_lock<std::mutex> gm(m->mu);
   if (m->state == CommState::kPendingAbort) return 0;
   if (m->state == CommState::kCreating) {
     {
@@ -653,6 +654,13 @@ int pptk_rx_comm_abort(struct pptk_rx_ctx *c) {
     m->job->cv.notify_all();
     return 0;
   }
+  // A live communicator: RCCL's abort can block while its kernels drain, so
+  // it runs under the communicator's own lock only -- every other context's
+  // create, destroy and abort go on meanwhile.  Nothing frees this RxComm
+  // while its lock is held: a live slot is deleted only by
+  // pptk_rx_comm_destroy / pptk_rx_ctx_destroy of this context (which must
+  // not race with this call, pptk_rx.h) after taking the same lock.
+  g.unlock();
   const Rccl *R = rccl();
   if (!R) return -ENOSYS;
   DeviceScope ds(ctx_device(c));

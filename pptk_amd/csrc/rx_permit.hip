@@ -63,6 +63,7 @@
 #include <unordered_map>
 #include <utility>
 
+#include <hip/hip_ext.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
@@ -1633,13 +1634,18 @@ std::unordered_map<const void *, std::pair<uint64_t, uint64_t>> g_status;   // f
 // The previous fused launch of each device, which the next one on another
 // stream waits for: two fused grids running at once could split the CUs
 // between them and each wait at its barrier for workgroups that cannot
-// become resident.  An event per device, recorded after every
-// fused launch (a marker on the same stream; no host wait).
+// become resident.  An event per device, the stop event of
+// every fused launch once the device has seen them from two streams.
+// (A/B builds: PPTK_PERMIT_ORDER=0, no order)
+#ifndef PPTK_PERMIT_ORDER
+#define PPTK_PERMIT_ORDER 1
+#endif
 struct FusedOrder {
   std::mutex mu;
   hipEvent_t ev = nullptr;
   hipStream_t last = nullptr;
-  bool any = false;
+  bool any = false;     // a fused launch was made on this device
+  bool multi = false;   // ... from more than one stream: launches record ev
 };
 FusedOrder g_order[64];
 
@@ -1720,9 +1726,17 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
                                                     hipEventDisableSystemFence) != hipSuccess &&
         (e = hipEventCreateWithFlags(&o.ev, hipEventDisableTiming)) != hipSuccess)
       return e;
-#ifndef PPTK_PERMIT_NO_ORDER   // (A/B: the launch order's cost)
-    if (o.any && o.last != st && (e = hipStreamWaitEvent(st, o.ev, 0)) != hipSuccess) return e;
-#endif
+    if (PPTK_PERMIT_ORDER && o.any && o.last != st) {
+      // The first time a second stream shows up, the launches so far carry
+      // no event (a process that issues every call on one stream never pays
+      // for one): wait for the device once, then order by event from here on.
+      if (!o.multi) {
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+        o.multi = true;
+      } else if ((e = hipStreamWaitEvent(st, o.ev, 0)) != hipSuccess) {
+        return e;
+      }
+    }
     const uint64_t k = g_nonce_ctr.fetch_add(1);
     f.nonce = nonce_of(k);
     {
@@ -1731,11 +1745,15 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
       if (it == g_status.end()) g_status.emplace(scratch, std::make_pair(k, k));
       else it->second.second = k;
     }
-    hipLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, a, f);
+    if (PPTK_PERMIT_ORDER && o.multi) {
+      // the order event as the launch's own stop event (2.2 us per call;
+      // a separate hipEventRecord behind the kernel cost 3.6)
+      hipExtLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, nullptr, o.ev, 0,
+                            a, f);
+    } else {
+      hipLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, a, f);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-#ifndef PPTK_PERMIT_NO_ORDER
-    if ((e = hipEventRecord(o.ev, st)) != hipSuccess) return e;
-#endif
     o.last = st;
     o.any = true;
     return hipSuccess;

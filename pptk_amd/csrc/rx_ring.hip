@@ -272,7 +272,7 @@ int pptk_rx_gather_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   if (!c || !b || !sp || !out) return -EINVAL;
   memset(out, 0, sizeof(*out));
   const uint32_t ncand0 = sp->cands ? sp->cands : 8;
-  const uint32_t reps = sp->reps ? sp->reps : 4;
+  const uint32_t reps = sp->reps ? sp->reps : 5;
   if (sp->nranks < 1 || sp->rank < 0 || sp->rank >= sp->nranks || sp->per_rank == 0 ||
       b->n > sp->per_rank || ncand0 > 16 || reps > 20 || sp->reserved ||
       (sp->flags & ~(uint32_t)PPTK_RX_RING_SETTLE) ||
@@ -307,42 +307,78 @@ int pptk_rx_gather_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   for (uint32_t k = 0; k < nc; ++k)
     if ((k > 0 && !alloc(spacer, spacers)) || !alloc(2 * nb, cands)) break;
   hipStream_t side = nullptr;
-  hipEvent_t ev = nullptr;
+  hipEvent_t ev = nullptr, te[3] = {nullptr, nullptr, nullptr};
   int err = 0;
   if (cands.empty() || hipMalloc(&src, srcb) != hipSuccess) err = -ENOMEM;
   if (!err && (hipMemsetAsync(src, 0, srcb, s) != hipSuccess ||
                hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess ||
                hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess))
     err = -EIO;
+  for (int k = 0; k < 3 && !err; ++k)
+    if (hipEventCreate(&te[k]) != hipSuccess) err = -EIO;
   nc = (uint32_t)cands.size();
-  std::vector<float> ms(nc, 0.f);
-  for (uint32_t k = 0; k < nc && !err; ++k) {
-    std::chrono::steady_clock::time_point t0;
-    for (uint32_t r = 0; r < reps + 2 && !err; ++r) {
-      if (r == 2) {   // two untimed warm-up batches per candidate
-        if (hipStreamSynchronize(s) != hipSuccess || hipStreamSynchronize(side) != hipSuccess) {
-          err = -EIO;
-          break;
-        }
-      }
-      if (r == 2) t0 = std::chrono::steady_clock::now();
-      uint8_t *half = (uint8_t *)cands[k] + (r & 1) * nb;
-      pptk_rx_dev_batch bb = *b;
-      bb.d_hash = (uint64_t *)(half + lo);
-      if ((err = pptk_rx_batch_device(c, &bb, stream)) != 0) break;
-      if (hipEventRecord(ev, s) != hipSuccess || hipStreamWaitEvent(side, ev, 0) != hipSuccess ||
-          (lo && hipMemcpyAsync(half, src, lo, hipMemcpyDeviceToDevice, side) != hipSuccess) ||
-          (nb > hi &&
-           hipMemcpyAsync(half + hi, src, nb - hi, hipMemcpyDeviceToDevice, side) != hipSuccess))
-        err = -EIO;
-      if (r == reps + 1 && !err) {
-        if (hipStreamSynchronize(s) != hipSuccess || hipStreamSynchronize(side) != hipSuccess)
-          err = -EIO;
-        ms[k] = (float)(std::chrono::duration<double, std::milli>(
-                            std::chrono::steady_clock::now() - t0).count() / reps);
+  // One batch into half h of candidate k, then (second stream) the bytes the
+  // gather would land in the rest of that half, beside the NEXT launch -- as
+  // in an rx loop, where batch k's gather overlaps batch k + 1.
+  auto batch = [&](uint32_t k, int h) {
+    uint8_t *half = (uint8_t *)cands[k] + (uint64_t)h * nb;
+    pptk_rx_dev_batch bb = *b;
+    bb.d_hash = (uint64_t *)(half + lo);
+    int e = pptk_rx_batch_device(c, &bb, stream);
+    if (e) return e;
+    if (hipEventRecord(ev, s) != hipSuccess || hipStreamWaitEvent(side, ev, 0) != hipSuccess ||
+        (lo && hipMemcpyAsync(half, src, lo, hipMemcpyDeviceToDevice, side) != hipSuccess) ||
+        (nb > hi &&
+         hipMemcpyAsync(half + hi, src, nb - hi, hipMemcpyDeviceToDevice, side) != hipSuccess))
+      return -EIO;
+    return 0;
+  };
+  auto drain = [&]() {
+    return hipStreamSynchronize(s) == hipSuccess && hipStreamSynchronize(side) == hipSuccess
+               ? 0 : -EIO;
+  };
+  // Warm-up: clocks ramp over the first few hundred ms of sustained load;
+  // without it the first candidates probed look slower than the rest.
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; !err; ++r) {
+      err = batch(0, r & 1);
+      if (!err && (r & 7) == 7) {
+        err = drain();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(300)) break;
       }
     }
   }
+  // Rounds over the candidates (drift falls on all alike); per visit one
+  // untimed batch (the previous candidate's gather copies are beside it),
+  // then two timed by events on the batch stream: kernel durations with
+  // this candidate's gather writes beside them.  Median per candidate.
+  std::vector<std::vector<float>> samp(nc);
+  for (uint32_t r = 0; r < reps && !err; ++r) {
+    for (uint32_t k = 0; k < nc && !err; ++k) {
+      if ((err = batch(k, 0)) != 0) break;
+      if (hipEventRecord(te[0], s) != hipSuccess) err = -EIO;
+      if (!err) err = batch(k, 1);
+      if (!err && hipEventRecord(te[1], s) != hipSuccess) err = -EIO;
+      if (!err) err = batch(k, 0);
+      if (!err && hipEventRecord(te[2], s) != hipSuccess) err = -EIO;
+      if (!err) err = drain();
+      float m1 = 0.f, m2 = 0.f;
+      if (!err && (hipEventElapsedTime(&m1, te[0], te[1]) != hipSuccess ||
+                   hipEventElapsedTime(&m2, te[1], te[2]) != hipSuccess))
+        err = -EIO;
+      samp[k].push_back(m1);
+      samp[k].push_back(m2);
+    }
+  }
+  std::vector<float> ms(nc, 0.f);
+  for (uint32_t k = 0; k < nc && !err; ++k) {
+    std::vector<float> &v = samp[k];
+    std::sort(v.begin(), v.end());
+    ms[k] = v.empty() ? 0.f : v[v.size() / 2];
+  }
+  for (hipEvent_t x : te)
+    if (x) (void)hipEventDestroy(x);
   if (side) {
     (void)hipStreamSynchronize(side);
     (void)hipStreamDestroy(side);
@@ -377,6 +413,7 @@ int pptk_rx_gather_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *
   out->chosen_ms = ms[best];
   out->first_ms = ms[0];
   out->freed_bytes = freed;
+  for (uint32_t k = 0; k < nc; ++k) out->cand_ms[k] = ms[k];
   if (sp->flags & PPTK_RX_RING_SETTLE) {
     const double sec = (double)freed / kScrubBytesPerS;
     std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(sec * 1e6)));

@@ -57,10 +57,11 @@ class RxGatherC(ctypes.Structure):
                 ("nranks", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("cands", ctypes.c_uint32), ("chosen", ctypes.c_int32),
                 ("chosen_ms", ctypes.c_float), ("first_ms", ctypes.c_float),
-                ("settle_ms", ctypes.c_uint32), ("freed_bytes", ctypes.c_uint64)]
+                ("settle_ms", ctypes.c_uint32), ("freed_bytes", ctypes.c_uint64),
+                ("cand_ms", ctypes.c_float * 16)]
 
 
-assert ctypes.sizeof(RxGatherSpec) == 40 and ctypes.sizeof(RxGatherC) == 64
+assert ctypes.sizeof(RxGatherSpec) == 40 and ctypes.sizeof(RxGatherC) == 128
 
 
 class RxRingC(ctypes.Structure):
@@ -133,6 +134,7 @@ class DeviceGather:
         self.report = {"candidates": g.cands, "chosen": g.chosen,
                        "chosen_ms": round(g.chosen_ms, 4), "first_ms": round(g.first_ms, 4),
                        "freed_bytes": g.freed_bytes, "settle_ms": g.settle_ms,
+                       "candidate_ms": [round(x, 4) for x in g.cand_ms[:g.cands]],
                        "alloc": "pptk_rx_gather_alloc"}
 
 

@@ -168,9 +168,9 @@ def test_bench_one_rank_rccl_path(tmp_path, frames, scaling):
     assert g["rccl_ranks"] == 1 and g["bytes_per_rank"] == frames * 8
     assert g["gathered_check"]["own_slice_equals_records"]
     assert g["gathered_check"]["sampled_mismatches"] == 0
-    p = line["parity"]
-    assert p["oracle_sample"]["mismatches"] == 0 and all(
-        v for k, v in p["full_batch"].items() if k != "corrupted")
+    c = line["configs"]["c1500"]
+    assert c["oracle_mismatches"] == 0 and c["verdicts_ok"] is True
+    assert g["placement"]["alloc"] == "pptk_rx_gather_alloc"
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
