@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ instruction counters (VALU/SALU/LDS/VMEM per dispatch) for one config:
-#   gpurun -- bash scripts/gpu_pmc_sq.sh c64
+#   gpurun -- bash profiles/r01/scripts/gpu_pmc_sq.sh c64
 source scripts/gpu_steps.sh
 export TMPDIR=/tmp
 c=${1:-c64}

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Final-tree evidence of this round (profiles/r02): scripts/gpu_r02_main.sh
+# Final-tree evidence of this round (profiles/r02): profiles/r02/scripts/gpu_r02_main.sh
 # (GPU suite, smoke, the default bench under kernel tracing, FETCH/WRITE
 # passes of the rx kernels) plus the rate limiter's trace and traffic.
-bash scripts/gpu_r02_main.sh || exit $?
+bash profiles/r02/scripts/gpu_r02_main.sh || exit $?
 source scripts/gpu_steps.sh
 export TMPDIR=/tmp
 O=gpurun_out/r02p

@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ instruction counters of one config under diagnostic tune flags
 # (PPTK_RX_TUNE, include/pptk_rx.h: 16 = skip the per-frame phase, 8 = skip
-# record stores), e.g.  gpurun -- bash scripts/gpu_sq_diag.sh cmix 32 48 40
+# record stores), e.g.  gpurun -- bash profiles/r03/scripts/gpu_sq_diag.sh cmix 32 48 40
 source scripts/gpu_steps.sh
 export TMPDIR=/tmp
 c=$1

@@ -28,4 +28,4 @@ rc=$?; echo "ab cmix rc=$rc"; cat gpurun_out/r04c/ab_cmix.json | cut -c1-700
 timeout -k 10 300 python -u tools/ab.py c1500 4:1 14:1 3:1 > gpurun_out/r04c/ab_c1500.json 2> gpurun_out/r04c/ab_c1500.log
 rc=$?; echo "ab c1500 rc=$rc"; cat gpurun_out/r04c/ab_c1500.json | cut -c1-700
 [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_r04_sq.sh
+bash profiles/r04/scripts/gpu_r04_sq.sh
