@@ -37,6 +37,47 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+_ROCTX = []
+
+
+def roctx_range(name):
+    """A ROCTx range around a timed region when PPTK_BENCH_ROCTX=1, so that a
+    `rocprofv3 --kernel-trace --marker-trace --kernel-rename --stats` run
+    reports the timed launches under the range's name, apart from the
+    placement probes, autotune trials and warm-up launches of the same
+    kernel (profiles/ READMEs: the summary's average is then exactly the
+    timed steps').  A no-op otherwise."""
+    import contextlib
+    if os.environ.get("PPTK_BENCH_ROCTX") != "1":
+        return contextlib.nullcontext()
+    if not _ROCTX:
+        import ctypes
+        L = None
+        for nm in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"):
+            try:
+                L = ctypes.CDLL(nm)
+                break
+            except OSError:
+                continue
+        if L is not None:
+            L.roctxRangePushA.argtypes = [ctypes.c_char_p]
+            L.roctxRangePushA.restype = ctypes.c_int
+            L.roctxRangePop.restype = ctypes.c_int
+        _ROCTX.append(L)
+    L = _ROCTX[0]
+    if L is None:
+        return contextlib.nullcontext()
+
+    @contextlib.contextmanager
+    def rng():
+        L.roctxRangePushA(name.encode())
+        try:
+            yield
+        finally:
+            L.roctxRangePop()
+    return rng()
+
+
 def dist_on(ws):
     """A process group exists: N > 1, or PPTK_BENCH_FORCE_DIST=1 (a one-rank
     RCCL communicator, to exercise the all-gather path on a one-GPU box)."""
@@ -371,11 +412,12 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     t0 = time.perf_counter()
-    for k in range(steps):
-        ev[k][0].record(main)
-        step(k)
-        ev[k][1].record(main)
-    barrier(ws, dev)
+    with roctx_range(f"timed_{cfg}{'_rec32' if compact else ''}"):
+        for k in range(steps):
+            ev[k][0].record(main)
+            step(k)
+            ev[k][1].record(main)
+        barrier(ws, dev)
     wall = time.perf_counter() - t0
     wall = max_over_ranks(wall, ws, dev)
     # kernel-only duration: the rx launch is the only work between the

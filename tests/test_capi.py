@@ -537,6 +537,13 @@ def test_entry_points_reject_bad_arguments(lib):
     assert lib.pptk_rx_ring_alloc(None, ctypes.byref(spec), ctypes.byref(ring), None) == EINVAL
     assert lib.pptk_rx_ring_free(None) == EINVAL
     assert lib.pptk_rx_ring_free(ctypes.byref(ring)) == 0   # an empty ring: nothing to free
+    from pptk_amd.rx import RxGatherC, RxGatherSpec
+    gs, g = RxGatherSpec(16, 1, 0), RxGatherC()
+    assert lib.pptk_rx_gather_alloc(None, ctypes.byref(b), ctypes.byref(gs), ctypes.byref(g),
+                                    None) == EINVAL
+    assert lib.pptk_rx_gather_free(None) == EINVAL
+    assert lib.pptk_rx_gather_free(ctypes.byref(g)) == 0    # empty: nothing to free
+    assert lib.pptk_rx_permit_status(None, None, None) == EINVAL
     lib.pptk_rx_ctx_destroy(None)                           # a no-op
 
 
@@ -580,3 +587,30 @@ def test_permit_pmc_summary(tmp_path):
                 w.writerow([i, "rx_kernel", cname, 99999.0])
     fe = permit_pmc.per_kernel(str(tmp_path / "pmc_keys_FETCH_SIZE"), "FETCH_SIZE")
     assert list(fe) == ["permit_fused"] and abs(fe["permit_fused"] - 1100 * 1024 / 1e6) < 1e-9
+
+
+def test_ctypes_structs_match_the_header(tmp_path):
+    """The ctypes mirrors of the C-ABI's structs (pptk_amd/rx.py) have the
+    size and field offsets gcc gives the header's structs."""
+    from pptk_amd import rx as R
+    structs = {"pptk_rx_opts": R.RxOpts, "pptk_rx_dev_batch": R.RxDevBatch,
+               "pptk_rx_ring_spec": R.RxRingSpec, "pptk_rx_ring": R.RxRingC,
+               "pptk_rx_gather_spec": R.RxGatherSpec, "pptk_rx_gather": R.RxGatherC}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "pptk_rx.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} sizeof %zu\\n", sizeof(struct {cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'  printf("{cname} {fname} %zu\\n", offsetof(struct {cname}, {fname}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = str(tmp_path / "layout")
+    subprocess.check_call(["gcc", "-std=gnu11", "-Wall", "-Werror", "-I", INCLUDE, str(src), "-o", exe])
+    got = {}
+    for line in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.splitlines():
+        c, f, v = line.split()
+        got[(c, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
