@@ -1008,6 +1008,14 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
   Desc dc = load_desc<GATHER>(a, tile, lane);
   Desc dn = load_desc<GATHER>(a, tile + step, lane);
   uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * step, lane);
+#ifdef PPTK_RX_WGFLUSH
+  // (A/B build: the workgroup's waves flush their records together -- their
+  // four tiles are consecutive, 16 KB of records -- after a barrier; every
+  // wave runs the workgroup's trip count, past-the-end tiles as dead rounds)
+  const bool wgf = !blocked;
+#else
+  constexpr bool wgf = false;
+#endif
   // prologue: the first D rounds of the first tile, in slots 0 .. D-1
   Buf<S> b[D + 1];
   // (issued strictly in slot order: the loop-header wait is computed from
@@ -1019,7 +1027,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  while (tile < tend) {
+  while (wgf ? tile - (uint64_t)wv < ntiles : tile < tend) {
     uint32_t my_sum = 0;
     // Descriptors run ahead in two stages so that no wait on them ever has
     // to drain the chunk loads in flight: the index (perm) of tile + 3 nwaves
@@ -1126,7 +1134,8 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
       // program order) for the coalesced store below
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
     }
-    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
+    if (wgf) __builtin_amdgcn_s_barrier();   // (no fence: each wave reads only its own slots)
+    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32) && tile < ntiles)   // tune bit 3: diagnostics, no stores
       flush_records(a, wimg, tile, lane, dc.idx, scatter);
     tile += step;
     dc = dn;

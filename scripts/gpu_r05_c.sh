@@ -16,4 +16,11 @@ rc=$?; echo "ab_permit $tok rc=$rc"; cat gpurun_out/r05c/ab_permit_$tok.json
 done
 PPTK_BENCH_FORCE_DIST=1 timeout -k 10 500 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 20 --warmup 5 --no-secondary --no-cpu --no-live-pmc --detail gpurun_out/r05c/dist1_detail.json > gpurun_out/r05c/bench_dist1.json 2> gpurun_out/r05c/bench_dist1.log
 rc=$?; echo "dist1 rc=$rc"; tail -c 1200 gpurun_out/r05c/bench_dist1.json
+[ $rc -eq 0 ] || exit $rc
+for cfg in cmix c1500; do
+AB_PLACE=1 AB_ROUNDS=6 AB_LIBS=wgf=tools/ab_libs/wgflush.so timeout -k 10 300 python -u tools/ab.py $cfg -1:-1 wgf:-1:-1 > gpurun_out/r05c/ab_wgflush_$cfg.json 2> gpurun_out/r05c/ab_wgflush_$cfg.log
+rc=$?; echo "ab wgflush $cfg rc=$rc"; python3 -c "
+import json; d=json.load(open('gpurun_out/r05c/ab_wgflush_$cfg.json')); print({k: v for k, v in d.items() if ':' in k})"
+[ $rc -eq 0 ] || exit $rc
+done
 exit $rc
