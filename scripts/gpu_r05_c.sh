@@ -18,7 +18,7 @@ PPTK_BENCH_FORCE_DIST=1 timeout -k 10 500 python -u -m torch.distributed.run --n
 rc=$?; echo "dist1 rc=$rc"; tail -c 1200 gpurun_out/r05c/bench_dist1.json
 [ $rc -eq 0 ] || exit $rc
 for cfg in cmix c1500; do
-AB_PLACE=1 AB_ROUNDS=6 AB_LIBS=wgf=tools/ab_libs/wgflush.so timeout -k 10 300 python -u tools/ab.py $cfg -1:-1 wgf:-1:-1 > gpurun_out/r05c/ab_wgflush_$cfg.json 2> gpurun_out/r05c/ab_wgflush_$cfg.log
+AB_PLACE=1 AB_ROUNDS=6 AB_LIBS=wgf=tools/ab_libs/wgflush.so timeout -k 10 300 python -u tools/ab.py $cfg 3:-1 wgf:3:-1 > gpurun_out/r05c/ab_wgflush_$cfg.json 2> gpurun_out/r05c/ab_wgflush_$cfg.log
 rc=$?; echo "ab wgflush $cfg rc=$rc"; python3 -c "
 import json; d=json.load(open('gpurun_out/r05c/ab_wgflush_$cfg.json')); print({k: v for k, v in d.items() if ':' in k})"
 [ $rc -eq 0 ] || exit $rc
