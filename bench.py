@@ -261,7 +261,7 @@ def placed_buffers(ctx, b, n, dev, compact, kw, frames=True, nf=PLACE_FRAMES,
     return recs, report
 
 
-def ring_buffers(ctx, b, n, dev, compact):
+def ring_buffers(ctx, b, n, dev, compact, probe_hash=False):
     """The product's default device rings (pptk_rx_ring_alloc): the library
     allocates frame and record candidates spread apart in HBM, probes every
     pair with a synthetic batch of the ring's geometry and keeps the fastest
@@ -270,7 +270,8 @@ def ring_buffers(ctx, b, n, dev, compact):
     the ring's frame buffer.  Returns (recs, report)."""
     fbytes = b["frames"].numel() - 64
     probe = b.get("fixed_len") or 1500
-    ring = ctx.ring_alloc(fbytes, n, 32 if compact else 64, probe_len=min(1536, max(64, probe)))
+    ring = ctx.ring_alloc(fbytes, n, 32 if compact else 64, probe_len=min(1536, max(64, probe)),
+                          probe_hash=probe_hash)
     ring.frames.copy_(b["frames"])
     b["frames"] = ring.frames
     report = dict(ring.report)

@@ -618,6 +618,11 @@ int pptk_rx_place_records(struct pptk_rx_ctx *ctx, const struct pptk_rx_dev_batc
  * freed_bytes says how much was freed.  -EINVAL for a bad spec, -ENOMEM if
  * not even one pair fits.  Release with pptk_rx_ring_free. */
 #define PPTK_RX_RING_SETTLE 0x1
+/* The queue's batches will also write the dense flow hashes (d_hash, the
+ * multi-GPU gather's send slice): the probe batches write them too (into a
+ * scratch buffer freed with the candidates), so the pair kept is the best
+ * for all three write streams, not for the records alone. */
+#define PPTK_RX_RING_PROBE_HASH 0x2
 struct pptk_rx_ring_spec {
   uint64_t frame_bytes;   /* frame ring bytes (the ring stays readable 64 B past it) */
   uint64_t nrec;          /* records the record ring holds (<= 2^32 - 1) */
@@ -626,7 +631,7 @@ struct pptk_rx_ring_spec {
   uint32_t frame_cands;   /* 0 = 3 */
   uint32_t rec_cands;     /* 0 = 8 */
   uint32_t reps;          /* timed probe launches per pair, 0 = 3 */
-  uint32_t flags;         /* PPTK_RX_RING_SETTLE */
+  uint32_t flags;         /* PPTK_RX_RING_SETTLE | PPTK_RX_RING_PROBE_HASH */
   uint64_t budget_bytes;  /* device memory the call may hold at once (candidates
                              and spacers included), 0 = 60 % of the free memory */
   uint64_t reserved;      /* 0 */

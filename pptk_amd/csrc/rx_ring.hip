@@ -125,7 +125,7 @@ int pptk_rx_ring_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_ring_spec *sp
   const uint32_t reps = sp->reps ? sp->reps : 3;
   if ((rb != 64 && rb != 32) || sp->frame_bytes == 0 || sp->nrec == 0 || plen < 64 ||
       plen > 1536 || nf0 > 8 || nr0 > 16 || reps > 20 || sp->nrec > 0xffffffffull ||
-      (sp->flags & ~(uint32_t)PPTK_RX_RING_SETTLE) || sp->reserved)
+      (sp->flags & ~(uint32_t)(PPTK_RX_RING_SETTLE | PPTK_RX_RING_PROBE_HASH)) || sp->reserved)
     return -EINVAL;
   // the probe batch: fixed-stride frames of probe_len bytes over the frame
   // ring (up to nrec of them)
@@ -182,6 +182,10 @@ int pptk_rx_ring_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_ring_spec *sp
   int err = 0;
   nf = (uint32_t)fc.size();
   nr = (uint32_t)rc.size();
+  // the probe's dense hashes (PPTK_RX_RING_PROBE_HASH), allocated after the
+  // candidates and freed with them
+  void *hbuf = nullptr;
+  if ((sp->flags & PPTK_RX_RING_PROBE_HASH) && alloc(n * 8, spacers)) hbuf = spacers.back();
   const uint64_t freed = allocated - fbytes - rbytes;   // all but the pair kept
 
   const uint64_t ndw = (n * plen + 3) / 4;
@@ -203,6 +207,7 @@ int pptk_rx_ring_alloc(struct pptk_rx_ctx *c, const struct pptk_rx_ring_spec *sp
     b.n = n;
     if (rb == 64) b.d_recs = (pptk_rx_rec *)rc[0];
     else b.d_recs32 = (pptk_rx_rec32 *)rc[0];
+    b.d_hash = (uint64_t *)hbuf;
     err = pptk_rx_place_buffers(c, &b, fptr.data(), (int)nf, rc.data(), (int)nr, (int)reps, &bf,
                                 &br, ms.data(), stream);
   }

@@ -77,6 +77,7 @@ class RxRingC(ctypes.Structure):
 
 
 RING_SETTLE = 0x1
+RING_PROBE_HASH = 0x2
 
 
 class _RingOwner:
@@ -480,12 +481,15 @@ class RxContext:
         return bf.value, br.value, [round(x, 4) for x in ms[:nf * nr]]
 
     def ring_alloc(self, frame_bytes, nrec, rec_bytes=64, probe_len=0, frame_cands=0,
-                   rec_cands=0, reps=0, settle=False, stream=None, budget_bytes=0):
+                   rec_cands=0, reps=0, settle=False, stream=None, budget_bytes=0,
+                   probe_hash=False):
         """pptk_rx_ring_alloc: placed device frame and record rings (a
-        DeviceRing; its .report carries the probe)."""
+        DeviceRing; its .report carries the probe).  probe_hash: the probe
+        batches also write dense flow hashes (PPTK_RX_RING_PROBE_HASH)."""
         import torch
         spec = RxRingSpec(frame_bytes, nrec, rec_bytes, probe_len, frame_cands, rec_cands, reps,
-                          RING_SETTLE if settle else 0, budget_bytes, 0)
+                          (RING_SETTLE if settle else 0) | (RING_PROBE_HASH if probe_hash else 0),
+                          budget_bytes, 0)
         ring = RxRingC()
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         rc = self._L.pptk_rx_ring_alloc(self._ctx, ctypes.byref(spec), ctypes.byref(ring),

@@ -4,7 +4,8 @@ what decides it.  On the library's rings (pptk_rx_ring_alloc, as bench.py),
 after the scrub: the batch without hashes, and with its hashes into the
 library-placed gather buffer (pptk_rx_gather_alloc) and into several fresh
 buffers allocated 4 GB apart -- interleaved rounds, median kernel ms.  Then
-the same on a second ring allocation (another frame/record placement).
+the same on a second ring allocation (another frame/record placement) and
+on a third placed with the hash stream in its probe (PPTK_RX_RING_PROBE_HASH).
 
     python tools/hash_probe.py [rounds]
 """
@@ -29,10 +30,12 @@ def main():
     n = bench.N_PER_GPU
     ctx = RxContext(0, bench.KEY)
     out = {"frames": n}
-    for ring_k in range(2):
+    for ring_k in range(3):
         b = make_batch("c1500", n, dev)
         kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
-        recs, rep = bench.ring_buffers(ctx, b, n, dev, False)
+        # rings 0 and 1: placed for the records alone (two allocations);
+        # ring 2: placed with the hash stream in the probe
+        recs, rep = bench.ring_buffers(ctx, b, n, dev, False, probe_hash=ring_k == 2)
         time.sleep(max(0.0, rep["_freed_at"] + rep["freed_bytes"] / bench.SCRUB_BYTES_PER_S
                        - time.perf_counter()))
         ctx.autotune(b["frames"], n, recs=recs, reps=5, **kw)
