@@ -72,6 +72,21 @@ def timed_launches(d, name, steps, gap_ms=20.0):
     return out
 
 
+def timed_range(d, cfg):
+    """The bench's timed launches of `cfg` as the traced run reports them
+    when run with PPTK_BENCH_ROCTX=1 under `rocprofv3 --marker-trace
+    --kernel-rename`: the kernels inside bench.py's ROCTx range
+    "timed_<cfg>" are renamed to it, so kernel_stats.csv has a row of
+    exactly the timed steps (no probe, autotune or settle launches)."""
+    ks = [r for r in rows(d, "*kernel_stats.csv") if r["Name"] == f"timed_{cfg}"]
+    if not ks:
+        return {}
+    return {"timed_range_calls": int(ks[0]["Calls"]),
+            "timed_range_avg_ms": float(ks[0]["AverageNs"]) / 1e6,
+            "timed_range_min_ms": float(ks[0]["MinNs"]) / 1e6,
+            "timed_range_max_ms": float(ks[0]["MaxNs"]) / 1e6}
+
+
 def op_counter(d, cname, regex):
     """Per-launch values of the kernels matching `regex` (all of them: an
     op's launches), and their durations."""
@@ -147,6 +162,7 @@ def main():
         e["pmc_pass_kernel_ms"] = sum(fd + wd) / len(fd + wd)
         if len(dirs) > 2:
             e.update(timed_launches(dirs[2], fname, int(os.environ.get("PMC_STEPS", "20"))))
+            e.update(timed_range(dirs[2], cfg))
         out[cfg] = e
     json.dump(out, open(sys.argv[1], "w"), indent=1)
     print(json.dumps(out, indent=1))
