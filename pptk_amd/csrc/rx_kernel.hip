@@ -805,12 +805,7 @@ __device__ __forceinline__ bool lane_fast(const RxKArgs &a, const uint32_t d[16]
 #ifndef PPTK_RX_HASH_MODE
 #define PPTK_RX_HASH_MODE 2
 #endif
-#ifndef PPTK_RX_PAIRS   // (A/B: two consecutive tiles per wave, one flush)
-#define PPTK_RX_PAIRS 0
-#endif
-#ifndef PPTK_RX_HASH_TEMPORAL   // (A/B: the staged hash run with temporal stores)
-#define PPTK_RX_HASH_TEMPORAL 0
-#endif
+
 
 // Record of frame `idx`: the optional dense flow-hash word, then the record
 // (64 bytes, or the 32-byte compact projection) either parked in the lane's
@@ -916,7 +911,9 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
   }
   // the tile's flow hashes (parked in each record slot's spare 16 bytes):
   // lanes 0..31 store two records' hashes each, one 512-byte run
-  if (PPTK_RX_HASH_MODE == 2 && a.hash && !scatter && lane < WAVE / 2) {
+  // (the same condition as emit_record's: !a.perm -- a permuted batch
+  // stored its hashes per lane)
+  if (PPTK_RX_HASH_MODE == 2 && a.hash && !scatter && !a.perm && lane < WAVE / 2) {
     const uint32_t r0 = 2u * (uint32_t)lane;
     if ((uint64_t)r0 < nrec) {
       const uint64_t h0 = *(const LDS_AS uint64_t *)(st + r0 * 5 + 4);
@@ -924,7 +921,7 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
       if ((uint64_t)r0 + 1 < nrec && ((uintptr_t)hd & 15u) == 0) {
         const uint64_t h1 = *(const LDS_AS uint64_t *)(st + (r0 + 1) * 5 + 4);
         const u64x2 v = {h0, h1};
-        if ((a.tune & 32u) && !PPTK_RX_HASH_TEMPORAL)
+        if (a.tune & 32u)
           __builtin_nontemporal_store(v, (GLB_AS u64x2 *)hd);
         else
           *(GLB_AS u64x2 *)hd = v;
@@ -991,7 +988,6 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     if (!group_range(a)) return;
   }
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * IMG_STRIDE];
-  __shared__ __attribute__((aligned(16))) uint8_t rlds[PPTK_RX_PAIRS ? WPB * WAVE * 80 : 16];
   constexpr int IMGC = (S * T < IMG_CHUNKS) ? S * T : IMG_CHUNKS;  // chunks parked
   constexpr uint32_t ALM = (1u << AL) - 1;
   static_assert(T % (D + 1) == 0, "prefetch ring must wrap at the tile boundary");
@@ -1011,30 +1007,10 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
   const uint64_t step = blocked ? 1 : nwaves;
   const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
 
-  // (A/B build PPTK_RX_PAIRS: each wave takes two consecutive tiles, 2 w
-  // and 2 w + 1, then jumps by 2 nwaves; the first tile's records wait in
-  // LDS of their own and both tiles' records (8 KB) and hashes (1 KB) go out
-  // as one run each -- half the write bursts)
-  const bool pairs = PPTK_RX_PAIRS && !blocked;
-  auto nxt = [&](uint64_t t) -> uint64_t {
-    return pairs ? ((t & 1) ? t - 1 + 2 * nwaves : t + 1) : t + step;
-  };
-  uint64_t tile = pairs ? 2 * wid : blocked ? wid * per : wid;
+  uint64_t tile = blocked ? wid * per : wid;
   Desc dc = load_desc<GATHER>(a, tile, lane);
-  Desc dn = load_desc<GATHER>(a, nxt(tile), lane);
-  uint32_t idx2 = desc_idx<GATHER>(a, nxt(nxt(tile)), lane);
-  LDS_AS u32x4 *const rpend = (LDS_AS u32x4 *)rlds + (PPTK_RX_PAIRS ? wv * WAVE * 5 : 0);
-  bool pend = false;        // the pair's first tile's records wait in rpend
-  uint64_t pend_tile = 0;
-  uint32_t pend_idx = 0;
-#ifdef PPTK_RX_WGFLUSH
-  // (A/B build: the workgroup's waves flush their records together -- their
-  // four tiles are consecutive, 16 KB of records -- after a barrier; every
-  // wave runs the workgroup's trip count, past-the-end tiles as dead rounds)
-  const bool wgf = !blocked;
-#else
-  constexpr bool wgf = false;
-#endif
+  Desc dn = load_desc<GATHER>(a, tile + step, lane);
+  uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * step, lane);
   // prologue: the first D rounds of the first tile, in slots 0 .. D-1
   Buf<S> b[D + 1];
   // (issued strictly in slot order: the loop-header wait is computed from
@@ -1046,13 +1022,13 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  while (wgf ? tile - (uint64_t)wv < ntiles : tile < tend) {
+  while (tile < tend) {
     uint32_t my_sum = 0;
     // Descriptors run ahead in two stages so that no wait on them ever has
     // to drain the chunk loads in flight: the index (perm) of tile + 3 nwaves
     // is loaded here, the dependent offset/length of tile + 2 nwaves (whose
     // index arrived during the previous tile) before the last round group.
-    const uint32_t idx3 = desc_idx<GATHER>(a, nxt(nxt(nxt(tile))), lane);
+    const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
     // the chunk holding the last byte of this lane's frame (for the
     // over-count correction of the unmasked team sums); issued before this
     // tile's rounds so that waiting for it never drains them
@@ -1123,12 +1099,11 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // the descriptors two tiles ahead are loaded BEFORE the last group issues
     // the next tile's first D rounds: the copies dc <- dn <- d2 at the tile
     // boundary then wait only for these loads, not for the rounds in flight
-    const Desc d2 = desc_fill<GATHER>(a, idx2, nxt(nxt(tile)), lane);
+    const Desc d2 = desc_fill<GATHER>(a, idx2, tile + 2 * step, lane);
     __builtin_amdgcn_sched_barrier(0);
     group(T - (D + 1));
 
     // ---- lane phase: frame `lane` -> record (parsed once per frame)
-    const bool first_of_pair = pairs && !(tile & 1);
     const bool stage = !(a.tune & 2u);
     const bool scatter = GATHER && a.perm;
     // tune bit 4 (diagnostics only, output invalid): skip the lane phase
@@ -1152,27 +1127,15 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
         a.txside[dc.idx] = o.tx;   // two-pass tx: 8 B per frame, coalesced in batch order
       // park the record in LDS (every lane's image reads are behind us in
       // program order) for the coalesced store below
-      emit_record(a, o, dc.idx, (first_of_pair ? rpend : (LDS_AS u32x4 *)wimg) + lane * 5, stage);
+      emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
     }
-    if (wgf) __builtin_amdgcn_s_barrier();   // (no fence: each wave reads only its own slots)
-    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32) && tile < ntiles) {   // tune bit 3: diagnostics, no stores
-      if (first_of_pair) {
-        pend = true;
-        pend_tile = tile;
-        pend_idx = dc.idx;
-      } else {
-        if (pend) flush_records(a, (const LDS_AS uint8_t *)rpend, pend_tile, lane, pend_idx, scatter);
-        pend = false;
-        flush_records(a, wimg, tile, lane, dc.idx, scatter);
-      }
-    }
-    tile = nxt(tile);
+    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
+      flush_records(a, wimg, tile, lane, dc.idx, scatter);
+    tile += step;
     dc = dn;
     dn = d2;
     idx2 = idx3;
   }
-  if (pend)   // a pair's first tile that had no second
-    flush_records(a, (const LDS_AS uint8_t *)rpend, pend_tile, lane, pend_idx, GATHER && a.perm);
 }
 
 // ---- Mixed-shape kernel (RX_M6): lanes binned by length inside each tile.
