@@ -187,15 +187,16 @@ def test_bench_validates_multi_gpu_line():
 
 
 def test_committed_forced_dist_line_passes():
-    """The one-rank RCCL bench line committed under profiles/ (round 4,
-    PPTK_BENCH_FORCE_DIST=1 on one MI355X) carries every N > 1 field and
-    passes bench.validate_line."""
+    """The one-rank RCCL bench lines committed under profiles/ (rounds 4 and
+    5, PPTK_BENCH_FORCE_DIST=1 on one MI355X; round 5's in the compact line
+    format) carry every N > 1 field and pass bench.validate_line."""
     import glob
     import json
     import sys
     sys.path.insert(0, ROOT)
     import bench
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "dist1", "bench_dist1*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "dist1", "bench_dist1*.json"))
+                   + glob.glob(os.path.join(ROOT, "profiles", "r05", "*", "bench_dist1*.json")))
     if not files:
         pytest.skip("no round-4 forced one-rank line committed yet")
     for f in files:
