@@ -433,3 +433,36 @@ def test_gather_alloc_rejects(dev):
             ctx.gather_alloc(frames, 10, *args, stride=64, fixed_len=64)
         assert e.value.errno == EINVAL, args
     ctx.close()
+
+
+def test_gather_alloc_n_rank_slice_probe(dev):
+    """pptk_rx_gather_alloc for rank 2 of 4 on one GPU (no collective: the
+    probe is rank-local): every probe launch lands the bytes the 4-rank
+    gather would -- device copies into the other three slices beside the
+    batch -- and the kept buffers come back zeroed; the kernel then writes
+    the golden hashes into rank 2's slice of either buffer, and nothing
+    else changes."""
+    from pptk_amd.rx import shard_range
+    from pptk_amd.shard import GatherBuffer
+    z = load_golden("fuzz")
+    ctx = _ctx(z)
+    n = len(z["off"])
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    kw = dict(off=off, lens=lens, max_len=int(z["len"].max()))
+    n_total = 4 * n
+    first, count, per = shard_range(n_total, 4, 2)
+    assert count == n
+    g = ctx.gather_alloc(frames, n, per, 4, 2, cands=2, reps=1, **kw)
+    assert g.report["candidates"] == 2 and len(g.report["candidate_ms"]) == 2
+    want = as_records(z["recs"])["flow_hash"]
+    for k in range(2):
+        gb = GatherBuffer(n_total, 4, 2, dev, out=g.out[k])
+        assert int(gb.out.abs().sum().item()) == 0
+        ctx.batch_device(frames, n, hash_out=gb.local[:n], **kw)
+        torch.cuda.synchronize()
+        got = gb.out.cpu().numpy().view(np.uint64)
+        assert np.array_equal(got[2 * per:2 * per + n], want), k
+        assert (got[:2 * per] == 0).all() and (got[2 * per + n:] == 0).all()
+    ctx.close()
