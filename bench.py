@@ -335,7 +335,9 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
         # pick a well-placed pair, untimed, as a long-lived rx ring would be
         # set up once (a reused batch keeps its frames: records only)
         if batch is None:
-            recs, placement = ring_buffers(ctx, b, n, dev, compact)
+            # (with a gather the batches also write the dense hashes: the
+            # ring probe writes them too, PPTK_RX_RING_PROBE_HASH)
+            recs, placement = ring_buffers(ctx, b, n, dev, compact, probe_hash=bool(gbs))
         else:
             recs, placement = placed_buffers(ctx, b, n, dev, compact, kw, frames=False,
                                              autotune=autotune)

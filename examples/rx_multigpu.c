@@ -158,7 +158,9 @@ static void *thrfn(void *arg)
   rs.nrec = count ? count : 1;
   rs.rec_bytes = sizeof(struct pptk_rx_rec);
   rs.probe_len = rs.frame_bytes >= 1500 ? 0 : (uint32_t)rs.frame_bytes;
-  rs.flags = PPTK_RX_RING_SETTLE;   /* the gather probe below runs after the scrub */
+  /* the gather probe below runs after the scrub; the ring probe writes the
+   * dense hashes too, as this queue's batches do */
+  rs.flags = PPTK_RX_RING_SETTLE | PPTK_RX_RING_PROBE_HASH;
   if ((t->rc = pptk_rx_ring_alloc(t->ctx, &rs, &ring, st)) != 0)
     goto out;
   CHECK_HIP(hipMalloc((void **)&d_off, count * 8 + 8));
