@@ -1108,3 +1108,40 @@ def test_m6_fixed_stride_forced(name, stride, dev):
             got = _run(ctx, z, dev, shift=shift, stride=stride, compact=True)
             d = diff_records(got, to_rec32(z["recs"]), dtype=REC32_DTYPE)
             assert not d, f"compact shift {shift} flags {flags}: {d}"
+
+
+@pytest.mark.parametrize("name,stride", [("c1500", 1500), ("c64", 64), ("cmix", None)])
+@pytest.mark.parametrize("compact", [False, True])
+def test_dense_hash_misaligned_and_ragged(name, stride, compact, dev):
+    """The dense flow-hash array (d_hash) as the flush stores it -- one run
+    of 16-byte stores per tile from the record slots' spare bytes -- into a
+    destination 8 bytes off a 16-byte boundary (a rank's slice of a gather
+    buffer with an odd per-rank count) and for a frame count that leaves the
+    last tile ragged: every hash equals the golden flow hash, the words
+    around the slice are untouched, every variant the batch may run, full
+    and compact records."""
+    from pptk_amd.rx import VARIANTS
+    z = load_golden(name)
+    n_all = len(z["off"])
+    n = n_all - 37 if n_all > 100 else n_all    # ragged last tile
+    zz = dict(z)
+    zz["off"], zz["len"], zz["recs"] = z["off"][:n], z["len"][:n], z["recs"][:n]
+    ctx = _ctx(z)
+    _keep, frames = _upload(zz["buf"], dev, 0)
+    kw = (dict(stride=stride, fixed_len=int(zz["len"][0])) if stride else
+          dict(off=torch.from_numpy(zz["off"].view(np.int64)).to(dev),
+               lens=torch.from_numpy(zz["len"].view(np.int16)).to(dev),
+               max_len=int(zz["len"].max())))
+    want = as_records(zz["recs"])["flow_hash"]
+    variants = [-1] + ([VARIANTS.index(v) for v in ("T16S6", "T16S7L", "M6")] if name != "c64"
+                       else [VARIANTS.index(v) for v in ("L4", "T4S2", "M6")])
+    for v in variants:
+        ctx.set_tuning(v, -1)
+        big = torch.full((n + 3,), -7, dtype=torch.int64, device=dev)
+        assert (big[1:].data_ptr() % 16) == 8
+        ctx.batch_device(frames, n, hash_out=big[1:n + 1], compact=compact, **kw)
+        torch.cuda.synchronize()
+        got = big.cpu().numpy()
+        assert np.array_equal(got[1:n + 1].view(np.uint64), want), VARIANTS[ctx.last_variant()]
+        assert got[0] == -7 and (got[n + 1:] == -7).all()
+    ctx.close()
