@@ -575,6 +575,7 @@ def compact_line(full, detail_path=None):
     src = r.get("traffic_source") or ""
     line["roofline"]["traffic_source"] = "live rocprofv3 PMC" if src.startswith("live") else src
     cpu = full.get("cpu_baseline")
+    line["cpu_baseline"] = None           # (rank 0 of a one-GPU run only)
     if cpu:
         line["cpu_baseline"] = {k: cpu.get(k) for k in ("value", "unit", "cores", "kind",
                                                         "single_thread_mpkts", "cpu_model")}
