@@ -1002,16 +1002,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
   // (experiment), a contiguous block of tiles per wave, so that one wave's
   // successive record flushes are adjacent in memory.
   const bool blocked = a.tune & 256u;
-#ifdef PPTK_RX_XCD_ORDER
-  // (A/B build: the waves of the blocks one XCD runs (blockIdx % 8) take
-  // consecutive tiles, so each XCD's L2 holds contiguous runs of records and
-  // hashes instead of every eighth group of four tiles)
-  const uint64_t wid = gridDim.x % 8 == 0
-                           ? ((uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8) * WPB + wv
-                           : (uint64_t)blockIdx.x * WPB + wv;
-#else
   const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
-#endif
   const uint64_t per = (ntiles + nwaves - 1) / nwaves;
   const uint64_t step = blocked ? 1 : nwaves;
   const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
@@ -1312,16 +1303,7 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
   const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
   const bool blocked = a.tune & 256u;
-#ifdef PPTK_RX_XCD_ORDER
-  // (A/B build: the waves of the blocks one XCD runs (blockIdx % 8) take
-  // consecutive tiles, so each XCD's L2 holds contiguous runs of records and
-  // hashes instead of every eighth group of four tiles)
-  const uint64_t wid = gridDim.x % 8 == 0
-                           ? ((uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8) * WPB + wv
-                           : (uint64_t)blockIdx.x * WPB + wv;
-#else
   const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
-#endif
   const uint64_t per = (ntiles + nwaves - 1) / nwaves;
   const uint64_t step = blocked ? 1 : nwaves;
   const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
