@@ -83,3 +83,8 @@ tools/librwmix.so: tools/rwmix.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
 all: tools/librwmix.so
+
+tools/libglds_probe.so: tools/glds_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
+
+all: tools/libglds_probe.so
