@@ -54,6 +54,7 @@ def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
     s = torch.cuda.current_stream(dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     best = (float("inf"), None)
+    shapes = {}
     for mode in (0, 1, 4, 5):
         m = mode | (2 if gather else 0)
         for mult in (2, 4, 8):
@@ -72,9 +73,12 @@ def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
                     ts.append(a.elapsed_time(b))
             ts.sort()
             med = ts[len(ts) // 2]
+            shapes[f"{'nt' if mode & 1 else 'plain'}_l{4 if mode & 4 else 16}_b{mult}"] = round(med, 4)
             if med < best[0]:
                 best = (med, {"nt": bool(mode & 1), "loads_in_flight": 4 if mode & 4 else 16,
                               "blocks_per_cu": mult * 1})
+    if os.environ.get("RWMIX_SOL_SHAPES"):   # every shape's median (A/B probes)
+        best[1]["shapes"] = shapes
     return best
 
 
