@@ -88,3 +88,8 @@ tools/libglds_probe.so: tools/glds_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
 all: tools/libglds_probe.so
+
+tools/libteam_probe.so: tools/team_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
+
+all: tools/libteam_probe.so
