@@ -479,27 +479,6 @@ __device__ __forceinline__ Buf<S> load_round(const RxKArgs &a, const Desc &d, in
   const u32x4 *c0 = (const u32x4 *)(a.frames + (b.pb - (uint64_t)m));
   const int nch = (m + (int)b.pl + 15) >> 4;
   const int clast = nch > 0 ? nch - 1 : 0;
-#ifdef PPTK_RX_PRED_LOADS
-  // (A/B build: lanes past the frame's last chunk load nothing; with 1 and
-  // the line-aligned grid, the two chunk groups that can hold the frame's
-  // last line load that line temporally and the rest non-temporally)
-  const int cl0 = clast & ~7;
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const int c = s * T + j;
-    const bool in = c <= clast;
-    if (PPTK_RX_PRED_LOADS == 1 && NT && AL == 7 && s >= S - 2) {
-      const bool tl = c >= cl0;
-      u32x4 x = (u32x4){0u, 0u, 0u, 0u}, t = x;
-      if (in && !tl) x = ldc<true>(c0 + c);
-      if (in && tl) t = c0[c];
-      b.v[s] = tl ? t : x;
-      continue;
-    }
-    b.v[s] = in ? ldc<NT>(c0 + c) : (u32x4){0u, 0u, 0u, 0u};
-  }
-  return b;
-#endif
   // Unconditional loads (chunks past the frame re-read its last chunk):
   // branch-free loads let the compiler count vmcnt precisely, so the D
   // rounds in flight are not drained at every use.
