@@ -103,6 +103,36 @@ def launch_ranks(argv, ngpus):
     raise SystemExit(subprocess.call(cmd))
 
 
+def join_all(ctx, ws, rank, join_fn=None):
+    """Join `ctx` to the job's RCCL communicator on every rank or on none.  A
+    rank whose creation fails (no RCCL, a peer that never joins: -ETIMEDOUT
+    after opts.comm_timeout_ms) tells the others over the gloo group; every
+    rank that did join then aborts and drops its communicator, and the run
+    goes on without the collective: the line carries allgather.error (and
+    fails validate_line, so the process still exits non-zero) beside the
+    sharded rates every rank measured.  Returns None or the error."""
+    if join_fn is None:
+        from pptk_amd.shard import join as join_fn
+    err = None
+    try:
+        join_fn(ctx, ws, rank)
+    except Exception as e:   # (RuntimeError from the C-ABI's -errno, or a missing librccl)
+        err = f"[rank {rank}] {type(e).__name__}: {e}"[:300]
+    if ws > 1:
+        import torch
+        import torch.distributed as dist
+        failed = torch.tensor([0 if err is None else 1], dtype=torch.int32)
+        dist.all_reduce(failed)
+        if int(failed.item()) and err is None:
+            err = f"{int(failed.item())} of {ws} ranks could not join the RCCL communicator"
+            for drop in (ctx.comm_abort, ctx.comm_destroy):
+                try:
+                    drop()
+                except Exception:   # (already gone: nothing to drop)
+                    pass
+    return err
+
+
 def dist_setup(ngpus):
     """One process per GPU.  The host control plane (barriers, max over
     ranks, the communicator uid) is a gloo group; the data-path collective
@@ -504,7 +534,9 @@ def validate_line(line):
         return ["n_gpus missing"]
     if ws > 1 and not gat:
         bad.append("N > 1 without an all-gather")
-    if gat:
+    if gat and gat.get("error"):
+        bad.append(f"all-gather failed: {gat['error']}")
+    elif gat:
         if line.get("config", {}).get("rccl_ranks") != ws:
             bad.append(f"config.rccl_ranks {line.get('config', {}).get('rccl_ranks')} != n_gpus {ws}")
         if gat.get("rccl_ranks") != ws:
@@ -617,7 +649,9 @@ def compact_line(full, detail_path=None):
     if ops:
         line["ops"] = ops
     gat = full.get("allgather")
-    if gat:
+    if gat and gat.get("error"):
+        line["allgather"] = {"error": gat["error"]}
+    elif gat:
         g = {k: gat.get(k) for k in ("ms", "algbw_gbs", "busbw_gbs", "overlap_loss", "rccl_ranks",
                                       "bytes_per_rank")}
         chk = gat.get("gathered_check") or {}
@@ -1318,7 +1352,7 @@ def main():
 
     import torch
     from pptk_amd.rx import RxContext
-    from pptk_amd.shard import GatherBuffer, join, shard_range
+    from pptk_amd.shard import GatherBuffer, shard_range
     ws, rank, dev = dist_setup(args.gpus)
     ctx = RxContext(dev.index, KEY)
     place = not args.no_place
@@ -1326,11 +1360,15 @@ def main():
     # (pptk_rx_shard_range: the last shards padded for the all-gather)
     n_total = args.frames * ws if args.scaling == "weak" else args.frames
     gbs = None
+    comm_error = None
     if dist_on(ws):
-        join(ctx, ws, rank)                       # RCCL communicator in libpptkrx.so
-        # the gather buffers are placed inside run_config, once the batch's
-        # frame and record buffers are (placed_gather)
-        gbs = "place" if place else [GatherBuffer(n_total, ws, rank, dev) for _ in range(2)]
+        comm_error = join_all(ctx, ws, rank)     # RCCL communicator in libpptkrx.so
+        if comm_error:
+            log(f"[rank {rank}] no all-gather: {comm_error}")
+        else:
+            # the gather buffers are placed inside run_config, once the
+            # batch's frame and record buffers are (placed_gather)
+            gbs = "place" if place else [GatherBuffer(n_total, ws, rank, dev) for _ in range(2)]
         first, n, _ = shard_range(n_total, ws, rank)
     else:
         first, n = 0, n_total
@@ -1530,7 +1568,7 @@ def main():
             "cpu_baseline": cpu,
             "value_no_gather": None if nog is None else round(nog["mpkts"], 1),
             "rec32": rec32,
-            "allgather": gat,
+            "allgather": gat if gat else ({"error": comm_error} if comm_error else None),
             "box_hbm": box,
             "parity": {"full_batch": full_check, "oracle_sample": sample_check},
             "secondary": secondary,

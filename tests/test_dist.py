@@ -122,6 +122,73 @@ def test_bench_multi_rank_helpers():
     assert alg == round(1024 * 2 * 8 / 1e-3 / 1e9, 1) and abs(bus - alg / 2) <= 0.1
 
 
+class _FakeCommCtx:
+    """Stands in for RxContext's communicator calls (no GPU, no RCCL)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def comm_abort(self):
+        self.calls.append("abort")
+
+    def comm_destroy(self):
+        self.calls.append("destroy")
+
+
+def _join_worker(rank, world, port, fail_ranks, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def join_fn(ctx, ws, r):
+            if r in fail_ranks:
+                raise RuntimeError("pptk_rx_comm_create: -110")
+        ctx = _FakeCommCtx()
+        err = bench.join_all(ctx, world, rank, join_fn)
+        q.put((rank, err, ctx.calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_ranks", [(), (1,), (0, 1)])
+def test_bench_joins_all_ranks_or_none(fail_ranks):
+    """bench.join_all on gloo, world 2: when one rank cannot create its RCCL
+    communicator every rank learns it, the ranks that did join abort and
+    drop theirs, and the run goes on without the collective; the line then
+    names the error and fails bench.validate_line (non-zero exit)."""
+    import bench
+    world, port = 2, 31700 + (os.getpid() % 1000) + 10 * len(fail_ranks)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, fail_ranks, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (e, c)) for r, e, c in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        err, calls = got[r]
+        if not fail_ranks:
+            assert err is None and calls == []
+        elif r in fail_ranks:
+            assert "-110" in err and calls == []
+        else:
+            assert "could not join" in err and calls == ["abort", "destroy"]
+    if fail_ranks:
+        full = {"n_gpus": world, "allgather": {"error": got[fail_ranks[0]][0]},
+                "per_rank_kernel_ms": [4.0] * world, "config": {"workload": "C1500: x"},
+                "roofline": {}}
+        line = bench.compact_line(full, detail_path=None)
+        assert line["allgather"] == {"error": got[fail_ranks[0]][0]}
+        probs = bench.validate_line(line)
+        assert len(probs) == 1 and probs[0].startswith("all-gather failed")
+
+
 def test_bench_launches_ranks_itself(tmp_path, monkeypatch):
     """`python bench.py --gpus N` outside a launcher starts N ranks through
     torch.distributed.run (the command it builds, not run here)."""
