@@ -93,3 +93,8 @@ tools/libteam_probe.so: tools/team_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
 all: tools/libteam_probe.so
+
+tools/libepoch_probe.so: tools/epoch_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
+
+all: tools/libepoch_probe.so

@@ -441,11 +441,33 @@ static int auto_variant(const pptk_rx_dev_batch *b, bool *lane_ok_out) {
   return lane_ok ? RX_L4 : pick_variant(maxlen + mmax);
 }
 
+// The write-phase period of a launch (rx_kernel.hip "Global write phases"):
+// ~0.75 of the time one wave takes for one 64-frame tile, estimated from the
+// tile's frame bytes (fixed-stride batches: 64 strides; offset-described
+// ones: 64 frames of half the max_len hint, as for lengths spread evenly up
+// to it), the waves of the grid, and ~5.5 TB/s of frame stream.  Measured:
+// the best periods lie at 0.6-0.9 of a tile (profiles/r05/w: C1500 30-40 us
+// against 47-51 us tiles, CMIX 15-20 us against 20 us).  0 (off) for the
+// small-frame shapes, permuted batches (records scatter) and tx batches.
+static uint32_t phase_ticks_for(const pptk_rx_dev_batch *b, int variant, int grid) {
+  static const long force = EXP_KNOB("PPTK_RX_PHASE_TICKS", -1);
+  if (force >= 0) return (uint32_t)force;
+  if (!rx_variant_phased(variant) || b->d_perm || (!b->d_recs && !b->d_recs32)) return 0;
+  const uint64_t maxlen = b->d_len ? (b->max_len ? b->max_len : 1518u) : b->fixed_len;
+  const uint64_t tile_bytes = 64 * (b->d_off ? std::max<uint64_t>(64, maxlen / 2)
+                                             : std::max<uint64_t>(b->stride, 64));
+  const uint64_t waves = (uint64_t)grid * 4;
+  const uint64_t ticks = tile_bytes * waves * 3 / 4 / 55000;   // 5.5 TB/s = 55 000 B per tick
+  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ticks, 100), 1000000);
+}
+
 static int launch_batch(pptk_rx_ctx *c, const pptk_rx_dev_batch *b, int variant, void *stream) {
   RxKArgs a = batch_args(c, b);
   a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm);
   c->last_variant = variant;
-  return hip_err(launch_rx(variant, a, grid_for(c, variant, b->n), (hipStream_t)stream));
+  const int grid = grid_for(c, variant, b->n);
+  a.phase_ticks = phase_ticks_for(b, variant, grid);
+  return hip_err(launch_rx(variant, a, grid, (hipStream_t)stream));
 }
 
 int pptk_rx_batch_device(struct pptk_rx_ctx *c, const struct pptk_rx_dev_batch *b,

@@ -100,6 +100,9 @@ struct RxKArgs {
   const uint64_t *off0;
   const uint16_t *len0;
   uint32_t plan_group;
+  // global write phases of the streaming shapes (rx_kernel.hip): the period
+  // in s_memrealtime ticks (10 ns); 0 = each tile's records at its end
+  uint32_t phase_ticks;
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S
@@ -129,6 +132,9 @@ constexpr uint32_t kGroupMaxLen[kGroups] = {113, 1521, 0xffffffffu};
 constexpr int kGroupVariant[kGroups] = {RX_T4S2, RX_T16S6, RX_T64S2};
 
 hipError_t launch_rx(int variant, const RxKArgs &a, int grid, hipStream_t s);
+// whether a variant's kernel holds records for the write phases (the
+// streaming team shapes; RxKArgs::phase_ticks)
+bool rx_variant_phased(int variant);
 // tx second pass: frames[base(i) + off] = value (big-endian) for the
 // fields txside[i] names; base(i) = off ? off[i] : i * stride
 hipError_t launch_tx_apply(const uint64_t *txside, uint8_t *frames, const uint64_t *off,

@@ -871,7 +871,8 @@ __device__ __forceinline__ void emit_record(const RxKArgs &a, const LaneRec &o, 
 // instead of one 16-byte piece of each of 64 records.  `my_idx` is the
 // lane's frame index (~0: no record).
 __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uint8_t *wimg, uint64_t tile,
-                                              int lane, uint32_t my_idx, bool scatter) {
+                                              int lane, uint32_t my_idx, bool scatter,
+                                              LDS_AS u32x4 *stash = nullptr) {
   const bool c32 = a.recs32 != nullptr;
   __builtin_amdgcn_wave_barrier();
   const LDS_AS u32x4 *st = (const LDS_AS u32x4 *)wimg;
@@ -895,7 +896,9 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
     }
     if (live && k < kmax) {
       const u32x4 val = st[r * 5 + piece];
-      if (a.tune & 64u) {            // bit 6: write-through, drop from L2 (sc1)
+      if (stash) {                   // (write-phase A/B build: held in LDS, stored later)
+        stash[e] = val;
+      } else if (a.tune & 64u) {     // bit 6: write-through, drop from L2 (sc1)
         GLB_AS uint64_t *d8 = (GLB_AS uint64_t *)d;
         __hip_atomic_store(d8, (uint64_t)val.x | ((uint64_t)val.y << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -932,6 +935,40 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
     }
   }
   __builtin_amdgcn_wave_barrier();
+}
+
+// Global write phases (RxKArgs::phase_ticks != 0).  The record writes beside
+// the frame stream cost the memory more than their bytes (DESIGN.md section
+// 7 "Placement"), and less when every wave's come together: a tile's record
+// run waits in the wave's LDS stash until the chip-wide clock
+// (s_memrealtime, 100 MHz, one clock for every CU) passes the next multiple
+// of phase_ticks -- checked between round groups -- or until the next
+// tile's run needs the stash, so the waves' record writes fall in the first
+// microseconds of each period instead of each at its own tile end.  The
+// host sets the period to ~0.75 of a tile's expected duration (rx_capi.hip
+// phase_ticks_for): C1500 4.036 -> 3.954 ms and 4.370 -> 4.102 ms on two
+// boxes, CMIX 2.541 -> 2.510 ms (profiles/r05/v, w).
+__device__ __forceinline__ uint64_t phase_deadline(uint32_t period) {
+  const uint64_t rt = __builtin_amdgcn_s_memrealtime();
+  return rt - rt % period + period;
+}
+__device__ __forceinline__ void flush_stash(const RxKArgs &a, const LDS_AS u32x4 *stash, uint64_t tile,
+                                            int lane) {
+  const bool c32 = a.recs32 != nullptr;
+  GLB_AS uint8_t *rbase = c32 ? (GLB_AS uint8_t *)a.recs32 : (GLB_AS uint8_t *)a.recs;
+  GLB_AS u32x4 *dst = (GLB_AS u32x4 *)(rbase + tile * (uint64_t)WAVE * (c32 ? 32u : 64u));
+  const uint64_t nrec = min((uint64_t)WAVE, a.n - tile * WAVE);
+  const int lg = c32 ? 1 : 2;
+  const int kmax = c32 ? 2 : 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = k * WAVE + lane;
+    if (k < kmax && (uint64_t)(e >> lg) < nrec) {
+      const u32x4 val = stash[e];
+      asm volatile("" ::: "memory");
+      __builtin_nontemporal_store(val, dst + e);
+    }
+  }
 }
 
 // Waves per SIMD the register allocator must leave room for: the streaming
@@ -991,11 +1028,21 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
   constexpr int IMGC = (S * T < IMG_CHUNKS) ? S * T : IMG_CHUNKS;  // chunks parked
   constexpr uint32_t ALM = (1u << AL) - 1;
   static_assert(T % (D + 1) == 0, "prefetch ring must wrap at the tile boundary");
+  // the streaming shapes up to 1536-byte frames hold a tile's records for
+  // the write phases (the small-frame shapes, four waves per SIMD, have no
+  // LDS to spare; the jumbo shape T64S2 measured slower with them: JMIX
+  // 3.832 -> 3.939 ms, profiles/r05/x)
+  constexpr bool PHASED = S * T >= 32 && T <= 32;
+  __shared__ __attribute__((aligned(16))) u32x4 stash_lds[PHASED ? WPB * 4 * WAVE : 1];
+  const bool phased = PHASED && a.phase_ticks != 0;
+  uint64_t st_tile = ~0ull;     // the tile whose records wait in the stash
+  uint64_t st_deadline = 0;
   constexpr bool UNROLL = T <= 32;   // tail chunks summed in the lane phase
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const int g = lane / T, j = lane % T;
   LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * IMG_STRIDE;
+  LDS_AS u32x4 *stash = (LDS_AS u32x4 *)stash_lds + (PHASED ? wv * 4 * WAVE : 0);
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
   const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
   // Tile order: strided over the grid (default), or, with tune bit 8
@@ -1094,8 +1141,13 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
 #else
 #pragma unroll 1
 #endif
-    for (int r0 = 0; r0 < T - (D + 1); r0 += D + 1)
+    for (int r0 = 0; r0 < T - (D + 1); r0 += D + 1) {
       group(r0);
+      if (PHASED && st_tile != ~0ull && __builtin_amdgcn_s_memrealtime() >= st_deadline) {
+        flush_stash(a, stash, st_tile, lane);
+        st_tile = ~0ull;
+      }
+    }
     // the descriptors two tiles ahead are loaded BEFORE the last group issues
     // the next tile's first D rounds: the copies dc <- dn <- d2 at the tile
     // boundary then wait only for these loads, not for the rounds in flight
@@ -1129,13 +1181,22 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
       // program order) for the coalesced store below
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
     }
-    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32))   // tune bit 3: diagnostics, no stores
-      flush_records(a, wimg, tile, lane, dc.idx, scatter);
+    if (stage && !(kDiag && (a.tune & 8u)) && (a.recs || a.recs32)) {  // tune bit 3: diagnostics, no stores
+      if (PHASED && phased && !scatter) {
+        if (st_tile != ~0ull) flush_stash(a, stash, st_tile, lane);   // the stash is needed
+        flush_records(a, wimg, tile, lane, dc.idx, scatter, stash);
+        st_tile = tile;
+        st_deadline = phase_deadline(a.phase_ticks);
+      } else {
+        flush_records(a, wimg, tile, lane, dc.idx, scatter);
+      }
+    }
     tile += step;
     dc = dn;
     dn = d2;
     idx2 = idx3;
   }
+  if (PHASED && st_tile != ~0ull) flush_stash(a, stash, st_tile, lane);
 }
 
 // ---- Mixed-shape kernel (RX_M6): lanes binned by length inside each tile.
@@ -1936,6 +1997,16 @@ hipError_t launch_rewrite(const RxKArgs &a, int grid, hipStream_t s) {
 hipError_t launch_mss_clamp(const RxKArgs &a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(rx_mss_kernel, dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
+}
+
+bool rx_variant_phased(int variant) {
+  switch (variant) {
+#define X(name, T, S, D, AL) \
+  case name: return S * T >= 32 && T <= 32;
+    PPTK_RX_VARIANTS(X)
+#undef X
+    default: return false;   // M6, L4: no stash
+  }
 }
 
 int rx_variant_blocks_per_cu(int variant) {

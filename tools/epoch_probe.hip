@@ -1,0 +1,75 @@
+// epoch_probe.hip -- PROBE TOOLING: does the record stream cost the frame
+// stream less when every wave writes its records in the same short window
+// (global write phases) instead of each at its own tile end?  One wave per
+// C1500-shaped tile (tiles strided over the grid's waves), the tile's bytes
+// read with non-temporal 16-byte loads, 8 in flight per lane, then the
+// tile's 4 KB record run written (non-temporal):
+//   MODE 0: right after the tile (the rx kernel's order)
+//   MODE 1: held until the chip-wide clock (s_memrealtime, 100 MHz) enters a
+//           new period of P ticks, checked after every 8 KB of reads, and
+//           written at the latest when the next tile's record is ready --
+//           every wave's writes fall in the first microseconds of a period.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE>
+__global__ __launch_bounds__(256) void epoch_kernel(const uint8_t *in, uint64_t ntiles,
+                                                    uint32_t tile_bytes, u32x4 *recs,
+                                                    uint64_t period, uint32_t *sink) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  const uint32_t nins = (tile_bytes + 1023) / 1024;
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 pend = acc;
+  uint64_t tpend = ~0ull, epend = 0;
+  auto flush = [&](uint64_t t, u32x4 v) {
+    u32x4 *q = recs + t * 256;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v, q + k * 64 + lane);
+  };
+  for (uint64_t t = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64; t < ntiles; t += nwaves) {
+    const uint8_t *base = in + t * (uint64_t)tile_bytes;
+    for (uint32_t i = 0; i < nins; i += 8) {
+      u32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t o = min((i + k) * 1024u + (uint32_t)lane * 16u, tile_bytes - 16u);
+        v[k] = __builtin_nontemporal_load((const u32x4 *)(base + o));
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc ^= v[k];
+      if (MODE == 1 && tpend != ~0ull) {
+        const uint64_t e = __builtin_amdgcn_s_memrealtime() / period;
+        if (e != epend) {
+          flush(tpend, pend);
+          tpend = ~0ull;
+        }
+      }
+    }
+    if (MODE == 0) {
+      flush(t, acc);
+    } else {
+      if (tpend != ~0ull) flush(tpend, pend);
+      tpend = t;
+      pend = acc;
+      epend = __builtin_amdgcn_s_memrealtime() / period;
+    }
+  }
+  if (MODE == 1 && tpend != ~0ull) flush(tpend, pend);
+  const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (x == 0x9e3779b9u) sink[lane] = x;
+}
+
+extern "C" int epoch_probe_run(const void *in, uint64_t ntiles, uint32_t tile_bytes, void *recs,
+                               int mode, uint64_t period, int grid, uint32_t *sink, void *stream) {
+  if (tile_bytes < 16 || tile_bytes % 16 || period == 0) return -22;
+  if (mode == 0)
+    hipLaunchKernelGGL(epoch_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
+  else
+    hipLaunchKernelGGL(epoch_kernel<1>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}

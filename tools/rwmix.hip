@@ -93,15 +93,29 @@ extern "C" int rwblk_run(const void *in, void *out, uint64_t ntiles, uint32_t rb
 // tile is 4 loads per lane), then the tile's wb record bytes are written
 // as one burst.  Nothing is parsed or summed beyond a xor that keeps the
 // loads alive.
-template <bool NT, bool GATHER, int U>
+// PH (period > 0): the rx kernel's global write phases -- a tile's record
+// bytes held (here: the value they are made of) until the chip-wide clock
+// passes the next multiple of `period` ticks, checked after every load
+// group, or until the next tile's are ready (rx_kernel.hip "Global write
+// phases").
+template <bool NT, bool GATHER, int U, bool PH = false>
 __global__ __launch_bounds__(256) void sol_kernel(const uint8_t *in, const uint64_t *off,
                                                   const uint16_t *len, uint64_t n, u32x4 *out,
                                                   uint64_t ntiles, uint32_t rb, uint32_t wb16,
-                                                  uint32_t *sink) {
+                                                  uint32_t *sink, uint32_t period = 0) {
   const int lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   const uint64_t wid = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
   u32x4 acc = {0, 0, 0, 0};
+  u32x4 pend = acc;
+  uint64_t tpend = ~0ull, deadline = 0;
+  auto write = [&](uint64_t t, u32x4 v) {
+    u32x4 *q = out + t * (uint64_t)wb16;
+    for (uint32_t e = lane; e < wb16; e += 64) {
+      if (NT) __builtin_nontemporal_store(v, q + e);
+      else q[e] = v;
+    }
+  };
   for (uint64_t t = wid; t < ntiles; t += nwaves) {
     uint64_t lo, hi;
     if constexpr (GATHER) {
@@ -124,19 +138,49 @@ __global__ __launch_bounds__(256) void sol_kernel(const uint8_t *in, const uint6
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) acc ^= v[u];
+      if (PH && tpend != ~0ull && __builtin_amdgcn_s_memrealtime() >= deadline) {
+        write(tpend, pend);
+        tpend = ~0ull;
+      }
     }
-    u32x4 *q = out + t * (uint64_t)wb16;
-    for (uint32_t e = lane; e < wb16; e += 64) {
-      if (NT) __builtin_nontemporal_store(acc, q + e);
-      else q[e] = acc;
+    if (PH) {
+      if (tpend != ~0ull) write(tpend, pend);
+      tpend = t;
+      pend = acc;
+      const uint64_t rt = __builtin_amdgcn_s_memrealtime();
+      deadline = rt - rt % period + period;
+    } else {
+      write(t, acc);
     }
   }
+  if (PH && tpend != ~0ull) write(tpend, pend);
   const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
   if (x == 0x9e3779b9u) sink[lane] = x;
 }
 
 // mode bit 0: non-temporal loads/stores; bit 1: descriptors (off/len);
-// bit 2: 4 loads per lane in flight instead of 16
+// bit 2: 4 loads per lane in flight instead of 16; bit 3: global write
+// phases of `period` ticks (non-temporal modes)
+extern "C" int sol_run_phased(const void *in, const void *off, const void *len, uint64_t n,
+                              void *out, uint64_t ntiles, uint32_t rb, uint32_t wb, int mode,
+                              int grid, uint32_t *sink, uint32_t period, void *stream) {
+  const hipStream_t s = (hipStream_t)stream;
+  if (period == 0) return -22;
+#define SOL_PH(G, U)                                                                              \
+  hipLaunchKernelGGL((sol_kernel<true, G, U, true>), dim3(grid), dim3(256), 0, s,                 \
+                     (const uint8_t *)in, (const uint64_t *)off, (const uint16_t *)len, n,        \
+                     (u32x4 *)out, ntiles, rb, wb / 16, sink, period)
+  switch (mode & 7) {
+    case 1: SOL_PH(false, 16); break;
+    case 3: SOL_PH(true, 16); break;
+    case 5: SOL_PH(false, 4); break;
+    case 7: SOL_PH(true, 4); break;
+    default: return -22;
+  }
+#undef SOL_PH
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int sol_run(const void *in, const void *off, const void *len, uint64_t n, void *out,
                        uint64_t ntiles, uint32_t rb, uint32_t wb, int mode, int grid,
                        uint32_t *sink, void *stream) {

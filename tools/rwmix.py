@@ -25,6 +25,10 @@ def _lib():
     L.sol_run.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32,
                           ctypes.c_uint32, ctypes.c_int, ctypes.c_int, vp, vp]
     L.sol_run.restype = ctypes.c_int
+    L.sol_run_phased.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64,
+                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, vp,
+                                 ctypes.c_uint32, vp]
+    L.sol_run_phased.restype = ctypes.c_int
     L.rwdefer_run.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                               ctypes.c_int, ctypes.c_int, vp, vp]
     L.rwdefer_run.restype = ctypes.c_int
@@ -41,7 +45,9 @@ def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
     reading the launch's frame bytes in 64-frame tiles -- fixed tiles of rb
     bytes, or (off/lens given: frames packed in batch order) each tile's
     actual span after its descriptors -- and writing wb record bytes per
-    tile.  Returns (ms, setting)."""
+    tile; the non-temporal shapes also with the rx kernel's global write
+    phases (period ~0.75 of a tile's duration at 5.5 TB/s, as
+    rx_capi.hip phase_ticks_for sets it).  Returns (ms, setting)."""
     import torch
     L = _lib()
     dev = inp.device
@@ -55,17 +61,27 @@ def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     best = (float("inf"), None)
     shapes = {}
-    for mode in (0, 1, 4, 5):
-        m = mode | (2 if gather else 0)
+    if gather:   # the tiles' mean span
+        tile_bytes = (int(off[ntiles * 64 - 1].item()) + int(lens[ntiles * 64 - 1].item() & 0xFFFF)
+                      - int(off[0].item())) / ntiles
+    else:
+        tile_bytes = rb
+    for mode in (0, 1, 4, 5, 9, 13):
+        m = (mode & 7) | (2 if gather else 0)
+        phased = bool(mode & 8)
         for mult in (2, 4, 8):
+            period = max(100, int(tile_bytes * ncu * mult * 4 * 3 / 4 / 55000))
             ts = []
             for k in range(reps + 2):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
-                rc = L.sol_run(inp.data_ptr(), off.data_ptr() if gather else None,
-                               lens.data_ptr() if gather else None, n, out.data_ptr(), ntiles,
-                               rb, wb, m, ncu * mult, sink.data_ptr(),
-                               ctypes.c_void_p(s.cuda_stream))
+                args = (inp.data_ptr(), off.data_ptr() if gather else None,
+                        lens.data_ptr() if gather else None, n, out.data_ptr(), ntiles, rb, wb, m,
+                        ncu * mult, sink.data_ptr())
+                if phased:
+                    rc = L.sol_run_phased(*args, period, ctypes.c_void_p(s.cuda_stream))
+                else:
+                    rc = L.sol_run(*args, ctypes.c_void_p(s.cuda_stream))
                 b.record()
                 torch.cuda.synchronize(dev)
                 assert rc == 0
@@ -73,10 +89,11 @@ def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
                     ts.append(a.elapsed_time(b))
             ts.sort()
             med = ts[len(ts) // 2]
-            shapes[f"{'nt' if mode & 1 else 'plain'}_l{4 if mode & 4 else 16}_b{mult}"] = round(med, 4)
+            shapes[f"{'nt' if mode & 1 else 'plain'}_l{4 if mode & 4 else 16}_b{mult}"
+                   + ("_phased" if phased else "")] = round(med, 4)
             if med < best[0]:
                 best = (med, {"nt": bool(mode & 1), "loads_in_flight": 4 if mode & 4 else 16,
-                              "blocks_per_cu": mult * 1})
+                              "blocks_per_cu": mult * 1, "write_phases": phased})
     if os.environ.get("RWMIX_SOL_SHAPES"):   # every shape's median (A/B probes)
         best[1]["shapes"] = shapes
     return best
