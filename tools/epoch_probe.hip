@@ -9,6 +9,8 @@
 //           new period of P ticks, checked after every 8 KB of reads, and
 //           written at the latest when the next tile's record is ready --
 //           every wave's writes fall in the first microseconds of a period.
+//   MODE 2: as 1 with room for two tiles' runs (written together at the
+//           period start, or the older one when a third is ready).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,8 +24,8 @@ __global__ __launch_bounds__(256) void epoch_kernel(const uint8_t *in, uint64_t 
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   const uint32_t nins = (tile_bytes + 1023) / 1024;
   u32x4 acc = {0, 0, 0, 0};
-  u32x4 pend = acc;
-  uint64_t tpend = ~0ull, epend = 0;
+  u32x4 pend = acc, pend2 = acc;
+  uint64_t tpend = ~0ull, tpend2 = ~0ull, epend = 0;
   auto flush = [&](uint64_t t, u32x4 v) {
     u32x4 *q = recs + t * 256;
 #pragma unroll
@@ -40,24 +42,44 @@ __global__ __launch_bounds__(256) void epoch_kernel(const uint8_t *in, uint64_t 
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc ^= v[k];
-      if (MODE == 1 && tpend != ~0ull) {
+      if (MODE >= 1 && tpend != ~0ull) {
         const uint64_t e = __builtin_amdgcn_s_memrealtime() / period;
         if (e != epend) {
           flush(tpend, pend);
           tpend = ~0ull;
+          if (MODE == 2 && tpend2 != ~0ull) {
+            flush(tpend2, pend2);
+            tpend2 = ~0ull;
+          }
         }
       }
     }
     if (MODE == 0) {
       flush(t, acc);
-    } else {
+    } else if (MODE == 1) {
       if (tpend != ~0ull) flush(tpend, pend);
       tpend = t;
       pend = acc;
       epend = __builtin_amdgcn_s_memrealtime() / period;
+    } else {
+      // two slots: the older run goes out when a third is ready
+      if (tpend == ~0ull) {
+        tpend = t;
+        pend = acc;
+        epend = __builtin_amdgcn_s_memrealtime() / period;
+      } else {
+        if (tpend2 != ~0ull) {
+          flush(tpend, pend);
+          tpend = tpend2;
+          pend = pend2;
+        }
+        tpend2 = t;
+        pend2 = acc;
+      }
     }
   }
-  if (MODE == 1 && tpend != ~0ull) flush(tpend, pend);
+  if (MODE >= 1 && tpend != ~0ull) flush(tpend, pend);
+  if (MODE == 2 && tpend2 != ~0ull) flush(tpend2, pend2);
   const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
   if (x == 0x9e3779b9u) sink[lane] = x;
 }
@@ -68,8 +90,11 @@ extern "C" int epoch_probe_run(const void *in, uint64_t ntiles, uint32_t tile_by
   if (mode == 0)
     hipLaunchKernelGGL(epoch_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
-  else
+  else if (mode == 1)
     hipLaunchKernelGGL(epoch_kernel<1>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
+  else
+    hipLaunchKernelGGL(epoch_kernel<2>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -49,8 +49,10 @@ def main():
     settings = [("rx", None, 0, 0)]
     for bpc in (2, 3):
         settings.append((f"tile_end_b{bpc}", 0, 1, bpc))
-        for per in (1000, 2000, 4000, 8000):
+        for per in (2000, 3000, 4000, 6000):
             settings.append((f"phase{per // 100}us_b{bpc}", 1, per, bpc))
+    for per in (3000, 4000, 6000, 8000, 12000):   # two tiles' runs held (2 blocks per CU)
+        settings.append((f"phase2x{per // 100}us_b2", 2, per, 2))
 
     def run(mode, per, bpc):
         if mode is None:
