@@ -454,8 +454,11 @@ static uint32_t phase_ticks_for(const pptk_rx_dev_batch *b, int variant, int gri
   if (force >= 0) return (uint32_t)force;
   if (!rx_variant_phased(variant) || b->d_perm || (!b->d_recs && !b->d_recs32)) return 0;
   const uint64_t maxlen = b->d_len ? (b->max_len ? b->max_len : 1518u) : b->fixed_len;
-  const uint64_t tile_bytes = 64 * (b->d_off ? std::max<uint64_t>(64, maxlen / 2)
-                                             : std::max<uint64_t>(b->stride, 64));
+  // (a stride far past any frame only lengthens the estimate; capped so the
+  // product below cannot overflow)
+  const uint64_t tile_bytes =
+      64 * (b->d_off ? std::max<uint64_t>(64, maxlen / 2)
+                     : std::min<uint64_t>(std::max<uint64_t>(b->stride, 64), 1u << 20));
   const uint64_t waves = (uint64_t)grid * 4;
   const uint64_t ticks = tile_bytes * waves * 3 / 4 / 55000;   // 5.5 TB/s = 55 000 B per tick
   return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ticks, 100), 1000000);
