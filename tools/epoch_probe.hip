@@ -11,6 +11,9 @@
 //           every wave's writes fall in the first microseconds of a period.
 //   MODE 2: as 1 with room for two tiles' runs (written together at the
 //           period start, or the older one when a third is ready).
+//   MODE 3: as 1, the period's start shifted by (blockIdx % 8) / 8 of a
+//           period -- each XCD's waves write together, the eight XCDs in turn.
+//   MODE 4: as 3 with (blockIdx % 2) / 2: two groups of XCDs in turn.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -23,6 +26,8 @@ __global__ __launch_bounds__(256) void epoch_kernel(const uint8_t *in, uint64_t 
   const int lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   const uint32_t nins = (tile_bytes + 1023) / 1024;
+  const uint64_t shift = MODE == 3 ? (uint64_t)(blockIdx.x % 8) * period / 8
+                         : MODE == 4 ? (uint64_t)(blockIdx.x % 2) * period / 2 : 0;
   u32x4 acc = {0, 0, 0, 0};
   u32x4 pend = acc, pend2 = acc;
   uint64_t tpend = ~0ull, tpend2 = ~0ull, epend = 0;
@@ -43,7 +48,7 @@ __global__ __launch_bounds__(256) void epoch_kernel(const uint8_t *in, uint64_t 
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc ^= v[k];
       if (MODE >= 1 && tpend != ~0ull) {
-        const uint64_t e = __builtin_amdgcn_s_memrealtime() / period;
+        const uint64_t e = (__builtin_amdgcn_s_memrealtime() + shift) / period;
         if (e != epend) {
           flush(tpend, pend);
           tpend = ~0ull;
@@ -56,11 +61,11 @@ __global__ __launch_bounds__(256) void epoch_kernel(const uint8_t *in, uint64_t 
     }
     if (MODE == 0) {
       flush(t, acc);
-    } else if (MODE == 1) {
+    } else if (MODE == 1 || MODE >= 3) {
       if (tpend != ~0ull) flush(tpend, pend);
       tpend = t;
       pend = acc;
-      epend = __builtin_amdgcn_s_memrealtime() / period;
+      epend = (__builtin_amdgcn_s_memrealtime() + shift) / period;
     } else {
       // two slots: the older run goes out when a third is ready
       if (tpend == ~0ull) {
@@ -93,8 +98,14 @@ extern "C" int epoch_probe_run(const void *in, uint64_t ntiles, uint32_t tile_by
   else if (mode == 1)
     hipLaunchKernelGGL(epoch_kernel<1>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
-  else
+  else if (mode == 2)
     hipLaunchKernelGGL(epoch_kernel<2>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
+  else if (mode == 3)
+    hipLaunchKernelGGL(epoch_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
+  else
+    hipLaunchKernelGGL(epoch_kernel<4>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

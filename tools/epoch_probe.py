@@ -47,12 +47,20 @@ def main():
     s = torch.cuda.current_stream(dev)
     ntiles = n // 64
     settings = [("rx", None, 0, 0)]
-    for bpc in (2, 3):
-        settings.append((f"tile_end_b{bpc}", 0, 1, bpc))
-        for per in (2000, 3000, 4000, 6000):
-            settings.append((f"phase{per // 100}us_b{bpc}", 1, per, bpc))
-    for per in (3000, 4000, 6000, 8000, 12000):   # two tiles' runs held (2 blocks per CU)
-        settings.append((f"phase2x{per // 100}us_b2", 2, per, 2))
+    sweep = os.environ.get("EPOCH_SWEEP", "stagger")
+    if sweep == "depth":
+        for bpc in (2, 3):
+            settings.append((f"tile_end_b{bpc}", 0, 1, bpc))
+            for per in (2000, 3000, 4000, 6000):
+                settings.append((f"phase{per // 100}us_b{bpc}", 1, per, bpc))
+        for per in (3000, 4000, 6000, 8000, 12000):   # two tiles' runs held (2 blocks per CU)
+            settings.append((f"phase2x{per // 100}us_b2", 2, per, 2))
+    else:   # all waves at once vs the XCDs (or two halves) in turn, 3 blocks per CU
+        settings.append(("tile_end_b3", 0, 1, 3))
+        for per in (3000, 4000):
+            settings.append((f"phase{per // 100}us_b3", 1, per, 3))
+            settings.append((f"phase{per // 100}us_xcd8_b3", 3, per, 3))
+            settings.append((f"phase{per // 100}us_half2_b3", 4, per, 3))
 
     def run(mode, per, bpc):
         if mode is None:
