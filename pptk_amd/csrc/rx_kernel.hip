@@ -896,7 +896,7 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
     }
     if (live && k < kmax) {
       const u32x4 val = st[r * 5 + piece];
-      if (stash) {                   // (write-phase A/B build: held in LDS, stored later)
+      if (stash) {                   // global write phases: held in LDS, stored later
         stash[e] = val;
       } else if (a.tune & 64u) {     // bit 6: write-through, drop from L2 (sc1)
         GLB_AS uint64_t *d8 = (GLB_AS uint64_t *)d;
@@ -942,7 +942,7 @@ __device__ __forceinline__ void flush_records(const RxKArgs &a, const LDS_AS uin
 // 7 "Placement"), and less when every wave's come together: a tile's record
 // run waits in the wave's LDS stash until the chip-wide clock
 // (s_memrealtime, 100 MHz, one clock for every CU) passes the next multiple
-// of phase_ticks -- checked between round groups -- or until the next
+// of phase_ticks -- checked after every streaming round -- or until the next
 // tile's run needs the stash, so the waves' record writes fall in the first
 // microseconds of each period instead of each at its own tile end.  The
 // host sets the period to ~0.75 of a tile's expected duration (rx_capi.hip
