@@ -98,3 +98,8 @@ tools/libepoch_probe.so: tools/epoch_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
 all: tools/libepoch_probe.so
+
+tools/libstandin.so: tools/standin.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
+
+all: tools/libstandin.so

@@ -31,6 +31,11 @@ HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KEY = bytes(range(1, 17))
 N_PER_GPU = 16 * 1024 * 1024
 SETTLE_S = 1.5                  # seconds of untimed launches before warmup
+# N > 1: CUs left to the all-gather beside the batches (pptk_rx_stream_split):
+# RCCL's kernel needs whole CUs and the persistent grid fills them all, so
+# without a split the gather runs between batches, not beside them (DESIGN
+# section 8: +1.6-1.8 ms per batch with a 1.7 ms stand-in, +0.09 ms split)
+COLL_CUS = int(os.environ.get("PPTK_BENCH_COLL_CUS", "32"))
 
 
 def log(*a):
@@ -339,12 +344,12 @@ def placed_gather(ctx, b, recs, kw, n_total, ws, rank, dev):
 
 def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SETTLE_S,
                compact=False, batch=None, autotune=True, first=None, place=True, recs=None,
-               n_gather_total=None):
+               n_gather_total=None, coll_stream=None):
     """Generate this rank's shard of config `cfg` (n frames from global frame
     `first`, default rank * n) or reuse `batch`, time `steps` launches.
     gbs: two shard.GatherBuffer (double-buffered all-gather of the flow
-    hashes after every launch, on a second stream) or None.  compact:
-    32-byte records (struct pptk_rx_rec32)."""
+    hashes after every launch, on a second stream: `coll_stream`, or a new
+    one) or None.  compact: 32-byte records (struct pptk_rx_rec32)."""
     import torch
     from tools.synth import make_batch
     first = rank * n if first is None else first
@@ -389,7 +394,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
         ctx.autotune(b["frames"], n, recs=recs, compact=compact, reps=9, **kw)
 
     main = torch.cuda.current_stream(dev)
-    gs = torch.cuda.Stream(dev) if gbs else None
+    gs = (coll_stream or torch.cuda.Stream(dev)) if gbs else None
     del GATHER_STREAMS[:]
     if gbs:
         GATHER_STREAMS.extend([(ctx, main), (ctx, gs)])
@@ -653,7 +658,8 @@ def compact_line(full, detail_path=None):
         line["allgather"] = {"error": gat["error"]}
     elif gat:
         g = {k: gat.get(k) for k in ("ms", "algbw_gbs", "busbw_gbs", "overlap_loss", "rccl_ranks",
-                                      "bytes_per_rank")}
+                                      "bytes_per_rank", "coll_cus", "split",
+                                      "nccl_max_nchannels")}
         chk = gat.get("gathered_check") or {}
         g["gathered_check"] = {k: chk.get(k) for k in ("own_slice_equals_records",
                                                         "sampled_frames_per_rank",
@@ -1221,11 +1227,12 @@ def forced_ms(ctx, b, recs, n, variant, steps, warmup=3):
     return round(float(np.median([a.elapsed_time(z) for a, z in ev])), 4), same
 
 
-def gather_bench(ctx, gb, ws, dev, steps):
+def gather_bench(ctx, gb, ws, dev, steps, stream=None):
     """The all-gather of `per` u64 flow hashes per rank alone
-    (pptk_rx_allgather_hash): time and bandwidths."""
+    (pptk_rx_allgather_hash): time and bandwidths, on `stream`
+    (default: the current one)."""
     import torch
-    main = torch.cuda.current_stream(dev)
+    main = stream or torch.cuda.current_stream(dev)
     GATHER_STREAMS[:] = [(ctx, main)]
     for _ in range(3):
         gb.gather(ctx, stream=main)
@@ -1362,6 +1369,11 @@ def main():
     gbs = None
     comm_error = None
     if dist_on(ws):
+        if COLL_CUS > 0:
+            # at most one RCCL block per CU the split leaves the gather, so
+            # every channel of the collective is resident at once (set before
+            # RCCL reads its environment, at the communicator's creation)
+            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(COLL_CUS))
         comm_error = join_all(ctx, ws, rank)     # RCCL communicator in libpptkrx.so
         if comm_error:
             log(f"[rank {rank}] no all-gather: {comm_error}")
@@ -1375,10 +1387,27 @@ def main():
     check = not args.no_check
 
     primary_cfg = args.only or "c1500"
+    split = None
+    if gbs and COLL_CUS > 0:
+        # the batches on all CUs but COLL_CUS, the gather on those
+        # (pptk_rx_stream_split; placement and autotune probes run split too)
+        split = ctx.stream_split(COLL_CUS)
+        torch.cuda.set_stream(split[0])
     prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, gbs, check,
-                      args.settle, first=first, place=place, n_gather_total=n_total)
+                      args.settle, first=first, place=place, n_gather_total=n_total,
+                      coll_stream=split[1] if split else None)
     gbs = prim.pop("_gbs")
     log(f"[rank {rank}] {primary_cfg}: {prim['mpkts']:.1f} Mpkts/s, kernel {prim['kernel_ms']:.3f} ms")
+    gat_split = None
+    if split:
+        torch.cuda.synchronize(dev)
+        # the gather alone on the CUs the split left it
+        gat_split = gather_bench(ctx, gbs[0], ws, dev, args.steps, stream=split[1])
+        torch.cuda.synchronize(dev)
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
+        GATHER_STREAMS[:] = [(ctx, torch.cuda.default_stream(dev))]   # (not the split's)
+        ctx.stream_join()
+        del split
     nog = gat = None
     if gbs:
         # same launches without the collective: the kernel-only duration the
@@ -1393,6 +1422,10 @@ def main():
         if gat["rccl_ranks"] != ws:
             raise RuntimeError(f"the RCCL communicator has {gat['rccl_ranks']} ranks, not {ws}")
         gat["overlap_loss"] = round(1.0 - prim["mpkts"] / nog["mpkts"], 4)
+        gat["coll_cus"] = COLL_CUS if gat_split else 0
+        gat["nccl_max_nchannels"] = os.environ.get("NCCL_MAX_NCHANNELS")
+        if gat_split:
+            gat["split"] = {k: gat_split[k] for k in ("ms", "algbw_gbs", "busbw_gbs")}
         gat["buffer_placement"] = prim.get("gather_placement")
         if check:
             gat["gathered_check"] = gathered_check(prim, gbs, n, dev)

@@ -559,6 +559,24 @@ void pptk_rx_shard_range(uint64_t n, int nranks, int rank, uint64_t *first, uint
 int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint64_t n,
                            uint64_t *d_out, void *stream);
 
+/* Two streams that split the chip's CUs between the batches and the
+ * gather that overlaps them (no reference counterpart: the reference has no
+ * device; this belongs with the collective above).  RCCL's all-gather
+ * kernel needs a whole CU per block on gfx950 (512 threads, 37 KB of LDS,
+ * 248 VGPRs), and the persistent receive grid fills every CU, so at each
+ * batch boundary one kernel takes CUs the other was sized for and the two
+ * run one after the other.  *coll_stream (for
+ * pptk_rx_allgather_hash) may use `coll_cus` CUs -- the same number in
+ * every shader engine of every XCC -- and *rx_stream (for the batches) the
+ * rest; the context sizes its receive grids for the rest from now on, on
+ * any stream.  coll_cus: a multiple of 4 x the device's XCC count (32 on an
+ * MI355X), below its CU count; -EINVAL otherwise.  coll_cus 0 (streams
+ * NULL allowed) gives the context the whole chip again.  Destroy the
+ * streams with pptk_rx_stream_destroy. */
+int pptk_rx_stream_split(struct pptk_rx_ctx *ctx, int coll_cus, void **rx_stream,
+                         void **coll_stream);
+int pptk_rx_stream_destroy(void *stream);
+
 /* Buffer placement.  What the memory charges for the record writes beside
  * the frame-read stream depends on where the frame buffer and the record
  * buffer sit physically: the same C1500 launch, same kernel, same bytes,

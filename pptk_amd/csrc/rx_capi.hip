@@ -163,6 +163,7 @@ struct pptk_rx_ctx {
   uint64_t *d_txuser = nullptr;   // pptk_tx_set_side_buffer
   uint64_t txuser_n = 0;
   int ncu = 256;
+  int coll_cus = 0;   // pptk_rx_stream_split: CUs left to the collective
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
   int forced_flags = -1;   // the receive transform's memory policy, -1 automatic
@@ -373,10 +374,12 @@ static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n) {
   const uint64_t ntiles = (n + 63) / 64;
   const uint64_t want_blocks = (ntiles + 3) / 4;
   static const long grid_mult = std::max(1l, EXP_KNOB("PPTK_RX_GRID_MULT", 1));
-  // PPTK_RX_RESERVE_CUS: leave that many CUs' worth of resident blocks
-  // free, so a concurrent kernel (an RCCL collective overlapping the batch)
-  // finds room on the chip instead of waiting for the persistent grid.
-  static const int reserve = (int)std::max(0l, EXP_KNOB("PPTK_RX_RESERVE_CUS", 0));
+  // the CUs pptk_rx_stream_split left to the collective (the batches'
+  // stream cannot use them); PPTK_RX_RESERVE_CUS: that many CUs' worth of
+  // resident blocks fewer without a mask (on its own it leaves no CU free:
+  // the dispatcher spreads the smaller grid over every CU)
+  static const int reserve_knob = (int)std::max(0l, EXP_KNOB("PPTK_RX_RESERVE_CUS", 0));
+  const int reserve = std::max(reserve_knob, c->coll_cus);
   const uint64_t ncu = (uint64_t)std::max(1, c->ncu - std::min(reserve, c->ncu - 1));
   const uint64_t cap = ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, cap));
@@ -899,6 +902,50 @@ int pptk_rx_set_tuning(struct pptk_rx_ctx *c, int variant, int flags) {
   c->forced_flags = flags >= 0 && rx == 0 && (flags & PPTK_RX_TUNE_PERMIT_PASSES) ? -1 : rx;
   c->permit_passes = flags >= 0 && (flags & PPTK_RX_TUNE_PERMIT_PASSES);
   return 0;
+}
+
+// CU-mask bit i names CU i / nxcc of XCC i % nxcc, and CU k of an XCC sits
+// in shader engine k % 4 (tools/cumask_map.py, profiles/r05 row aj): the
+// top coll_cus bits are coll_cus / nxcc CUs of every XCC, the same number
+// in each of its four SEs when that is a multiple of 4.  Each workgroup goes
+// to an XCC and SE in turn, so a mask that leaves one SE short of another
+// overfills it and the persistent grid runs a tail (-EINVAL below).
+static constexpr int kSePerXcc = 4;
+
+int pptk_rx_stream_split(struct pptk_rx_ctx *c, int coll_cus, void **rx_stream,
+                         void **coll_stream) {
+  if (!c || coll_cus < 0) return -EINVAL;
+  if (coll_cus == 0) {
+    if (rx_stream) *rx_stream = nullptr;
+    if (coll_stream) *coll_stream = nullptr;
+    c->coll_cus = 0;
+    return 0;
+  }
+  if (!rx_stream || !coll_stream) return -EINVAL;
+  *rx_stream = *coll_stream = nullptr;
+  DeviceScope dg(c->device);
+  if (!dg.ok) return -EIO;
+  int nxcc = 1;
+  if (hipDeviceGetAttribute(&nxcc, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess ||
+      nxcc < 1)
+    nxcc = 1;
+  if (coll_cus % (nxcc * kSePerXcc) || coll_cus >= c->ncu || c->ncu % nxcc) return -EINVAL;
+  std::vector<uint32_t> rx((c->ncu + 31) / 32, 0), coll(rx.size(), 0);
+  for (int i = 0; i < c->ncu; ++i) (i >= c->ncu - coll_cus ? coll : rx)[i / 32] |= 1u << (i % 32);
+  hipStream_t a = nullptr, b = nullptr;
+  if (hipExtStreamCreateWithCUMask(&a, (uint32_t)rx.size(), rx.data()) != hipSuccess) return -EIO;
+  if (hipExtStreamCreateWithCUMask(&b, (uint32_t)coll.size(), coll.data()) != hipSuccess) {
+    (void)hipStreamDestroy(a);
+    return -EIO;
+  }
+  *rx_stream = a;
+  *coll_stream = b;
+  c->coll_cus = coll_cus;
+  return 0;
+}
+
+int pptk_rx_stream_destroy(void *stream) {
+  return stream ? hip_err(hipStreamDestroy((hipStream_t)stream)) : -EINVAL;
 }
 
 int pptk_rx_variant_count(void) { return RX_NVARIANTS; }

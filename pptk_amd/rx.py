@@ -184,7 +184,8 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_device_count", "pptk_rx_comm_uid", "pptk_rx_comm_create",
            "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
            "pptk_rx_comm_abort", "pptk_rx_comm_sync",
-           "pptk_rx_shard_range", "pptk_rx_allgather_hash",
+           "pptk_rx_shard_range", "pptk_rx_allgather_hash", "pptk_rx_stream_split",
+           "pptk_rx_stream_destroy",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init",
@@ -310,6 +311,12 @@ def lib(path=None):
             L.pptk_rx_comm_abort.restype = ctypes.c_int
             L.pptk_rx_comm_sync.argtypes = [vp, vp, ctypes.c_uint32]
             L.pptk_rx_comm_sync.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_stream_split"):         # absent from older A/B builds
+            L.pptk_rx_stream_split.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp),
+                                               ctypes.POINTER(vp)]
+            L.pptk_rx_stream_split.restype = ctypes.c_int
+            L.pptk_rx_stream_destroy.argtypes = [vp]
+            L.pptk_rx_stream_destroy.restype = ctypes.c_int
         L.pptk_rx_version.restype = ctypes.c_char_p
         L.pptk_rx_set_tuning.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.pptk_rx_set_tuning.restype = ctypes.c_int
@@ -362,6 +369,7 @@ class RxContext:
             o.comm_timeout_ms = comm_timeout_ms
         self._ctx = ctypes.c_void_p()
         self._inflight = collections.deque()   # (pkts, out) of submitted host batches
+        self._split = []                       # HIP streams of stream_split
         rc = L.pptk_rx_ctx_create(ctypes.byref(self._ctx), ctypes.byref(o))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_ctx_create failed ({rc})")
@@ -379,6 +387,7 @@ class RxContext:
 
     def close(self):
         if self._ctx:
+            self.stream_join()
             self._L.pptk_rx_ctx_destroy(self._ctx)   # (waits for outstanding submissions)
             self._ctx = ctypes.c_void_p()
             self._inflight.clear()
@@ -701,6 +710,32 @@ class RxContext:
                                             ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_allgather_hash failed ({rc})")
+
+    def stream_split(self, coll_cus):
+        """pptk_rx_stream_split: (rx stream, collective stream) as torch
+        streams on this context's device, the collective's holding coll_cus
+        CUs (a multiple of 32 on an MI355X) and the batches' the rest; the
+        context sizes its grids for the rest until stream_join().  The HIP
+        streams live until stream_join() or close()."""
+        import torch
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        rc = self._L.pptk_rx_stream_split(self._ctx, coll_cus, ctypes.byref(a), ctypes.byref(b))
+        if rc != 0:
+            raise OSError(-rc, f"pptk_rx_stream_split({coll_cus}) failed ({rc})")
+        self._split.extend([a.value, b.value])
+        dev = torch.device("cuda", self.device)
+        return (torch.cuda.ExternalStream(a.value, device=dev),
+                torch.cuda.ExternalStream(b.value, device=dev))
+
+    def stream_join(self):
+        """Undo stream_split: the whole chip for this context's grids again;
+        the split streams are destroyed (work on them still completes)."""
+        if not hasattr(self._L, "pptk_rx_stream_split"):
+            return
+        self._L.pptk_rx_stream_split(self._ctx, 0, None, None)
+        while self._split:
+            h = self._split.pop()
+            self._L.pptk_rx_stream_destroy(h)
 
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""

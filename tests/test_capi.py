@@ -529,6 +529,8 @@ def test_entry_points_reject_bad_arguments(lib):
     assert lib.pptk_rx_comm_destroy(None) == EINVAL
     assert lib.pptk_rx_comm_info(None, None, None) == EINVAL
     assert lib.pptk_rx_allgather_hash(None, None, 1, None, None) == EINVAL
+    assert lib.pptk_rx_stream_split(None, 32, None, None) == EINVAL
+    assert lib.pptk_rx_stream_destroy(None) == EINVAL
     assert lib.pptk_rx_place_records(None, ctypes.byref(b), None, 1, 1, None, None, None) == EINVAL
     assert lib.pptk_rx_place_buffers(None, ctypes.byref(b), None, 1, None, 1, 1, None, None, None,
                                      None) == EINVAL

@@ -935,6 +935,43 @@ def test_place_records(compact, dev):
     ctx.close()
 
 
+def test_stream_split(dev):
+    """pptk_rx_stream_split: the collective's stream holds the top 32 CU-mask
+    bits (4 CUs of every XCC, one per shader engine), the batches' stream the
+    rest; other counts are -EINVAL; records are the same on either stream,
+    split or not, and after the join."""
+    import ctypes
+    from pptk_amd.rx import RxContext
+    from tools.synth import make_batch
+    n = 1 << 16
+    b = make_batch("c1500", n, dev)
+    kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])
+    ctx = RxContext(0, bytes(range(1, 17)))
+    want = ctx.batch_device(b["frames"], n, **kw)
+    torch.cuda.synchronize()
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    for bad in (-1, 16, 33, ncu):
+        with pytest.raises(OSError) as e:
+            ctx.stream_split(bad)
+        assert e.value.errno == 22
+    rx, coll = ctx.stream_split(32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    for s, lo, hi in ((rx, 0, ncu - 32), (coll, ncu - 32, ncu)):
+        words = (ctypes.c_uint32 * (ncu // 32))()
+        assert hip.hipExtStreamGetCUMask(ctypes.c_void_p(s.cuda_stream), len(words), words) == 0
+        bits = [i for i in range(ncu) if words[i // 32] >> (i % 32) & 1]
+        assert bits == list(range(lo, hi))
+    for s in (rx, coll):
+        got = ctx.batch_device(b["frames"], n, stream=s, **kw)
+        s.synchronize()
+        assert torch.equal(got, want)
+    ctx.stream_join()
+    got = ctx.batch_device(b["frames"], n, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    ctx.close()
+
+
 def test_tuning_rejects_diagnostic_bits(dev):
     """The product library accepts only the result-preserving tuning bits:
     the diagnostic ones (skip record stores 0x8, skip the per-frame phase
