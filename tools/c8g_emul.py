@@ -28,7 +28,9 @@ or every (256/K)-th -- so the stand-in's blocks find whole CUs free; run it
 under the experiment build with PPTK_RX_RESERVE_CUS=K (grid for the rest).
 "side": as "top", and the second stream's mask holds just those K CUs.
 --split K: the same through the library (pptk_rx_stream_split), product
-build.
+build.  --copy: the stand-in also copies the 7 x 128 MiB landing bytes into
+the gather buffer, paced to STANDIN_US (the collective's HBM side and its CU
+footprint together).
 Mask bit i names CU i // 8 of XCC i % 8, and CU c of an XCC sits in SE
 c % 4 (tools/cumask_map.py): the top K bits are K / 8 CUs of every XCC,
 spread over its SEs.
@@ -88,7 +90,7 @@ def run(ctx, b, recs, n, kw, bufs, steps, land, dev):
             with torch.cuda.stream(side):
                 out[n:8 * n].copy_(src)
         elif land:
-            land(side)
+            land(side, out)
         gdone[k & 1].record(side)
 
     for k in range(40):            # settle (clocks)
@@ -154,8 +156,20 @@ def main():
 
         trace = torch.zeros(3 * 256, dtype=torch.int64, device=dev)
 
+        lib.standin_copy.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        copy = "--copy" in sys.argv
+        src = torch.zeros(7 * n, dtype=torch.int64, device=dev) if copy else None
+
         def standin(nb):
-            def land(side):
+            def land(side, out=None):
+                if copy:
+                    # the landing bytes, copied by the stand-in at xGMI pace
+                    dst = out if out is not None else src
+                    assert lib.standin_copy(nb, ticks, src.data_ptr(), dst[n:8 * n].data_ptr()
+                                            if out is not None else dst.data_ptr(),
+                                            7 * n * 8, side.cuda_stream) == 0
+                    return
                 assert lib.standin_run(nb, ticks, sink.data_ptr(), trace.data_ptr(),
                                        side.cuda_stream) == 0
             return land
@@ -186,7 +200,8 @@ def main():
             for nb in blocks:
                 res[f"standin_{nb}"].append(run(ctx, b, recs, n, kw, placed, steps,
                                                 standin(nb), dev))
-                st[nb] = starts(nb)
+                if not copy:
+                    st[nb] = starts(nb)
         ms = {k: round(float(np.median(v)), 4) for k, v in res.items()}
         print(json.dumps({"frames_per_rank": n, "steps": steps, "ms_per_step": ms,
                           "standin_alone_ms": round(alone, 4), "standin_starts": st, "standin_us": ticks // 100,

@@ -30,6 +30,49 @@ __global__ __launch_bounds__(512, 1) void standin_kernel(uint64_t ticks, uint32_
   }
 }
 
+// The same footprint copying `bytes` from src to dst (the ranks' landing
+// bytes and the forwarded reads of a ring all-gather), paced so that it
+// takes at least `ticks`: each block copies its contiguous slice in 16-byte
+// non-temporal loads and stores, and after every 64 KB waits until the
+// clock has reached that fraction of the duration (xGMI-rate arrival).
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(512, 1) void standin_copy_kernel(const u32x4s *src, u32x4s *dst,
+                                                             uint64_t n16, uint64_t ticks) {
+  __shared__ uint32_t lds[37664 / 4];
+  asm volatile("" ::: "v247");
+  lds[threadIdx.x] = threadIdx.x;
+  __syncthreads();
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t lo = min(n16, per * blockIdx.x), hi = min(n16, lo + per);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t chunk = 4096;   // 16-byte units: 64 KB
+  for (uint64_t c = lo; c < hi; c += chunk) {
+    const uint64_t e = min(hi, c + chunk);
+    u32x4s v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t i = c + threadIdx.x + k * 512;
+      if (i < e) v[k] = __builtin_nontemporal_load(src + i);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t i = c + threadIdx.x + k * 512;
+      if (i < e) __builtin_nontemporal_store(v[k], dst + i);
+    }
+    const uint64_t due = t0 + ticks * (e - lo) / max<uint64_t>(1, hi - lo);
+    while (__builtin_amdgcn_s_memrealtime() < due) __builtin_amdgcn_s_sleep(8);
+  }
+  if (lds[(threadIdx.x + 1) % 512] == 0xffffffffu) dst[0] = u32x4s{0, 0, 0, 0};
+}
+
+extern "C" int standin_copy(int blocks, uint64_t ticks, const void *src, void *dst, uint64_t bytes,
+                            void *stream) {
+  if (bytes % 16) return -22;
+  hipLaunchKernelGGL(standin_copy_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream,
+                     (const u32x4s *)src, (u32x4s *)dst, bytes / 16, ticks);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int standin_run(int blocks, uint64_t ticks, uint32_t *sink, uint64_t *trace,
                            void *stream) {
   hipLaunchKernelGGL(standin_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, ticks, sink,
