@@ -467,12 +467,33 @@ static uint32_t phase_ticks_for(const pptk_rx_dev_batch *b, int variant, int gri
   return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ticks, 100), 1000000);
 }
 
+#ifdef PPTK_RX_WAVE_TIMES
+// probe build (tools/wave_times.py): every wave's (start, end) clock of the
+// last launch
+static uint64_t *g_wave_times = nullptr;
+static int g_wave_count = 0;
+extern "C" int pptk_rx_wave_times(uint64_t *host, int max_waves) {
+  if (!g_wave_times) return -EINVAL;
+  const int n = std::min(max_waves, g_wave_count);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(host, g_wave_times, (size_t)n * 16, hipMemcpyDeviceToHost) != hipSuccess)
+    return -EIO;
+  return n;
+}
+#endif
+
 static int launch_batch(pptk_rx_ctx *c, const pptk_rx_dev_batch *b, int variant, void *stream) {
   RxKArgs a = batch_args(c, b);
   a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm);
   c->last_variant = variant;
   const int grid = grid_for(c, variant, b->n);
   a.phase_ticks = phase_ticks_for(b, variant, grid);
+#ifdef PPTK_RX_WAVE_TIMES
+  if (!g_wave_times && hipMalloc(&g_wave_times, (size_t)65536 * 16) != hipSuccess) return -ENOMEM;
+  if (grid * 4 > 65536) return -EINVAL;
+  a.wave_times = g_wave_times;
+  g_wave_count = grid * 4;
+#endif
   return hip_err(launch_rx(variant, a, grid, (hipStream_t)stream));
 }
 

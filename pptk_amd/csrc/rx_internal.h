@@ -103,6 +103,9 @@ struct RxKArgs {
   // global write phases of the streaming shapes (rx_kernel.hip): the period
   // in s_memrealtime ticks (10 ns); 0 = each tile's records at its end
   uint32_t phase_ticks;
+#ifdef PPTK_RX_WAVE_TIMES
+  uint64_t *wave_times;   // probe build: per wave (start, end) of the last launch
+#endif
 };
 
 // Kernel variants: T lanes per frame in the streaming checksum phase, S

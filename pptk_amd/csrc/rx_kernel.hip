@@ -1055,6 +1055,9 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
   const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
 
   uint64_t tile = blocked ? wid * per : wid;
+#ifdef PPTK_RX_WAVE_TIMES
+  const uint64_t wt_start = __builtin_amdgcn_s_memrealtime();
+#endif
   Desc dc = load_desc<GATHER>(a, tile, lane);
   Desc dn = load_desc<GATHER>(a, tile + step, lane);
   uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * step, lane);
@@ -1206,6 +1209,13 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     idx2 = idx3;
   }
   if (PHASED && st_tile != ~0ull) flush_stash(a, stash, st_tile, lane);
+#ifdef PPTK_RX_WAVE_TIMES
+  // probe build (tools/wave_times.py): when each wave started and finished
+  if (a.wave_times && lane == 0) {
+    a.wave_times[2 * wid] = wt_start;
+    a.wave_times[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // ---- Mixed-shape kernel (RX_M6): lanes binned by length inside each tile.
