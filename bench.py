@@ -31,7 +31,8 @@ HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KEY = bytes(range(1, 17))
 N_PER_GPU = 16 * 1024 * 1024
 SETTLE_S = 1.5                  # seconds of untimed launches before warmup
-# N > 1: CUs left to the all-gather beside the batches (pptk_rx_stream_split):
+# N > 1: CUs left to the all-gather beside the batches (pptk_rx_stream_split;
+# the forced one-rank line splits only when PPTK_BENCH_COLL_CUS is set):
 # RCCL's kernel needs whole CUs and the persistent grid fills them all, so
 # without a split the gather runs between batches, not beside them (DESIGN
 # section 8: +1.6-1.8 ms per batch with a 1.7 ms stand-in, +0.09 ms split)
@@ -1369,7 +1370,7 @@ def main():
     gbs = None
     comm_error = None
     if dist_on(ws):
-        if COLL_CUS > 0:
+        if COLL_CUS > 0 and (ws > 1 or "PPTK_BENCH_COLL_CUS" in os.environ):
             # at most one RCCL block per CU the split leaves the gather, so
             # every channel of the collective is resident at once (set before
             # RCCL reads its environment, at the communicator's creation)
@@ -1388,9 +1389,11 @@ def main():
 
     primary_cfg = args.only or "c1500"
     split = None
-    if gbs and COLL_CUS > 0:
+    if gbs and COLL_CUS > 0 and (ws > 1 or "PPTK_BENCH_COLL_CUS" in os.environ):
         # the batches on all CUs but COLL_CUS, the gather on those
-        # (pptk_rx_stream_split; placement and autotune probes run split too)
+        # (pptk_rx_stream_split; placement and autotune probes run split too).
+        # A one-rank gather (PPTK_BENCH_FORCE_DIST) launches nothing that
+        # needs CUs: split only when asked.
         split = ctx.stream_split(COLL_CUS)
         torch.cuda.set_stream(split[0])
     prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, gbs, check,
