@@ -41,6 +41,12 @@
  *                              threads) or before its first gather
  *   RX_MULTIGPU_TIMEOUT_MS=t   opts.comm_timeout_ms
  *   RX_MULTIGPU_TRACE=1        progress lines on stderr
+ *   RX_MULTIGPU_SPLIT=k        overlap each gather with the next batch: the
+ *                              batches on one stream, the gathers on another,
+ *                              the chip's CUs split between them with
+ *                              pptk_rx_stream_split (k CUs for the gathers;
+ *                              RCCL's kernel needs whole CUs);
+ *                              batch r waits for gather r - 2 (same buffer)
  */
 #include <errno.h>
 #include <pthread.h>
@@ -63,6 +69,7 @@ static struct pptk_rx_ctx *g_ctx[MAXR];
 static int g_nranks;
 static atomic_int g_failed;
 static int g_join_threads, g_fail_rank = -1;
+static int g_split;   /* RX_MULTIGPU_SPLIT */
 static uint8_t g_uid[PPTK_RX_COMM_UID_BYTES];
 static int g_trace;
 
@@ -117,7 +124,8 @@ static void *thrfn(void *arg)
   uint64_t *d_off = NULL, *d_out = NULL, *h_off = NULL, *h_out = NULL;
   uint16_t *d_len = NULL;
   struct pptk_rx_rec *h_recs = NULL;
-  hipStream_t st = NULL;
+  hipStream_t st = NULL, cs = NULL;   /* batches; gathers (RX_MULTIGPU_SPLIT) */
+  hipEvent_t kdone[2] = {NULL, NULL}, gdone[2] = {NULL, NULL};
   uint64_t lo = 0, hi = 0;
   struct pptk_rx_dev_batch b;
   struct pptk_rx_ring ring;
@@ -151,7 +159,21 @@ static void *thrfn(void *arg)
     }
   }
   CHECK_HIP(hipSetDevice(t->device));
-  CHECK_HIP(hipStreamCreate(&st));
+  if (g_split) {
+    /* before the rings and gather buffers: their probes run on the batches'
+     * stream, with the grid the split leaves it */
+    void *rx_s, *coll_s;
+    if ((t->rc = pptk_rx_stream_split(t->ctx, g_split, &rx_s, &coll_s)) != 0)
+      goto out;
+    st = rx_s;
+    cs = coll_s;
+    for (int k = 0; k < 2; k++) {
+      CHECK_HIP(hipEventCreateWithFlags(&kdone[k], hipEventDisableTiming));
+      CHECK_HIP(hipEventCreateWithFlags(&gdone[k], hipEventDisableTiming));
+    }
+  } else {
+    CHECK_HIP(hipStreamCreate(&st));
+  }
   /* the frame and record rings of this queue, placed by the library */
   memset(&rs, 0, sizeof(rs));
   rs.frame_bytes = hi - lo + 64;
@@ -203,13 +225,25 @@ static void *thrfn(void *arg)
   for (int r = 0; r < t->rounds && t->rc == 0; r++) {
     d_out = gat.d_out[r & 1];   /* double-buffered, as an rx loop overlapping gathers does */
     b.d_hash = d_out + (uint64_t)t->rank * per;   /* this rank's slice: gather in place */
+    if (cs && r >= 2)   /* the gather of round r - 2 has read this buffer */
+      CHECK_HIP(hipStreamWaitEvent(st, gdone[r & 1], 0));
     if ((t->rc = pptk_rx_batch_device(t->ctx, &b, st)) != 0)
       break;
+    if (cs) {   /* the gather beside the next batch, on the CUs left to it */
+      CHECK_HIP(hipEventRecord(kdone[r & 1], st));
+      CHECK_HIP(hipStreamWaitEvent(cs, kdone[r & 1], 0));
+      if ((t->rc = pptk_rx_allgather_hash(t->ctx, b.d_hash, per, d_out, cs)) != 0)
+        break;
+      CHECK_HIP(hipEventRecord(gdone[r & 1], cs));
+      continue;
+    }
     if ((t->rc = pptk_rx_allgather_hash(t->ctx, b.d_hash, per, d_out, st)) != 0)
       break;
     /* bounded wait with RCCL error checks: -ECANCELED once a sibling failed */
     t->rc = pptk_rx_comm_sync(t->ctx, st, 0);
   }
+  if (cs && t->rc == 0 && (t->rc = pptk_rx_comm_sync(t->ctx, cs, 0)) == 0)
+    t->rc = pptk_rx_comm_sync(t->ctx, st, 0);
   if (t->rc)
     goto out;
   CHECK_HIP(hipMemcpy(h_recs, ring.d_recs, count * sizeof(struct pptk_rx_rec), hipMemcpyDeviceToHost));
@@ -224,9 +258,22 @@ out:
   trace("rank %d: done, rc %d", t->rank, t->rc);
   if (t->rc)
     fail_all();
+  if (cs) {
+    (void)pptk_rx_comm_sync(t->ctx, cs, 0);
+    (void)pptk_rx_stream_destroy(cs);
+  }
   if (st) {   /* drained: aborted gathers return, pptk_rx_comm_sync waited */
     (void)pptk_rx_comm_sync(t->ctx, st, 0);
-    (void)hipStreamDestroy(st);
+    if (cs)
+      (void)pptk_rx_stream_destroy(st);
+    else
+      (void)hipStreamDestroy(st);
+  }
+  for (int k = 0; k < 2; k++) {
+    if (kdone[k])
+      (void)hipEventDestroy(kdone[k]);
+    if (gdone[k])
+      (void)hipEventDestroy(gdone[k]);
   }
   (void)pptk_rx_ring_free(&ring);
   (void)pptk_rx_gather_free(&gat);
@@ -261,6 +308,7 @@ int main(int argc, char **argv)
     return 1;
   }
   g_join_threads = (e = getenv("RX_MULTIGPU_JOIN")) && !strcmp(e, "threads");
+  g_split = (e = getenv("RX_MULTIGPU_SPLIT")) ? atoi(e) : 0;
   if ((e = getenv("RX_MULTIGPU_FAIL")))
     g_fail_rank = atoi(e);
   g_trace = (e = getenv("RX_MULTIGPU_TRACE")) && *e == '1';

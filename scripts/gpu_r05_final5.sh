@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 5 closing tree with the collective's CU split (pptk_rx_stream_split):
+# the whole GPU suite, smoke, the default bench line (untraced; its own
+# same-run PMC passes give roofline.traffic), then the N > 1 code path on one
+# GPU (a one-rank RCCL communicator) unsplit, as the forced line runs by
+# default, and split (PPTK_BENCH_COLL_CUS=32, as N > 1 runs).
+cd $GRAFT_REPO_ROOT
+source scripts/gpu_steps.sh
+export TMPDIR=/tmp
+O=gpurun_out/r05final5
+mkdir -p $O
+step gputests 700 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests -m gpu || exit $?
+grep -E "passed|failed" $O/gputests.log | tail -1
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+step bench 900 python -u bench.py --detail $O/bench_detail.json || exit $?
+grep '^{' $O/bench.log | tail -1 > $O/bench.json
+tail -c 600 $O/bench.json
+export PPTK_BENCH_FORCE_DIST=1
+step bench_dist1 500 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 20 --warmup 5 --no-secondary --no-cpu --no-live-pmc --detail $O/dist1_detail.json || exit $?
+grep '^{' $O/bench_dist1.log | tail -1 > $O/bench_dist1.json
+PPTK_BENCH_COLL_CUS=32 step bench_dist1_split 500 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29520 bench.py --gpus 1 --steps 20 --warmup 5 --no-secondary --no-cpu --no-live-pmc --detail $O/dist1_split_detail.json || exit $?
+unset PPTK_BENCH_FORCE_DIST
+grep '^{' $O/bench_dist1_split.log | tail -1 > $O/bench_dist1_split.json
+python3 -c "
+import json
+for f in ('bench_dist1', 'bench_dist1_split'):
+    d=json.load(open('$O/'+f+'.json')); print(f, d['value'], d['value_no_gather'], d['allgather']['overlap_loss'], d['allgather'].get('coll_cus'))"

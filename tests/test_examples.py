@@ -106,6 +106,20 @@ def test_rx_multigpu_allgather_bit_exact(tmp_path):
 
 
 @pytest.mark.gpu
+def test_rx_multigpu_split_overlap_bit_exact(tmp_path):
+    """RX_MULTIGPU_SPLIT=32: the gathers on their own stream beside the next
+    batch, the chip's CUs split between the two (pptk_rx_stream_split),
+    batch r waiting for gather r - 2; four rounds, bit-exact as above."""
+    p = str(tmp_path / "s.rxq")
+    n = write_rxq(p)
+    env = dict(os.environ, RX_MULTIGPU_SPLIT="32")
+    out = subprocess.run([build(tmp_path, "rx_multigpu", hip=True), p, "1", "4"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert f"{n} frames, 0 mismatches" in out.stdout
+
+
+@pytest.mark.gpu
 def test_rx_multigpu_thread_join_bit_exact(tmp_path):
     """The per-process join form in threads (RX_MULTIGPU_JOIN=threads: a uid
     from main, pptk_rx_comm_create in every rank's thread), one rank per GPU:
