@@ -258,24 +258,28 @@ out:
   trace("rank %d: done, rc %d", t->rank, t->rc);
   if (t->rc)
     fail_all();
-  if (cs) {
+  if (cs)
     (void)pptk_rx_comm_sync(t->ctx, cs, 0);
-    (void)pptk_rx_stream_destroy(cs);
-  }
-  if (st) {   /* drained: aborted gathers return, pptk_rx_comm_sync waited */
+  if (st)   /* drained: aborted gathers return, pptk_rx_comm_sync waited */
     (void)pptk_rx_comm_sync(t->ctx, st, 0);
-    if (cs)
-      (void)pptk_rx_stream_destroy(st);
-    else
-      (void)hipStreamDestroy(st);
-  }
+  /* the events before the streams they were recorded on (destroying them
+   * the other way round hung this thread now and then) */
   for (int k = 0; k < 2; k++) {
     if (kdone[k])
       (void)hipEventDestroy(kdone[k]);
     if (gdone[k])
       (void)hipEventDestroy(gdone[k]);
   }
+  trace("rank %d: events destroyed", t->rank);
+  if (cs) {
+    (void)pptk_rx_stream_destroy(cs);
+    (void)pptk_rx_stream_destroy(st);
+  } else if (st) {
+    (void)hipStreamDestroy(st);
+  }
+  trace("rank %d: streams destroyed", t->rank);
   (void)pptk_rx_ring_free(&ring);
+  trace("rank %d: ring freed", t->rank);
   (void)pptk_rx_gather_free(&gat);
   (void)hipFree(d_off);
   (void)hipFree(d_len);

@@ -369,7 +369,6 @@ class RxContext:
             o.comm_timeout_ms = comm_timeout_ms
         self._ctx = ctypes.c_void_p()
         self._inflight = collections.deque()   # (pkts, out) of submitted host batches
-        self._split = []                       # HIP streams of stream_split
         rc = L.pptk_rx_ctx_create(ctypes.byref(self._ctx), ctypes.byref(o))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_ctx_create failed ({rc})")
@@ -716,26 +715,25 @@ class RxContext:
         streams on this context's device, the collective's holding coll_cus
         CUs (a multiple of 32 on an MI355X) and the batches' the rest; the
         context sizes its grids for the rest until stream_join().  The HIP
-        streams live until stream_join() or close()."""
+        streams live until the process exits (see stream_join)."""
         import torch
         a, b = ctypes.c_void_p(), ctypes.c_void_p()
         rc = self._L.pptk_rx_stream_split(self._ctx, coll_cus, ctypes.byref(a), ctypes.byref(b))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_stream_split({coll_cus}) failed ({rc})")
-        self._split.extend([a.value, b.value])
         dev = torch.device("cuda", self.device)
         return (torch.cuda.ExternalStream(a.value, device=dev),
                 torch.cuda.ExternalStream(b.value, device=dev))
 
     def stream_join(self):
-        """Undo stream_split: the whole chip for this context's grids again;
-        the split streams are destroyed (work on them still completes)."""
+        """Undo stream_split: the whole chip for this context's grids again.
+        The split's HIP streams are not destroyed here: torch events recorded
+        on them may outlive this call (an event destroyed after its stream
+        hung the process now and then, examples/rx_multigpu.c), so they live
+        until the process exits."""
         if not hasattr(self._L, "pptk_rx_stream_split"):
             return
         self._L.pptk_rx_stream_split(self._ctx, 0, None, None)
-        while self._split:
-            h = self._split.pop()
-            self._L.pptk_rx_stream_destroy(h)
 
     def bin_device(self, lens, n, stream=None):
         """Stable permutation of 0..n-1 by length class (torch uint32 tensor)."""

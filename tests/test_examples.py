@@ -112,11 +112,22 @@ def test_rx_multigpu_split_overlap_bit_exact(tmp_path):
     batch r waiting for gather r - 2; four rounds, bit-exact as above."""
     p = str(tmp_path / "s.rxq")
     n = write_rxq(p)
-    env = dict(os.environ, RX_MULTIGPU_SPLIT="32")
-    out = subprocess.run([build(tmp_path, "rx_multigpu", hip=True), p, "1", "4"],
-                         capture_output=True, text=True, timeout=300, env=env)
-    assert out.returncode == 0, out.stdout + out.stderr
-    assert f"{n} frames, 0 mismatches" in out.stdout
+    env = dict(os.environ, RX_MULTIGPU_SPLIT="32", RX_MULTIGPU_TRACE="1",
+               RX_MULTIGPU_TIMEOUT_MS="20000")
+    exe = build(tmp_path, "rx_multigpu", hip=True)
+    with open(tmp_path / "out", "w+") as fo, open(tmp_path / "err", "w+") as fe:
+        pr = subprocess.Popen([exe, p, "1", "4"], stdout=fo, stderr=fe, env=env)
+        try:
+            rc = pr.wait(timeout=90)
+        except subprocess.TimeoutExpired:
+            pr.kill()
+            pr.wait()
+            rc = "killed"
+        fo.seek(0)
+        fe.seek(0)
+        out, err = fo.read(), fe.read()
+    assert rc == 0, (rc, out, err)
+    assert f"{n} frames, 0 mismatches" in out
 
 
 @pytest.mark.gpu
