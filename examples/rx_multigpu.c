@@ -105,6 +105,12 @@ struct gpu_thread {
   const struct rxq_set *set;
   unsigned long rec_mismatches, hash_mismatches;
   int rc;
+  /* RX_MULTIGPU_SPLIT: the split streams and their events, destroyed by
+   * main after the context (RCCL keeps the gather stream until its
+   * communicator is destroyed; a device-wide wait after destroying it first
+   * hung now and then) */
+  hipStream_t split_st, split_cs;
+  hipEvent_t split_ev[4];
 };
 
 #define CHECK_HIP(x)                 \
@@ -262,22 +268,16 @@ out:
     (void)pptk_rx_comm_sync(t->ctx, cs, 0);
   if (st)   /* drained: aborted gathers return, pptk_rx_comm_sync waited */
     (void)pptk_rx_comm_sync(t->ctx, st, 0);
-  /* the events before the streams they were recorded on (destroying them
-   * the other way round hung this thread now and then) */
-  for (int k = 0; k < 2; k++) {
-    if (kdone[k])
-      (void)hipEventDestroy(kdone[k]);
-    if (gdone[k])
-      (void)hipEventDestroy(gdone[k]);
-  }
-  trace("rank %d: events destroyed", t->rank);
-  if (cs) {
-    (void)pptk_rx_stream_destroy(cs);
-    (void)pptk_rx_stream_destroy(st);
+  if (cs) {   /* main destroys them after the context */
+    t->split_st = st;
+    t->split_cs = cs;
+    for (int k = 0; k < 2; k++) {
+      t->split_ev[k] = kdone[k];
+      t->split_ev[2 + k] = gdone[k];
+    }
   } else if (st) {
     (void)hipStreamDestroy(st);
   }
-  trace("rank %d: streams destroyed", t->rank);
   (void)pptk_rx_ring_free(&ring);
   trace("rank %d: ring freed", t->rank);
   (void)pptk_rx_gather_free(&gat);
@@ -368,6 +368,16 @@ int main(int argc, char **argv)
     pptk_rx_ctx_destroy(g_ctx[i]);   /* destroys the communicator too */
   }
   trace("contexts destroyed");
+  for (i = 0; i < nr; i++) {   /* RX_MULTIGPU_SPLIT: events, then their streams */
+    if (!thr[i].split_cs)
+      continue;
+    (void)hipSetDevice(thr[i].device);
+    for (int k = 0; k < 4; k++)
+      if (thr[i].split_ev[k])
+        (void)hipEventDestroy(thr[i].split_ev[k]);
+    (void)pptk_rx_stream_destroy(thr[i].split_cs);
+    (void)pptk_rx_stream_destroy(thr[i].split_st);
+  }
   printf("rx_multigpu: %d ranks on %d GPUs, %u frames, %lu mismatches%s\n", g_nranks,
          g_nranks < ndev ? g_nranks : ndev, set.h.n, bad, failed ? ", FAILED" : "");
   rxq_free(&set);

@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round 5: the split example hung now and then after its run, in the
-# cleanup (the trace stopped after "done"), when its streams were destroyed
-# before the events recorded on them; now the events go first.  The
-# unsplit and split example tests, three times, each pass required.
+# cleanup, after destroying the stream its gathers ran on: in the device-wide
+# waits of the frees, or in the communicator teardown.  Now main destroys
+# the split streams (events first) after the contexts.
+# The unsplit and split example tests, three times, each pass required.
 cd $GRAFT_REPO_ROOT
 source scripts/gpu_steps.sh
 export TMPDIR=/tmp
