@@ -572,9 +572,10 @@ int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint
  * any stream.  coll_cus: a multiple of 4 x the device's XCC count (32 on an
  * MI355X), below its CU count; -EINVAL otherwise.  coll_cus 0 (streams
  * NULL allowed) gives the context the whole chip again.  Destroy the
- * streams with pptk_rx_stream_destroy, after every event recorded on them
- * (an event destroyed after its stream hung the calling thread now and
- * then on ROCm 7.2). */
+ * streams with pptk_rx_stream_destroy after the events recorded on them
+ * and after the context (its communicator): a gather stream destroyed
+ * first made later device-wide waits, or the communicator's teardown, hang
+ * now and then. */
 int pptk_rx_stream_split(struct pptk_rx_ctx *ctx, int coll_cus, void **rx_stream,
                          void **coll_stream);
 int pptk_rx_stream_destroy(void *stream);

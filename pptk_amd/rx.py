@@ -728,9 +728,10 @@ class RxContext:
     def stream_join(self):
         """Undo stream_split: the whole chip for this context's grids again.
         The split's HIP streams are not destroyed here: torch events recorded
-        on them may outlive this call (an event destroyed after its stream
-        hung the process now and then, examples/rx_multigpu.c), so they live
-        until the process exits."""
+        on them may outlive this call, and a gather stream must outlive the
+        communicator (destroyed first, later device-wide waits or the
+        teardown hung now and then: DESIGN.md section 8), so they live until
+        the process exits."""
         if not hasattr(self._L, "pptk_rx_stream_split"):
             return
         self._L.pptk_rx_stream_split(self._ctx, 0, None, None)
