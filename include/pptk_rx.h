@@ -569,7 +569,9 @@ int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint
  * pptk_rx_allgather_hash) may use `coll_cus` CUs -- the same number in
  * every shader engine of every XCC -- and *rx_stream (for the batches) the
  * rest; the context sizes its receive grids for the rest from now on, on
- * any stream.  coll_cus: a multiple of 4 x the device's XCC count (32 on an
+ * any stream, and the rate limiter's one-launch path
+ * (pptk_rx_permit_keys_device) its grid too; launch only the collective on
+ * *coll_stream.  coll_cus: a multiple of 4 x the device's XCC count (32 on an
  * MI355X), below its CU count; -EINVAL otherwise.  coll_cus 0 (streams
  * NULL allowed) gives the context the whole chip again.  Destroy the
  * streams with pptk_rx_stream_destroy after the events recorded on them

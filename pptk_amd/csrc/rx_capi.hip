@@ -1001,7 +1001,9 @@ static int permit_common(struct pptk_rx_ctx *c, const struct pptk_rx_rec *d_recs
   a.verdict = d_verdict;
   a.hash_size = hs;
   a.family = family;
-  a.ncu = c->ncu;
+  // the fused kernel's workgroups must all be resident at once (grid
+  // barriers): no more than the CUs a split leaves the batches' stream
+  a.ncu = c->ncu - c->coll_cus;
   a.force_passes =
       c->permit_passes || (env_tune() >= 0 && (env_tune() & PPTK_RX_TUNE_PERMIT_PASSES)) ? 1 : 0;
   return hip_err(launch_permit(a, d_scratch, (hipStream_t)stream));

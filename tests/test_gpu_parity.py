@@ -965,6 +965,25 @@ def test_stream_split(dev):
         got = ctx.batch_device(b["frames"], n, stream=s, **kw)
         s.synchronize()
         assert torch.equal(got, want)
+    # the rate limiter's one-launch path (grid barriers) on the batches'
+    # stream: its grid fits the CUs the split leaves it
+    rng = np.random.default_rng(5)
+    nk, hs = 1 << 22, 1 << 16
+    keys = torch.from_numpy(rng.integers(0, hs, nk).astype(np.int32)).to(dev)
+    tok0 = torch.from_numpy(rng.integers(0, 64, hs).astype(np.int32)).to(dev)
+    pctx = RxContext(0, bytes(range(1, 17)), iphash_bits4=24, iphash_bits6=48, iphash_size=hs)
+    t_ref = tok0.clone()
+    v_ref = pctx.permit_keys_device(keys, 4, t_ref)
+    torch.cuda.synchronize()
+    prx, _ = pctx.stream_split(32)
+    t_got = tok0.clone()
+    scratch = torch.empty(pctx._L.pptk_rx_permit_scratch_bytes(nk, hs), dtype=torch.uint8,
+                          device=dev)
+    v_got = pctx.permit_keys_device(keys, 4, t_got, scratch=scratch, stream=prx)
+    assert pctx.permit_status(scratch, stream=prx) == 0
+    assert torch.equal(v_got, v_ref) and torch.equal(t_got, t_ref)
+    pctx.stream_join()
+    pctx.close()
     ctx.stream_join()
     got = ctx.batch_device(b["frames"], n, **kw)
     torch.cuda.synchronize()
