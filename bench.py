@@ -1394,8 +1394,11 @@ def main():
         # (pptk_rx_stream_split; placement and autotune probes run split too).
         # A one-rank gather (PPTK_BENCH_FORCE_DIST) launches nothing that
         # needs CUs: split only when asked.
-        split = ctx.stream_split(COLL_CUS)
-        torch.cuda.set_stream(split[0])
+        try:
+            split = ctx.stream_split(COLL_CUS)
+            torch.cuda.set_stream(split[0])
+        except OSError as e:   # e.g. a partitioned GPU with fewer CUs: run unsplit
+            log(f"[rank {rank}] no CU split ({e}); the gather shares the CUs")
     prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, gbs, check,
                       args.settle, first=first, place=place, n_gather_total=n_total,
                       coll_stream=split[1] if split else None)
