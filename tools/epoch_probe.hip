@@ -14,6 +14,11 @@
 //   MODE 3: as 1, the period's start shifted by (blockIdx % 8) / 8 of a
 //           period -- each XCD's waves write together, the eight XCDs in turn.
 //   MODE 4: as 3 with (blockIdx % 2) / 2: two groups of XCDs in turn.
+//   MODE 5: a fifth wave per workgroup writes: the four streaming waves hand
+//           each tile's run to it through LDS and never store themselves
+//           (their wait counters then hold loads only).
+//   MODE 6: as 5, the writer holding each run until the clock enters a new
+//           period of P ticks, or until its wave has the next run ready.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -89,9 +94,102 @@ __global__ __launch_bounds__(256) void epoch_kernel(const uint8_t *in, uint64_t 
   if (x == 0x9e3779b9u) sink[lane] = x;
 }
 
+__device__ __forceinline__ uint32_t lds_ld(uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool PHASED>
+__global__ __launch_bounds__(320) void epoch_writer_kernel(const uint8_t *in, uint64_t ntiles,
+                                                           uint32_t tile_bytes, u32x4 *recs,
+                                                           uint64_t period, uint32_t *sink) {
+  __shared__ u32x4 stash[4][256];
+  __shared__ uint32_t flag[4], want[4], done[4];
+  __shared__ uint64_t stile[4], sdead[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x / 64;
+  if (threadIdx.x < 4) {
+    flag[threadIdx.x] = want[threadIdx.x] = done[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  const uint32_t nins = (tile_bytes + 1023) / 1024;
+  if (wv < 4) {
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < ntiles; t += nwaves) {
+      const uint8_t *base = in + t * (uint64_t)tile_bytes;
+      for (uint32_t i = 0; i < nins; i += 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t o = min((i + k) * 1024u + (uint32_t)lane * 16u, tile_bytes - 16u);
+          v[k] = __builtin_nontemporal_load((const u32x4 *)(base + o));
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= v[k];
+      }
+      // hand the run over: wait until the writer has emptied this wave's stash
+      if (lds_ld(&flag[wv]) != 0) {
+        if (lane == 0) lds_st(&want[wv], 1u);
+        while (lds_ld(&flag[wv]) != 0) __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) stash[wv][k * 64 + lane] = acc;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) {
+        stile[wv] = t;
+        const uint64_t rt = __builtin_amdgcn_s_memrealtime();
+        sdead[wv] = rt - rt % period + period;
+        lds_st(&want[wv], 0u);
+        lds_st(&flag[wv], 1u);
+      }
+    }
+    if (lane == 0) lds_st(&done[wv], 1u);
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9e3779b9u) sink[lane] = x;
+  } else {
+    // the writer: every streaming wave's stash, in turn, until all are done
+    for (;;) {
+      bool finished = true;
+      const uint64_t now = PHASED ? __builtin_amdgcn_s_memrealtime() : 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t d = lds_ld(&done[w]);
+        if (lds_ld(&flag[w]) != 0) {
+          if (!PHASED || d || lds_ld(&want[w]) || now >= sdead[w]) {
+            u32x4 *q = recs + stile[w] * 256;
+            u32x4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = stash[w][k * 64 + lane];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v[k], q + k * 64 + lane);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) lds_st(&flag[w], 0u);
+          }
+          finished = false;
+        } else if (!d) {
+          finished = false;
+        }
+      }
+      if (finished) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
 extern "C" int epoch_probe_run(const void *in, uint64_t ntiles, uint32_t tile_bytes, void *recs,
                                int mode, uint64_t period, int grid, uint32_t *sink, void *stream) {
   if (tile_bytes < 16 || tile_bytes % 16 || period == 0) return -22;
+  if (mode == 5 || mode == 6) {
+    if (mode == 5)
+      hipLaunchKernelGGL(epoch_writer_kernel<false>, dim3(grid), dim3(320), 0, (hipStream_t)stream,
+                         (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
+    else
+      hipLaunchKernelGGL(epoch_writer_kernel<true>, dim3(grid), dim3(320), 0, (hipStream_t)stream,
+                         (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   if (mode == 0)
     hipLaunchKernelGGL(epoch_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t *)in, ntiles, tile_bytes, (u32x4 *)recs, period, sink);

@@ -5,6 +5,7 @@ allocation), beside the rx kernel on the same frames.  Interleaved in one
 process; prints JSON (median ms per setting).
 
     python tools/epoch_probe.py [--rounds 4] [--out FILE]
+    EPOCH_SWEEP=stagger|depth|writer (default stagger)
 """
 import argparse
 import ctypes
@@ -48,7 +49,14 @@ def main():
     ntiles = n // 64
     settings = [("rx", None, 0, 0)]
     sweep = os.environ.get("EPOCH_SWEEP", "stagger")
-    if sweep == "depth":
+    if sweep == "writer":   # a fifth wave per workgroup writes the runs
+        for bpc in (2, 3):
+            settings.append((f"tile_end_b{bpc}", 0, 1, bpc))
+            settings.append((f"phase30us_b{bpc}", 1, 3000, bpc))
+            settings.append((f"writer_b{bpc}", 5, 1, bpc))
+            for per in (2000, 3000, 4000):
+                settings.append((f"writer_phase{per // 100}us_b{bpc}", 6, per, bpc))
+    elif sweep == "depth":
         for bpc in (2, 3):
             settings.append((f"tile_end_b{bpc}", 0, 1, bpc))
             for per in (2000, 3000, 4000, 6000):
