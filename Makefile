@@ -1,5 +1,7 @@
 # Build of libpptkrx.so (product) and the oracle (test infrastructure).
-#   make            -> pptk_amd/libpptkrx.so + oracle/liboracle.so (+ oracle/_ref)
+#   make            -> pptk_amd/libpptkrx.so + oracle/liboracle.so (+ oracle/_ref),
+#                      tests/hooks/libpptkrx_hooks.so, harness/*.so
+#   make tools      -> the probe libraries under tools/ (not built by default)
 # gfx950 only; hipcc cross-compiles without a GPU.
 HIPCC ?= /opt/rocm/bin/hipcc
 CC ?= gcc
@@ -68,38 +70,26 @@ clean:
 
 .PHONY: all oracle clean asm
 
-# bench/test tooling: synthetic frames generated in HBM
-tools/libpptksynth.so: tools/synth.hip
+# Measurement harness (bench.py and the GPU tests): synthetic frames generated
+# in HBM and the trivial kernels that give the box's speed of light.
+HARNESS_LIBS := harness/libpptksynth.so harness/libmembench.so harness/librwmix.so
+
+harness/lib%.so: harness/%.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
-all: tools/libpptksynth.so
-
-tools/libmembench.so: tools/membench.hip
+harness/libpptksynth.so: harness/synth.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
-all: tools/libmembench.so
+all: $(HARNESS_LIBS)
 
-tools/librwmix.so: tools/rwmix.hip
+# Probes (measured-and-kept evidence for DESIGN.md, not part of the product
+# or of the default build): make tools
+PROBE_LIBS := tools/libglds_probe.so tools/libteam_probe.so tools/libepoch_probe.so \
+              tools/libstandin.so
+
+tools/lib%.so: tools/%.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
 
-all: tools/librwmix.so
+tools: $(PROBE_LIBS)
 
-tools/libglds_probe.so: tools/glds_probe.hip
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
-
-all: tools/libglds_probe.so
-
-tools/libteam_probe.so: tools/team_probe.hip
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
-
-all: tools/libteam_probe.so
-
-tools/libepoch_probe.so: tools/epoch_probe.hip
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
-
-all: tools/libepoch_probe.so
-
-tools/libstandin.so: tools/standin.hip
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -o $@ $<
-
-all: tools/libstandin.so
+.PHONY: tools

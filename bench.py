@@ -352,7 +352,7 @@ def run_config(cfg, n, ctx, dev, ws, rank, steps, warmup, gbs, check, settle=SET
     hashes after every launch, on a second stream: `coll_stream`, or a new
     one) or None.  compact: 32-byte records (struct pptk_rx_rec32)."""
     import torch
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     first = rank * n if first is None else first
     b = batch if batch is not None else make_batch(cfg, n, dev, first=first)
     torch.cuda.synchronize(dev)
@@ -504,7 +504,7 @@ def gathered_check(prim, gbs, n, dev, k=GATHER_CHECK_FRAMES):
     run through the CPU oracle, equal their gathered slots."""
     import torch
     from oracle.oracle import Oracle, make_opts
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     gb = gbs[0]
     got = gb.out.cpu().numpy().view(np.uint64)
     own = prim["_recs"].view(torch.int64)[:, 0] if prim["_recs"].shape[1] == 64 else None
@@ -685,7 +685,7 @@ def mix_sol(b, recs, n):
     and writing the tile's records, nothing computed; None if the shapes do
     not fit.  A real ceiling only if the rx kernel never beats it
     (roofline.mix_sol_frac <= 1)."""
-    from tools.rwmix import sol_ms
+    from harness.rwmix import sol_ms
     ntiles = n // 64
     if ntiles == 0:
         return None
@@ -958,7 +958,7 @@ def rewrite_bench(ctx, n, dev, rank, steps, warmup):
     each frame is read once, 14 bytes of it written)."""
     import torch
     from pptk_amd.records import REWRITE_DTYPE
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     b = make_batch("c64", n, dev, first=rank * n)
     rw = np.zeros(1, REWRITE_DTYPE)
     rw["ops"], rw["src"], rw["dst"], rw["sport"], rw["dport"] = 0x1F, 0xC0A80A01, 0x0A000002, 4242, 443
@@ -1050,7 +1050,7 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
     `runs` selects the runs (profiling: one run per PMC pass)."""
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     b = make_batch("c64", n, dev, first=rank * n)
     ctx = RxContext(dev.index, KEY, 24, 0, hash_size, lib_path=lib_path)
     if tune is not None:          # (A/B: PPTK_RX_TUNE_PERMIT_PASSES = the four-launch path)
@@ -1151,7 +1151,7 @@ def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", 1 << 20, False), ("c64", 1 << 22
     import torch
     from pptk_amd.records import REC_DTYPE, diff_records
     from pptk_amd.rx import RxContext, ldp_packets
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     threads, _ = _cpu_topology()
     gt = max(1, min(8, threads))
     ceil = pcie_ceiling(dev)
@@ -1439,7 +1439,7 @@ def main():
 
     box = None
     if not args.no_membench:
-        from tools.membench import measure
+        from harness.membench import measure
         box = measure(prim["_batch"]["frames"])
         sol = mix_sol(prim["_batch"], prim["_recs"], n)
         if sol:

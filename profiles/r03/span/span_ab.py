@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from pptk_amd.rx import VARIANTS, RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfgs", default="cmix,imix,c1500")
     ap.add_argument("--reps", type=int, default=10)

@@ -20,7 +20,7 @@ def run(gap, n=70_000, L=1500):
     import torch
     from oracle.oracle import Oracle, make_opts
     from pptk_amd.rx import RxContext, ldp_packets
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     b = make_batch("c1500", n, dev)
     src = b["frames"][: n * L].cpu().numpy().reshape(n, L)

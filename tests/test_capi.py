@@ -147,7 +147,7 @@ def test_bench_and_tools_compile():
     interpreter rejects what the local parser might let through)."""
     import py_compile
     for f in ("bench.py", "__graft_entry__.py", "tools/ab.py", "tools/e2e.py",
-              "tools/membench.py", "tools/synth.py", "tools/pmc_summary.py",
+              "harness/membench.py", "harness/synth.py", "harness/rwmix.py", "tools/pmc_summary.py",
               "tools/permit_run.py", "tools/permit_pmc.py"):
         py_compile.compile(os.path.join(ROOT, f), doraise=True)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],

@@ -680,7 +680,7 @@ def test_host_batch_worker_pool_large_chunks(cfg, dev):
     import threading
     from oracle.oracle import Oracle, make_opts
     from pptk_amd.rx import RxContext, ldp_packets
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = 200_000 if cfg == "c64" else 70_000
     b = make_batch(cfg, n, dev)
     stride = b["stride"]
@@ -778,7 +778,7 @@ def test_mixed_shape_kernel_vs_oracle(cfg, oracle_lib, dev):
     the CPU oracle, in batch order and in a binned processing order."""
     from oracle.oracle import make_opts
     from pptk_amd.rx import RxContext, VARIANTS
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = 1 << 17
     b = make_batch(cfg, n, dev)
     host = b["frames"].cpu().numpy()
@@ -817,7 +817,7 @@ def test_mixed_shape_kernel_full_size(cfg, dev):
     checksums, ~1 % of frames corrupted) -- size-independent properties."""
     from pptk_amd.records import F_IP_OK, F_L4_OK, F_PARSED
     from pptk_amd.rx import RxContext, VARIANTS
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = 1 << 24
     b = make_batch(cfg, n, dev)
     kw = dict(off=b["off"], lens=b["lens"], max_len=b["max_len"])
@@ -844,7 +844,7 @@ def test_autotune_keeps_records(layout, dev):
     CPU oracle's, bit for bit."""
     from oracle.oracle import Oracle, make_opts
     from pptk_amd.rx import RxContext, VARIANTS
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = 1 << 17
     b = make_batch("c1500" if layout == "fixed" else "cmix", n, dev)
     kw = (dict(stride=b["stride"], fixed_len=b["fixed_len"]) if "off" not in b else
@@ -942,7 +942,7 @@ def test_stream_split(dev):
     split or not, and after the join."""
     import ctypes
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = 1 << 16
     b = make_batch("c1500", n, dev)
     kw = dict(stride=b["stride"], fixed_len=b["fixed_len"])

@@ -69,7 +69,7 @@ def test_rewrite_keeps_verdicts_large(dev):
     transform still verifies exactly the frames it verified before (but for
     UDP checksums of 0), and its records carry the new addresses and ports."""
     from pptk_amd.records import F_IP_OK, F_L4_OK, F_UDP_ZERO, REWRITE_DTYPE, as_records
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     ctx = _ctx()
     for cfg, n in (("c64", 1 << 20), ("c1500", 1 << 17)):
         b = make_batch(cfg, n, dev)

@@ -85,7 +85,7 @@ def test_tx_c1500_fixed_stride_vs_oracle(dev):
     through the two-pass tx against the CPU restatement's tx_batch, twice
     (the second call reuses the context's side array)."""
     from oracle.oracle import Oracle
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = 20_000
     b = make_batch("c1500", n, dev)
     host = b["frames"][: n * 1500].cpu().numpy().copy()
@@ -135,7 +135,7 @@ def test_tx_two_streams_one_context(dev):
     batches get exactly the reference's checksums; repeated so the pool's
     reuse is exercised too."""
     from oracle.oracle import Oracle
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = 40_000
     ba = make_batch("c1500", n, dev, first=0)
     bb = make_batch("c1500", n, dev, first=n)

@@ -48,8 +48,8 @@ def parse_setting(a):
 def main():
     import torch
     from pptk_amd.rx import RxContext
-    from tools.membench import measure
-    from tools.synth import make_batch
+    from harness.membench import measure
+    from harness.synth import make_batch
     cfg = sys.argv[1]
     settings = [parse_setting(a) for a in sys.argv[2:]]
     libs = {"": None}

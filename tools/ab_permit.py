@@ -19,7 +19,7 @@ def main():
     import torch
     import bench
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n, hs = 16 * 1024 * 1024, 1 << 16
     libs = {"": None}

@@ -19,7 +19,7 @@ def main():
     import torch
     from pptk_amd.records import REWRITE_DTYPE
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     cfg = sys.argv[1]
     names = sys.argv[2:] or [""]
     libs = {"": None}

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     cfg = sys.argv[1]
     def parse(a):
         p = a.split(":")

@@ -14,7 +14,7 @@ def main():
     import torch
     from pptk_amd.records import REC32_DTYPE, to_rec32
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     cfg = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 16 * 1024 * 1024
     dev = torch.device("cuda", 0)

@@ -70,7 +70,7 @@ def main():
     import torch
     import bench
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     amdsmi, h = smi_handle(0)
     print(json.dumps({"idle": sample(amdsmi, h)}, default=str), flush=True)

@@ -20,7 +20,7 @@ def main():
     import torch
     from pptk_amd.records import REC_DTYPE, diff_records
     from pptk_amd.rx import RxContext, ldp_packets
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
     chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     dev = torch.device("cuda", 0)

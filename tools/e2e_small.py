@@ -22,7 +22,7 @@ def main():
     import torch
     from pptk_amd.records import REC_DTYPE, diff_records
     from pptk_amd.rx import RxContext, ldp_packets
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c64"
     dev = torch.device("cuda", 0)
     sizes = [int(x) for x in os.environ.get("E2E_SIZES", "32,256,1024,4096").split(",")]

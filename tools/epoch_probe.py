@@ -26,7 +26,7 @@ def main():
     import torch
     import bench
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     L = ctypes.CDLL(os.path.join(HERE, "libepoch_probe.so"))
     vp = ctypes.c_void_p
     L.epoch_probe_run.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_int,

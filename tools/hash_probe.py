@@ -24,7 +24,7 @@ def main():
     import torch
     import bench
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
     dev = torch.device("cuda", 0)
     n = bench.N_PER_GPU

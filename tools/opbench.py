@@ -38,7 +38,7 @@ def gather_emul(ctx, dev, n, steps, warmup, world=8):
     (xGMI link time is not emulated: it overlaps the kernel.)"""
     import time
     import torch
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     b = make_batch("c1500", n, dev)
     recs = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     nbytes = (world - 1) * n * 8
@@ -77,7 +77,7 @@ def gather_emul_place(ctx, dev, n, steps, warmup, world=8, ncand=6):
     import time
     import torch
     import bench
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     b = make_batch("c1500", n, dev)
     kw = dict(stride=1500, fixed_len=1500)
     recs, place = bench.placed_buffers(ctx, b, n, dev, False, kw)
@@ -122,7 +122,7 @@ def main():
     args = ap.parse_args()
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     ctx = RxContext(0, bench.KEY)
     op, n = args.op, N

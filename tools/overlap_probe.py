@@ -6,7 +6,7 @@ import sys, time, json
 sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 import torch
 from pptk_amd.rx import RxContext
-from tools.synth import make_batch
+from harness.synth import make_batch
 dev = torch.device('cuda', 0)
 n = 16 * 1024 * 1024
 b = make_batch('c1500', n, dev)

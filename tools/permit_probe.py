@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=128)

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 def matrix(args):
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -61,8 +61,8 @@ def policies(args):
     store modes."""
     import torch
     from pptk_amd.rx import RxContext
-    from tools.rwmix import mix_ms
-    from tools.synth import make_batch
+    from harness.rwmix import mix_ms
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -98,7 +98,7 @@ def orders(args):
     slow, and is any allocation strategy reliably fast?"""
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -134,7 +134,7 @@ def flags(args):
     import ctypes
     import torch
     from pptk_amd.rx import RxContext, RxDevBatch
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -181,7 +181,7 @@ def keep(args):
     (empty_cache), (c) over a sustained run of 300 launches."""
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -230,7 +230,7 @@ def benchpath(args):
     import torch
     import bench
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -263,7 +263,7 @@ def txplace(args):
     spacers; tx timed on each, interleaved rounds, median per buffer."""
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -301,7 +301,7 @@ def txside(args):
     import torch
     import bench
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -345,8 +345,8 @@ def bursts(args):
     import ctypes
     import torch
     from pptk_amd.rx import RxContext
-    from tools.rwmix import _lib, sol_ms
-    from tools.synth import make_batch
+    from harness.rwmix import _lib, sol_ms
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -419,8 +419,8 @@ def xstage(args):
     import ctypes
     import torch
     from pptk_amd.rx import RxContext
-    from tools.rwmix import _lib
-    from tools.synth import make_batch
+    from harness.rwmix import _lib
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))
@@ -532,7 +532,7 @@ def main():
         return txside(args)
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = args.n
     ctx = RxContext(0, bytes(range(1, 17)))

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     L = ctypes.CDLL(os.path.join(HERE, "libteam_probe.so"))
     vp = ctypes.c_void_p
     L.team_probe_run.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_int, ctypes.c_int,
@@ -75,7 +75,7 @@ def main():
         ts.sort()
         res[k] = round(ts[len(ts) // 2], 4)
     os.environ["RWMIX_SOL_SHAPES"] = "1"
-    from tools.rwmix import sol_ms
+    from harness.rwmix import sol_ms
     ms, how = sol_ms(b["frames"], n, recs.view(n, 64), 4096, off=b["off"], lens=b["lens"])
     res["sol_ms"], res["sol_shapes"] = round(ms, 4), how.get("shapes")
     line = json.dumps(res)

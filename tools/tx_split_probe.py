@@ -33,7 +33,7 @@ def timed(fn, reps=10):
 def main():
     import torch
     from pptk_amd.rx import RxContext
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = 16 * 1024 * 1024
     ctx = RxContext(0, bytes(range(1, 17)))

@@ -24,7 +24,7 @@ def main():
     import torch
     import bench
     from pptk_amd.rx import RxContext, VARIANTS
-    from tools.synth import make_batch
+    from harness.synth import make_batch
     dev = torch.device("cuda", 0)
     n = bench.N_PER_GPU
     ctx = RxContext(0, bench.KEY)
