@@ -660,7 +660,7 @@ def compact_line(full, detail_path=None):
     elif gat:
         g = {k: gat.get(k) for k in ("ms", "algbw_gbs", "busbw_gbs", "overlap_loss", "rccl_ranks",
                                       "bytes_per_rank", "coll_cus", "split",
-                                      "nccl_max_nchannels")}
+                                      "max_ctas")}
         chk = gat.get("gathered_check") or {}
         g["gathered_check"] = {k: chk.get(k) for k in ("own_slice_equals_records",
                                                         "sampled_frames_per_rank",
@@ -1134,7 +1134,9 @@ def pcie_ceiling(dev, mb=96, reps=20):
     return round((mb << 20) * reps / (time.perf_counter() - t0) / 1e9, 2)
 
 
-def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", 1 << 20, False), ("c64", 1 << 22, True))):
+def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", "c1500", 1 << 20, False, False),
+                                      ("c64", "c64", 1 << 22, True, False),
+                                      ("c64_rec32", "c64", 1 << 22, True, True))):
     """End to end, host to host (the north star's "rate
     including pinned hipMemcpyAsync to and from the GPU"): pptk_rx_batch on
     borrowed ldp_packet frames in host memory (reference rx loop
@@ -1144,41 +1146,44 @@ def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", 1 << 20, False), ("c64", 1 << 22
     threads gather the frames into pinned staging, DMA down) and "ring" (the
     frame area registered once with pptk_rx_register_ring: dense chunks go
     down as one DMA span, nothing gathered); with `reg` the record array is
-    registered too (records written in place over PCIe, no copy back).
+    registered too (records written in place over PCIe, no copy back); with
+    `compact` the records are the 32-byte struct pptk_rx_rec32
+    (pptk_rx_batch32: half the bytes back over PCIe, what bounds C64).
     Every mode is checked bit-exact against a device-resident launch of the
     same frames before it is timed.  Reported: the faster path, Mpkt/s,
     frame GB/s and its fraction of this box's pinned H2D copy rate."""
     import torch
-    from pptk_amd.records import REC_DTYPE, diff_records
+    from pptk_amd.records import REC32_DTYPE, REC_DTYPE, diff_records
     from pptk_amd.rx import RxContext, ldp_packets
     from harness.synth import make_batch
     threads, _ = _cpu_topology()
     gt = max(1, min(8, threads))
     ceil = pcie_ceiling(dev)
     out = {"pcie_h2d_gbs": ceil, "gather_threads": gt}
-    for cfg, n, reg in cfgs:
+    for key, cfg, n, reg, compact in cfgs:
         b = make_batch(cfg, n, dev)
         stride, flen = b["stride"], b["fixed_len"]
         ring = b["frames"][: n * stride + 64].cpu().numpy()      # the host "ring"
         ctx = RxContext(0, KEY, max_batch=65536, max_frame=1518, gather_threads=gt)
-        ref = ctx.batch_device(b["frames"], n, stride=stride, fixed_len=flen)
-        want = ref.cpu().numpy()
+        ref = ctx.batch_device(b["frames"], n, stride=stride, fixed_len=flen, compact=compact)
+        dt = REC32_DTYPE if compact else REC_DTYPE
+        want = ref.cpu().numpy().reshape(-1).view(dt)
         del b, ref
         pkts = ldp_packets(ring, np.arange(n, dtype=np.uint64) * stride,
                            np.full(n, flen, np.uint16))
-        outbuf = np.zeros(n, dtype=REC_DTYPE)           # reused, as an rx loop's array
+        outbuf = np.zeros(n, dtype=dt)                  # reused, as an rx loop's array
         if reg:
             ctx.register_ring(outbuf)
         res = {}
         for mode in ("staged", "ring"):
             if mode == "ring":
                 ctx.register_ring(ring)
-            got = ctx.batch_host(pkts, out=outbuf)
-            if diff_records(got, want):
-                raise RuntimeError(f"e2e {cfg} {mode}: records differ from the device batch")
+            got = ctx.batch_host(pkts, out=outbuf, compact=compact)
+            if diff_records(got, want, dtype=dt):
+                raise RuntimeError(f"e2e {key} {mode}: records differ from the device batch")
             reps, t0 = 0, time.perf_counter()
             while time.perf_counter() - t0 < seconds:
-                ctx.batch_host(pkts, out=outbuf)
+                ctx.batch_host(pkts, out=outbuf, compact=compact)
                 reps += 1
             el = (time.perf_counter() - t0) / reps
             res[mode] = round(n / el / 1e6, 2)
@@ -1189,10 +1194,10 @@ def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", 1 << 20, False), ("c64", 1 << 22
         ctx.close()
         best = max(res, key=res.get)
         gbs = res[best] * flen / 1e3
-        out[cfg] = {"mpkts": res[best], "path": best, "frame_gbs": round(gbs, 2),
+        out[key] = {"mpkts": res[best], "path": best, "frame_gbs": round(gbs, 2),
                     "of_pcie": round(gbs / ceil, 3) if ceil else None, "frames": n,
-                    "records": "registered" if reg else "copied", "staged_mpkts": res["staged"],
-                    "ring_mpkts": res["ring"]}
+                    "records": ("registered" if reg else "copied") + (" 32 B" if compact else " 64 B"),
+                    "staged_mpkts": res["staged"], "ring_mpkts": res["ring"]}
         del ring, pkts, outbuf, want
         torch.cuda.empty_cache()
     return out
@@ -1369,15 +1374,25 @@ def main():
     n_total = args.frames * ws if args.scaling == "weak" else args.frames
     gbs = None
     comm_error = None
+    split = None
+    if dist_on(ws) and COLL_CUS > 0 and (ws > 1 or "PPTK_BENCH_COLL_CUS" in os.environ):
+        # the batches on all CUs but COLL_CUS, the gather on those
+        # (pptk_rx_stream_split; placement and autotune probes run split too),
+        # BEFORE the communicator: the library caps its channels at COLL_CUS
+        # (ncclConfig_t.maxCTAs), one RCCL block per CU left to the gather.
+        # A one-rank gather (PPTK_BENCH_FORCE_DIST) launches nothing that
+        # needs CUs: split only when asked.
+        try:
+            split = ctx.stream_split(COLL_CUS)
+        except OSError as e:   # e.g. a partitioned GPU with fewer CUs: run unsplit
+            log(f"[rank {rank}] no CU split ({e}); the gather shares the CUs")
     if dist_on(ws):
-        if COLL_CUS > 0 and (ws > 1 or "PPTK_BENCH_COLL_CUS" in os.environ):
-            # at most one RCCL block per CU the split leaves the gather, so
-            # every channel of the collective is resident at once (set before
-            # RCCL reads its environment, at the communicator's creation)
-            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(COLL_CUS))
         comm_error = join_all(ctx, ws, rank)     # RCCL communicator in libpptkrx.so
         if comm_error:
             log(f"[rank {rank}] no all-gather: {comm_error}")
+            if split:
+                ctx.stream_join()
+                split = None
         else:
             # the gather buffers are placed inside run_config, once the
             # batch's frame and record buffers are (placed_gather)
@@ -1388,17 +1403,8 @@ def main():
     check = not args.no_check
 
     primary_cfg = args.only or "c1500"
-    split = None
-    if gbs and COLL_CUS > 0 and (ws > 1 or "PPTK_BENCH_COLL_CUS" in os.environ):
-        # the batches on all CUs but COLL_CUS, the gather on those
-        # (pptk_rx_stream_split; placement and autotune probes run split too).
-        # A one-rank gather (PPTK_BENCH_FORCE_DIST) launches nothing that
-        # needs CUs: split only when asked.
-        try:
-            split = ctx.stream_split(COLL_CUS)
-            torch.cuda.set_stream(split[0])
-        except OSError as e:   # e.g. a partitioned GPU with fewer CUs: run unsplit
-            log(f"[rank {rank}] no CU split ({e}); the gather shares the CUs")
+    if split:
+        torch.cuda.set_stream(split[0])
     prim = run_config(primary_cfg, n, ctx, dev, ws, rank, args.steps, args.warmup, gbs, check,
                       args.settle, first=first, place=place, n_gather_total=n_total,
                       coll_stream=split[1] if split else None)
@@ -1429,7 +1435,8 @@ def main():
             raise RuntimeError(f"the RCCL communicator has {gat['rccl_ranks']} ranks, not {ws}")
         gat["overlap_loss"] = round(1.0 - prim["mpkts"] / nog["mpkts"], 4)
         gat["coll_cus"] = COLL_CUS if gat_split else 0
-        gat["nccl_max_nchannels"] = os.environ.get("NCCL_MAX_NCHANNELS")
+        # the channel cap the library gave the communicator (ncclConfig_t.maxCTAs)
+        gat["max_ctas"] = COLL_CUS if gat_split else None
         if gat_split:
             gat["split"] = {k: gat_split[k] for k in ("ms", "algbw_gbs", "busbw_gbs")}
         gat["buffer_placement"] = prim.get("gather_placement")

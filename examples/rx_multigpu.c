@@ -30,9 +30,17 @@
  *
  *   gcc -O2 -pthread -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude \
  *       examples/rx_multigpu.c -Lpptk_amd -lpptkrx -L/opt/rocm/lib -lamdhip64 -o rx_multigpu
- *   ./rx_multigpu frames.rxq [ranks [rounds]]
+ *   ./rx_multigpu frames.rxq [ranks [rounds [split_cus]]]
  *
  * ranks defaults to the visible GPUs; rank r runs on GPU r % visible.
+ * split_cus > 0 overlaps each gather with the next batch: the batches on one
+ * stream, the gathers on another, the chip's CUs split between them with
+ * pptk_rx_stream_split (split_cus CUs for the gathers; RCCL's kernel needs
+ * whole CUs), batch r waiting for gather r - 2 (same buffer).
+ * The split is made in main, before the communicator: the library then caps
+ * the communicator's channels at split_cus (one RCCL block per CU left to
+ * the gathers), and the two streams belong to the context, which destroys
+ * them after its communicator.
  * Environment (tests, drills):
  *   RX_MULTIGPU_JOIN=threads   every thread joins with pptk_rx_comm_create on
  *                              a uid made by main (the per-process form, in
@@ -41,12 +49,6 @@
  *                              threads) or before its first gather
  *   RX_MULTIGPU_TIMEOUT_MS=t   opts.comm_timeout_ms
  *   RX_MULTIGPU_TRACE=1        progress lines on stderr
- *   RX_MULTIGPU_SPLIT=k        overlap each gather with the next batch: the
- *                              batches on one stream, the gathers on another,
- *                              the chip's CUs split between them with
- *                              pptk_rx_stream_split (k CUs for the gathers;
- *                              RCCL's kernel needs whole CUs);
- *                              batch r waits for gather r - 2 (same buffer)
  */
 #include <errno.h>
 #include <pthread.h>
@@ -69,7 +71,7 @@ static struct pptk_rx_ctx *g_ctx[MAXR];
 static int g_nranks;
 static atomic_int g_failed;
 static int g_join_threads, g_fail_rank = -1;
-static int g_split;   /* RX_MULTIGPU_SPLIT */
+static int g_split;   /* split_cus */
 static uint8_t g_uid[PPTK_RX_COMM_UID_BYTES];
 static int g_trace;
 
@@ -105,12 +107,9 @@ struct gpu_thread {
   const struct rxq_set *set;
   unsigned long rec_mismatches, hash_mismatches;
   int rc;
-  /* RX_MULTIGPU_SPLIT: the split streams and their events, destroyed by
-   * main after the context (RCCL keeps the gather stream until its
-   * communicator is destroyed; a device-wide wait after destroying it first
-   * hung now and then) */
+  /* split_cus > 0: the context's split streams (pptk_rx_stream_split in
+   * main, before the communicator; the context owns and destroys them) */
   hipStream_t split_st, split_cs;
-  hipEvent_t split_ev[4];
 };
 
 #define CHECK_HIP(x)                 \
@@ -130,7 +129,7 @@ static void *thrfn(void *arg)
   uint64_t *d_off = NULL, *d_out = NULL, *h_off = NULL, *h_out = NULL;
   uint16_t *d_len = NULL;
   struct pptk_rx_rec *h_recs = NULL;
-  hipStream_t st = NULL, cs = NULL;   /* batches; gathers (RX_MULTIGPU_SPLIT) */
+  hipStream_t st = NULL, cs = NULL;   /* batches; gathers (split_cus > 0) */
   hipEvent_t kdone[2] = {NULL, NULL}, gdone[2] = {NULL, NULL};
   uint64_t lo = 0, hi = 0;
   struct pptk_rx_dev_batch b;
@@ -165,14 +164,11 @@ static void *thrfn(void *arg)
     }
   }
   CHECK_HIP(hipSetDevice(t->device));
-  if (g_split) {
-    /* before the rings and gather buffers: their probes run on the batches'
-     * stream, with the grid the split leaves it */
-    void *rx_s, *coll_s;
-    if ((t->rc = pptk_rx_stream_split(t->ctx, g_split, &rx_s, &coll_s)) != 0)
-      goto out;
-    st = rx_s;
-    cs = coll_s;
+  if (t->split_cs) {
+    /* the rings' and gather buffers' probes run on the batches' stream, with
+     * the grid the split leaves it */
+    st = t->split_st;
+    cs = t->split_cs;
     for (int k = 0; k < 2; k++) {
       CHECK_HIP(hipEventCreateWithFlags(&kdone[k], hipEventDisableTiming));
       CHECK_HIP(hipEventCreateWithFlags(&gdone[k], hipEventDisableTiming));
@@ -268,16 +264,14 @@ out:
     (void)pptk_rx_comm_sync(t->ctx, cs, 0);
   if (st)   /* drained: aborted gathers return, pptk_rx_comm_sync waited */
     (void)pptk_rx_comm_sync(t->ctx, st, 0);
-  if (cs) {   /* main destroys them after the context */
-    t->split_st = st;
-    t->split_cs = cs;
-    for (int k = 0; k < 2; k++) {
-      t->split_ev[k] = kdone[k];
-      t->split_ev[2 + k] = gdone[k];
-    }
-  } else if (st) {
-    (void)hipStreamDestroy(st);
+  for (int k = 0; k < 2; k++) {   /* (drained above) */
+    if (kdone[k])
+      (void)hipEventDestroy(kdone[k]);
+    if (gdone[k])
+      (void)hipEventDestroy(gdone[k]);
   }
+  if (st && !cs)   /* our own stream; the split ones are the context's */
+    (void)hipStreamDestroy(st);
   (void)pptk_rx_ring_free(&ring);
   trace("rank %d: ring freed", t->rank);
   (void)pptk_rx_gather_free(&gat);
@@ -295,6 +289,7 @@ int main(int argc, char **argv)
   struct rxq_set set;
   int ndev = pptk_rx_device_count();
   int nr = argc > 2 ? atoi(argv[2]) : ndev, rounds = argc > 3 ? atoi(argv[3]) : 3;
+  int split = argc > 4 ? atoi(argv[4]) : 0;
   const char *e;
   uint32_t timeout_ms = 0;
   struct gpu_thread thr[MAXR];
@@ -304,7 +299,7 @@ int main(int argc, char **argv)
 
   setvbuf(stdout, NULL, _IOLBF, 0);   /* every line out before anything can go wrong */
   if (argc < 2 || rxq_load(argv[1], &set) != 0) {
-    fprintf(stderr, "usage: rx_multigpu frames.rxq [ranks [rounds]]\n");
+    fprintf(stderr, "usage: rx_multigpu frames.rxq [ranks [rounds [split_cus]]]\n");
     return 1;
   }
   if (ndev < 1 || nr < 1 || nr > MAXR) {
@@ -312,7 +307,7 @@ int main(int argc, char **argv)
     return 1;
   }
   g_join_threads = (e = getenv("RX_MULTIGPU_JOIN")) && !strcmp(e, "threads");
-  g_split = (e = getenv("RX_MULTIGPU_SPLIT")) ? atoi(e) : 0;
+  g_split = split;
   if ((e = getenv("RX_MULTIGPU_FAIL")))
     g_fail_rank = atoi(e);
   g_trace = (e = getenv("RX_MULTIGPU_TRACE")) && *e == '1';
@@ -333,6 +328,17 @@ int main(int argc, char **argv)
       fprintf(stderr, "pptk_rx_ctx_create(%d): %d\n", i, rc);
       return 1;
     }
+    thr[i] = (struct gpu_thread){.rank = i, .nranks = nr, .rounds = rounds, .device = i % ndev,
+                                 .ctx = g_ctx[i], .set = &set};
+    if (g_split) {   /* before the communicator: it caps its channels at g_split */
+      void *rx_s = NULL, *coll_s = NULL;
+      if ((rc = pptk_rx_stream_split(g_ctx[i], g_split, &rx_s, &coll_s)) != 0) {
+        fprintf(stderr, "pptk_rx_stream_split(%d, %d): %d\n", i, g_split, rc);
+        return 1;
+      }
+      thr[i].split_st = rx_s;
+      thr[i].split_cs = coll_s;
+    }
   }
   if (g_join_threads)
     rc = pptk_rx_comm_uid(g_uid);
@@ -344,8 +350,6 @@ int main(int argc, char **argv)
     return 1;
   }
   for (i = 0; i < nr; i++) {
-    thr[i] = (struct gpu_thread){.rank = i, .nranks = nr, .rounds = rounds, .device = i % ndev,
-                                 .ctx = g_ctx[i], .set = &set};
     if (pthread_create(&pth[i], NULL, thrfn, &thr[i]) != 0) {
       fail_all();
       nr = i;   /* join the ones started */
@@ -364,20 +368,17 @@ int main(int argc, char **argv)
     bad += thr[i].rec_mismatches + thr[i].hash_mismatches;
   }
   for (i = 0; i < g_nranks; i++) {
+    if (thr[i].split_cs) {   /* the context's streams: not the caller's to destroy */
+      rc = pptk_rx_stream_destroy(thr[i].split_cs);
+      printf("rank %d: pptk_rx_stream_destroy(gather stream) before the context: %d%s\n", i, rc,
+             rc == -EBUSY ? " (EBUSY: the context owns it)" : "");
+      if (rc != -EBUSY)
+        failed = 1;
+    }
     trace("destroying context %d", i);
-    pptk_rx_ctx_destroy(g_ctx[i]);   /* destroys the communicator too */
+    pptk_rx_ctx_destroy(g_ctx[i]);   /* its communicator, then its split streams */
   }
   trace("contexts destroyed");
-  for (i = 0; i < nr; i++) {   /* RX_MULTIGPU_SPLIT: events, then their streams */
-    if (!thr[i].split_cs)
-      continue;
-    (void)hipSetDevice(thr[i].device);
-    for (int k = 0; k < 4; k++)
-      if (thr[i].split_ev[k])
-        (void)hipEventDestroy(thr[i].split_ev[k]);
-    (void)pptk_rx_stream_destroy(thr[i].split_cs);
-    (void)pptk_rx_stream_destroy(thr[i].split_st);
-  }
   printf("rx_multigpu: %d ranks on %d GPUs, %u frames, %lu mismatches%s\n", g_nranks,
          g_nranks < ndev ? g_nranks : ndev, set.h.n, bad, failed ? ", FAILED" : "");
   rxq_free(&set);

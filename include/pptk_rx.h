@@ -157,6 +157,15 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *ctx);
 int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
                   int num, struct pptk_rx_rec *recs);
 
+/* The same with compact 32-byte records (struct pptk_rx_rec32, the values
+ * of pptk_rx_rec minus the raw checksum words, ethertype, version and the
+ * IPv6 addresses): half the record bytes back over PCIe, which is what
+ * bounds small frames host to host (a 64-byte frame's 64-byte record moves
+ * as many bytes up as the frame moved down).  Same rules as pptk_rx_batch,
+ * including records written in place into a registered region. */
+int pptk_rx_batch32(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
+                    int num, struct pptk_rx_rec32 *recs);
+
 /* pptk_rx_batch split in two, so that an rx loop overlaps one batch's GPU
  * round trip with fetching and submitting the next (the synchronous call
  * leaves the host idle for the whole launch-to-completion latency, which
@@ -184,6 +193,10 @@ int pptk_rx_batch(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts,
 #define PPTK_RX_MAX_INFLIGHT 4
 int pptk_rx_batch_submit(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts, int num,
                          struct pptk_rx_rec *recs);
+/* pptk_rx_batch_submit with compact records (as pptk_rx_batch32); completed
+ * by pptk_rx_batch_complete like any other submission. */
+int pptk_rx_batch_submit32(struct pptk_rx_ctx *ctx, const struct ldp_packet *pkts, int num,
+                           struct pptk_rx_rec32 *recs);
 int pptk_rx_batch_complete(struct pptk_rx_ctx *ctx);
 int pptk_rx_batch_pending(const struct pptk_rx_ctx *ctx);
 
@@ -297,8 +310,10 @@ int pptk_rx_permit_device(struct pptk_rx_ctx *ctx, const struct pptk_rx_rec *d_r
  * concurrent calls never starve each other; calls that share one scratch
  * buffer must still be ordered on one stream.  Should the workgroups not
  * all become resident within 2 s (e.g. another process's kernels hold the
- * CUs), the launch aborts: verdicts undefined, the token counts left as
- * they were before the call (nothing half-updated), and
+ * CUs), the launch aborts and fails closed: every subject frame's verdict
+ * is 0 (denied, as the reference denies a frame it has no token for), the
+ * others 2, the token counts are left as they were before the call (nothing
+ * half-updated: all workgroups act on one commit-or-abort decision), and
  * pptk_rx_permit_status reports -ETIMEDOUT; never a hang.  The scratch
  * needs no initialisation. */
 int pptk_rx_permit_keys_device(struct pptk_rx_ctx *ctx, const uint32_t *d_keys, uint64_t n,
@@ -306,10 +321,12 @@ int pptk_rx_permit_keys_device(struct pptk_rx_ctx *ctx, const uint32_t *d_keys, 
                                uint8_t *d_verdict, void *d_scratch, void *stream);
 
 /* Whether every pptk_rx_permit_keys_device call on d_scratch since the last
- * status query completed: 0, or -ETIMEDOUT if one aborted (its verdicts are
- * undefined and its tokens unchanged: repeat it, e.g. with
- * PPTK_RX_TUNE_PERMIT_PASSES).  Synchronises `stream` (the stream those
- * calls ran on).  -EIO on a HIP error. */
+ * status query completed: 0, or -ETIMEDOUT if one aborted (its subject
+ * frames were denied and its tokens left unchanged: repeat it, e.g. with
+ * PPTK_RX_TUNE_PERMIT_PASSES, to get the verdicts the tokens allow).
+ * Synchronises `stream` (the stream those calls ran on).  -EIO on a HIP
+ * error.  The library tracks up to 1024 scratch buffers; a buffer not
+ * queried while 1024 others were used since reports 0. */
 int pptk_rx_permit_status(struct pptk_rx_ctx *ctx, const void *d_scratch, void *stream);
 
 /* The token refill timer (batch_timer_fn, reference iphash/iphash.c:
@@ -572,12 +589,23 @@ int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint
  * any stream, and the rate limiter's one-launch path
  * (pptk_rx_permit_keys_device) its grid too; launch only the collective on
  * *coll_stream.  coll_cus: a multiple of 4 x the device's XCC count (32 on an
- * MI355X), below its CU count; -EINVAL otherwise.  coll_cus 0 (streams
- * NULL allowed) gives the context the whole chip again.  Destroy the
- * streams with pptk_rx_stream_destroy after the events recorded on them
- * and after the context (its communicator): a gather stream destroyed
- * first made later device-wide waits, or the communicator's teardown, hang
- * now and then. */
+ * MI355X), below its CU count; -EINVAL otherwise.
+ *
+ * Order: split first, then create the communicator.  A communicator created
+ * on a split context runs at most coll_cus RCCL blocks (channels) per
+ * collective (ncclConfig_t.maxCTAs), so that all of them are resident on the
+ * CUs left to it at once; that cap is fixed at creation, so a split to a
+ * different CU count while the context has a communicator (or a creation in
+ * progress) returns -EBUSY.  A split to the count the context already holds
+ * returns the same two streams.  coll_cus 0 (streams NULL allowed) gives the
+ * context's grids the whole chip again; the streams stay valid.
+ *
+ * The streams belong to the context: pptk_rx_ctx_destroy destroys them,
+ * after its communicator (a gather stream destroyed before the communicator
+ * made later device-wide waits or the teardown hang).
+ * pptk_rx_stream_destroy returns -EBUSY for a stream its context still holds,
+ * 0 (and does nothing) for one its context has destroyed, and destroys any
+ * other stream. */
 int pptk_rx_stream_split(struct pptk_rx_ctx *ctx, int coll_cus, void **rx_stream,
                          void **coll_stream);
 int pptk_rx_stream_destroy(void *stream);

@@ -20,6 +20,8 @@
 #include <mutex>
 #include <new>
 #include <thread>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/hashseed.h"
@@ -52,8 +54,9 @@ struct RxSlot {
   uint64_t *hd_off = nullptr;
   uint16_t *hd_len = nullptr;
   pptk_rx_rec *hd_recs = nullptr;
-  pptk_rx_rec *out = nullptr;   // caller's records of the chunk in flight
+  void *out = nullptr;   // caller's records of the chunk in flight
   size_t count = 0;
+  size_t rec_bytes = 64;   // of the chunk in flight: 64 (pptk_rx_rec) or 32 (pptk_rx_rec32)
   bool busy = false;
   std::vector<PartDesc> parts;  // pptk_rx_batch's per-part descriptor sums
   std::unique_ptr<std::atomic<size_t>[]> run;   // the parts' running staging totals
@@ -163,7 +166,13 @@ struct pptk_rx_ctx {
   uint64_t *d_txuser = nullptr;   // pptk_tx_set_side_buffer
   uint64_t txuser_n = 0;
   int ncu = 256;
-  int coll_cus = 0;   // pptk_rx_stream_split: CUs left to the collective
+  int coll_cus = 0;   // pptk_rx_stream_split: CUs the grids leave to the collective now
+  // pptk_rx_stream_split's two streams, owned by the context: created by the
+  // first split (or a split to another CU count before any communicator),
+  // kept across pptk_rx_stream_split(0), destroyed by pptk_rx_ctx_destroy
+  // after the communicator; split_cus = the collective stream's CUs
+  hipStream_t split_rx = nullptr, split_coll = nullptr;
+  int split_cus = 0;
   int bpc[RX_NVARIANTS] = {};
   int forced_variant = -1;
   int forced_flags = -1;   // the receive transform's memory policy, -1 automatic
@@ -190,7 +199,37 @@ std::atomic<void *> *ctx_comm_slot(pptk_rx_ctx *c) { return &c->comm; }
 uint32_t ctx_comm_timeout_ms(const pptk_rx_ctx *c) {
   return c->opts.comm_timeout_ms ? c->opts.comm_timeout_ms : PPTK_RX_COMM_TIMEOUT_MS;
 }
+int ctx_coll_cap(const pptk_rx_ctx *c) { return c->split_coll ? c->split_cus : 0; }
 }  // namespace pptk
+
+// Streams pptk_rx_stream_split handed out, by owner (pptk_rx_stream_destroy
+// refuses them: -EBUSY), and the ones a context destroy has since destroyed
+// (a caller following the old contract -- destroy them after the context --
+// gets 0 for those instead of a second hipStreamDestroy).
+static std::mutex g_split_mu;
+static std::unordered_map<hipStream_t, const pptk_rx_ctx *> g_split_owned;
+static std::unordered_set<hipStream_t> g_split_retired;
+
+// Destroy the context's split streams (after their work; the communicator
+// that may have used the collective stream is gone or never existed).
+static void drop_split_streams(pptk_rx_ctx *c) {
+  hipStream_t s[2] = {c->split_rx, c->split_coll};
+  {
+    std::lock_guard<std::mutex> g(g_split_mu);
+    for (hipStream_t x : s)
+      if (x) {
+        g_split_owned.erase(x);
+        g_split_retired.insert(x);
+      }
+  }
+  for (hipStream_t x : s)
+    if (x) {
+      (void)hipStreamSynchronize(x);
+      (void)hipStreamDestroy(x);
+    }
+  c->split_rx = c->split_coll = nullptr;
+  c->split_cus = 0;
+}
 
 static int hip_err(hipError_t e) { return e == hipSuccess ? 0 : -EIO; }
 
@@ -306,6 +345,7 @@ void pptk_rx_ctx_destroy(struct pptk_rx_ctx *c) {
   if (!c) return;
   DeviceScope dg(c->device);
   comm_release(c);
+  drop_split_streams(c);   // after the communicator that may have used them
   free_staging(c);
   delete c->pool;
   (void)hipFree(c->d_zero);
@@ -936,7 +976,7 @@ static constexpr int kSePerXcc = 4;
 int pptk_rx_stream_split(struct pptk_rx_ctx *c, int coll_cus, void **rx_stream,
                          void **coll_stream) {
   if (!c || coll_cus < 0) return -EINVAL;
-  if (coll_cus == 0) {
+  if (coll_cus == 0) {   // the whole chip for the grids again; the streams stay the context's
     if (rx_stream) *rx_stream = nullptr;
     if (coll_stream) *coll_stream = nullptr;
     c->coll_cus = 0;
@@ -944,6 +984,16 @@ int pptk_rx_stream_split(struct pptk_rx_ctx *c, int coll_cus, void **rx_stream,
   }
   if (!rx_stream || !coll_stream) return -EINVAL;
   *rx_stream = *coll_stream = nullptr;
+  if (c->split_coll && c->split_cus == coll_cus) {   // the pair the context holds
+    *rx_stream = c->split_rx;
+    *coll_stream = c->split_coll;
+    c->coll_cus = coll_cus;
+    return 0;
+  }
+  // A new pair: the communicator's channel cap (ncclConfig_t.maxCTAs, fixed
+  // when it is created) follows the collective stream's CUs, so that stream
+  // cannot change under a communicator -- or a creation in progress.
+  if (ctx_comm_slot(c)->load(std::memory_order_acquire) != nullptr) return -EBUSY;
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   int nxcc = 1;
@@ -959,6 +1009,17 @@ int pptk_rx_stream_split(struct pptk_rx_ctx *c, int coll_cus, void **rx_stream,
     (void)hipStreamDestroy(a);
     return -EIO;
   }
+  drop_split_streams(c);   // a pair of another CU count, no communicator since
+  {
+    std::lock_guard<std::mutex> g(g_split_mu);
+    g_split_owned[a] = c;
+    g_split_owned[b] = c;
+    g_split_retired.erase(a);
+    g_split_retired.erase(b);
+  }
+  c->split_rx = a;
+  c->split_coll = b;
+  c->split_cus = coll_cus;
   *rx_stream = a;
   *coll_stream = b;
   c->coll_cus = coll_cus;
@@ -966,7 +1027,14 @@ int pptk_rx_stream_split(struct pptk_rx_ctx *c, int coll_cus, void **rx_stream,
 }
 
 int pptk_rx_stream_destroy(void *stream) {
-  return stream ? hip_err(hipStreamDestroy((hipStream_t)stream)) : -EINVAL;
+  if (!stream) return -EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  {
+    std::lock_guard<std::mutex> g(g_split_mu);
+    if (g_split_owned.count(s)) return -EBUSY;   // its context destroys it
+    if (g_split_retired.erase(s)) return 0;      // its context already did
+  }
+  return hip_err(hipStreamDestroy(s));
 }
 
 int pptk_rx_variant_count(void) { return RX_NVARIANTS; }
@@ -1206,7 +1274,7 @@ static int retire(RxSlot &sl, WorkerPool *pool) {
   // (HIP spins before it blocks: polling hipEventQuery instead measured
   // equal on 32-frame chunks)
   if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
-  if (sl.out) copy_out(pool, sl.out, sl.h_recs, sl.count * 64);
+  if (sl.out) copy_out(pool, sl.out, sl.h_recs, sl.count * sl.rec_bytes);
   return 0;
 }
 
@@ -1284,8 +1352,8 @@ static int chunk_failed(RxSlot &sl, int rc) {
 // In a registered ring the kernel reads the frames in place over PCIe (or
 // the span goes down by DMA) and only the 10-byte descriptors are written.
 static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp, size_t cnt,
-                         pptk_rx_rec *out, const RxRing *ring, const RxRing *rreg,
-                         WorkerPool *pool) {
+                         void *out, size_t rec_bytes, const RxRing *ring,
+                         const RxRing *rreg, WorkerPool *pool) {
   const uint32_t maxf = c->opts.max_frame ? c->opts.max_frame : 65535u;
   // Descriptors, then the frame bytes.  On one thread (no pool, or a
   // small chunk) both in one pass.  With the pool, both in parallel over
@@ -1415,17 +1483,20 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
   b.max_len = maxlen;
   b.n = cnt;
   // records: into the caller's array itself when it is registered
-  b.d_recs = rreg ? (pptk_rx_rec *)(rreg->dev + ((const uint8_t *)out - rreg->host))
-             : pcie ? sl.hd_recs
-                    : sl.d_recs;
+  void *d_out = rreg ? (void *)(rreg->dev + ((const uint8_t *)out - rreg->host))
+                : pcie ? (void *)sl.hd_recs
+                       : (void *)sl.d_recs;
+  if (rec_bytes == 32) b.d_recs32 = (pptk_rx_rec32 *)d_out;   // compact records
+  else b.d_recs = (pptk_rx_rec *)d_out;
   const int rc = pptk_rx_batch_device(c, &b, s);
   if (rc != 0) return chunk_failed(sl, rc);
   if ((!pcie && !rreg &&
-       hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * 64, hipMemcpyDeviceToHost, s) !=
+       hipMemcpyAsync(sl.h_recs, sl.d_recs, cnt * rec_bytes, hipMemcpyDeviceToHost, s) !=
            hipSuccess) ||
       hipEventRecord(sl.done, s) != hipSuccess)
     return chunk_failed(sl, -EIO);
   sl.out = rreg ? nullptr : out;   // (retire copies only staged records)
+  sl.rec_bytes = rec_bytes;
   sl.count = cnt;
   sl.busy = true;
   return 0;
@@ -1448,19 +1519,20 @@ static size_t chunk_bytes(const pptk_rx_ctx *c) {
 }
 
 static bool host_args_ok(const pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
-                         const struct pptk_rx_rec *recs) {
+                         const void *recs) {
   return c && num >= 0 && (num == 0 || (pkts && recs));
 }
 
-int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
-                  struct pptk_rx_rec *recs) {
+// pptk_rx_batch / pptk_rx_batch32: records of rec_bytes (64 or 32) each.
+static int host_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num, void *recs,
+                      size_t rec_bytes) {
   if (!host_args_ok(c, pkts, num, recs)) return -EINVAL;
   if (num == 0) return 0;
   if (c->async_n) return -EBUSY;   // the submissions own the slots
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   const RxRing *ring = ring_of(c, pkts, num);
-  const RxRing *rreg = records_region(c, recs, (size_t)num * sizeof(pptk_rx_rec));
+  const RxRing *rreg = records_region(c, recs, (size_t)num * rec_bytes);
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
   WorkerPool *pool = pool_of(c);
   int rc = 0;
@@ -1473,7 +1545,8 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
     if ((rc = retire(sl, pool)) != 0) break;
     cnt = std::min(chunk, (size_t)num - first);
     if ((rc = ensure_slot(c, sl, chunk, ring ? 64 : chunk_bytes(c))) != 0) break;
-    rc = enqueue_chunk(c, sl, pkts + first, cnt, recs + first, ring, rreg, pool);
+    rc = enqueue_chunk(c, sl, pkts + first, cnt, (uint8_t *)recs + first * rec_bytes, rec_bytes,
+                       ring, rreg, pool);
   }
   // drain (also on error: nothing may still read the caller's buffers)
   for (RxSlot &sl : c->slot) {
@@ -1483,8 +1556,18 @@ int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
   return rc;
 }
 
-int pptk_rx_batch_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
-                         struct pptk_rx_rec *recs) {
+int pptk_rx_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
+                  struct pptk_rx_rec *recs) {
+  return host_batch(c, pkts, num, recs, sizeof(pptk_rx_rec));
+}
+
+int pptk_rx_batch32(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
+                    struct pptk_rx_rec32 *recs) {
+  return host_batch(c, pkts, num, recs, sizeof(pptk_rx_rec32));
+}
+
+static int host_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num, void *recs,
+                       size_t rec_bytes) {
   if (!host_args_ok(c, pkts, num, recs)) return -EINVAL;
   if (num == 0) return 0;
   if ((size_t)num > std::max<size_t>(c->opts.max_batch, 1)) return -EINVAL;
@@ -1492,15 +1575,26 @@ int pptk_rx_batch_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, i
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   const RxRing *ring = ring_of(c, pkts, num);
-  const RxRing *rreg = records_region(c, recs, (size_t)num * sizeof(pptk_rx_rec));
+  const RxRing *rreg = records_region(c, recs, (size_t)num * rec_bytes);
   // the slots rotate in submission order (FIFO), so consecutive
   // submissions run on different streams and may overlap on the GPU
   RxSlot &sl = c->slot[(c->async_head + c->async_n) % PPTK_RX_MAX_INFLIGHT];
   int rc = ensure_slot(c, sl, std::max<size_t>(c->opts.max_batch, 1), ring ? 64 : chunk_bytes(c));
-  if (rc == 0) rc = enqueue_chunk(c, sl, pkts, (size_t)num, recs, ring, rreg, pool_of(c));
+  if (rc == 0)
+    rc = enqueue_chunk(c, sl, pkts, (size_t)num, recs, rec_bytes, ring, rreg, pool_of(c));
   if (rc != 0) return rc;
   ++c->async_n;
   return 0;
+}
+
+int pptk_rx_batch_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
+                         struct pptk_rx_rec *recs) {
+  return host_submit(c, pkts, num, recs, sizeof(pptk_rx_rec));
+}
+
+int pptk_rx_batch_submit32(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
+                           struct pptk_rx_rec32 *recs) {
+  return host_submit(c, pkts, num, recs, sizeof(pptk_rx_rec32));
 }
 
 int pptk_rx_batch_complete(struct pptk_rx_ctx *c) {

@@ -223,9 +223,19 @@ void teardown(const Rccl *R, RxComm *m, uint32_t timeout_ms) {
   }
 }
 
-ncclConfig_t nonblocking_config() {
+// The communicator's configuration: non-blocking (every wait here is
+// polled under a deadline), and, on a context whose CUs pptk_rx_stream_split
+// divided, at most one RCCL block per CU left to the collective stream
+// (maxCTAs = coll_cus).  RCCL's all-gather kernel takes a whole CU per block
+// on gfx950, so with more channels than those CUs the
+// collective's blocks could not all be resident beside the batches' grid and
+// the gather would run in waves; the cap is a creation-time setting, which is
+// why the split has to come first (pptk_rx_stream_split: -EBUSY once a
+// communicator exists).  Uncapped (RCCL's own channel count) without a split.
+ncclConfig_t comm_config(int coll_cus) {
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
   cfg.blocking = 0;
+  if (coll_cus > 0) cfg.maxCTAs = coll_cus;
 #ifdef PPTK_RX_EXPERIMENTS
   if (getenv("PPTK_RX_COMM_BLOCKING")) cfg.blocking = 1;
 #endif
@@ -289,13 +299,15 @@ uint32_t warmup_stall_ms() {
 }
 
 void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
-              std::vector<int> devs, std::vector<int> ranks, int nranks, uint32_t timeout_ms) {
+              std::vector<int> devs, std::vector<int> ranks, std::vector<int> caps, int nranks,
+              uint32_t timeout_ms) {
   // the helper's own bound (the caller's deadline plus a margin): even if
   // nobody marks the job abandoned, no wait here is unbounded
   const Deadline until(timeout_ms + 1000);
   const size_t k = devs.size();
   std::vector<ncclComm_t> comms(k, nullptr);
-  std::vector<ncclConfig_t> cfg(k, nonblocking_config());
+  std::vector<ncclConfig_t> cfg(k);
+  for (size_t i = 0; i < k; ++i) cfg[i] = comm_config(caps[i]);
   auto going = [](ncclResult_t x) { return x == ncclSuccess || x == ncclInProgress; };
   ncclResult_t r = k > 1 ? R->GroupStart() : ncclSuccess;   // (ncclCommInitAll's form)
   for (size_t i = 0; i < k && going(r); ++i) {
@@ -423,11 +435,12 @@ void init_run(const Rccl *R, std::shared_ptr<InitJob> job, ncclUniqueId id,
 // so that pptk_rx_comm_abort can cancel it: -ECANCELED).  -EAGAIN when too
 // many earlier helpers are still stuck (kMaxAbandoned).
 int bounded_init(const Rccl *R, const std::shared_ptr<InitJob> &job, const ncclUniqueId &id,
-                 const std::vector<int> &devs, const std::vector<int> &ranks, int nranks,
-                 uint32_t timeout_ms, std::vector<ncclComm_t> &comms) {
+                 const std::vector<int> &devs, const std::vector<int> &ranks,
+                 const std::vector<int> &caps, int nranks, uint32_t timeout_ms,
+                 std::vector<ncclComm_t> &comms) {
   if (g_abandoned.load() >= kMaxAbandoned) return -EAGAIN;
   try {
-    std::thread(init_run, R, job, id, devs, ranks, nranks, timeout_ms).detach();
+    std::thread(init_run, R, job, id, devs, ranks, caps, nranks, timeout_ms).detach();
   } catch (...) {
     return -EAGAIN;
   }
@@ -548,6 +561,18 @@ void comm_release(pptk_rx_ctx *c) {
 
 extern "C" {
 
+#ifdef PPTK_RX_TEST_HOOKS
+// The test library's view of the communicator configuration a context with
+// `coll_cus` split CUs creates (tests/test_capi.py, no GPU needed).
+int pptk_rx_test_comm_config(int coll_cus, int *blocking, int *min_ctas, int *max_ctas) {
+  const ncclConfig_t cfg = comm_config(coll_cus);
+  if (blocking) *blocking = cfg.blocking;
+  if (min_ctas) *min_ctas = cfg.minCTAs;
+  if (max_ctas) *max_ctas = cfg.maxCTAs;
+  return 0;
+}
+#endif
+
 int pptk_rx_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return -EIO;
@@ -585,7 +610,8 @@ int pptk_rx_comm_create(struct pptk_rx_ctx *c, int nranks, int rank,
   memcpy(&id, uid, sizeof(id));
   COMM_TRACE("create: init rank %d of %d", rank, nranks);
   std::vector<ncclComm_t> comms;
-  rc = bounded_init(R, job, id, {ctx_device(c)}, {rank}, nranks, ctx_comm_timeout_ms(c), comms);
+  rc = bounded_init(R, job, id, {ctx_device(c)}, {rank}, {ctx_coll_cap(c)}, nranks,
+                    ctx_comm_timeout_ms(c), comms);
   COMM_TRACE("create: %d", rc);
   return end_create(R, &c, 1, ms, comms, rc);
 }
@@ -617,10 +643,13 @@ int pptk_rx_comm_create_all(struct pptk_rx_ctx *const *ctxs, int n) {
     ms[(size_t)i]->rank = i;
   }
   // one group of per-device inits (what ncclCommInitAll does), bounded
-  std::vector<int> ranks((size_t)n);
-  for (int i = 0; i < n; ++i) ranks[(size_t)i] = i;
+  std::vector<int> ranks((size_t)n), caps((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    ranks[(size_t)i] = i;
+    caps[(size_t)i] = ctx_coll_cap(ctxs[i]);
+  }
   std::vector<ncclComm_t> comms;
-  rc = bounded_init(R, job, id, devs, ranks, n, ctx_comm_timeout_ms(ctxs[0]), comms);
+  rc = bounded_init(R, job, id, devs, ranks, caps, n, ctx_comm_timeout_ms(ctxs[0]), comms);
   return end_create(R, ctxs, n, ms, comms, rc);
 }
 

@@ -32,6 +32,9 @@ struct DeviceScope {
 int ctx_device(const pptk_rx_ctx *c);
 std::atomic<void *> *ctx_comm_slot(pptk_rx_ctx *c);
 uint32_t ctx_comm_timeout_ms(const pptk_rx_ctx *c);   // opts.comm_timeout_ms (0 -> default)
+// CUs of the collective stream pptk_rx_stream_split left the context (0: no
+// split): the channel cap (ncclConfig_t.maxCTAs) of a communicator created on it
+int ctx_coll_cap(const pptk_rx_ctx *c);
 void comm_release(pptk_rx_ctx *c);   // destroys the context's communicator, if any
 
 // Diagnostic tune bits (RxKArgs::tune 3, 4, 7, 9: skip record stores, the

@@ -484,8 +484,9 @@ struct PermitFused {
   uint32_t *need;    // hash_size
   uint32_t *code;    // ceil(hash_size / 2) words of u16 pairs
   uint32_t *ntok;    // hash_size: the new token counts, until the commit
-  uint64_t *arrive;  // FMAXBLK: workgroup c's barrier generation (nonce + k, or nonce | 4: abort)
-  uint64_t *out;     // [1] = nonce | 1: the launch aborted (status; [0] unused)
+  uint64_t *arrive;  // FMAXBLK: workgroup c's barrier generation (nonce + k, + 1: its flag)
+  uint64_t *out;     // [0] decision (nonce | 2 committed, nonce | 4 aborted: fused_decide);
+                     // [1] = nonce | 1: the launch aborted (status)
   uint32_t *stamps;  // FSTAMPS x FMAXBLK phase timestamps (tools/permit_run.py)
   uint64_t nonce;    // this launch's, low three bits clear (never 0)
   uint64_t spin_ticks;   // a barrier's bound (100 MHz ticks)
@@ -509,6 +510,26 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The launch's decision word f.out[0]: nonce | 2 once barrier 2 (the commit
+// point) has passed, nonce | 4 once the launch aborted; any other value (a
+// word an earlier launch left) is undecided.  Set once per launch by compare-
+// and-swap, so every workgroup acts on the same outcome: a workgroup that
+// saw every arrival at barrier 2 and one whose wait ran out cannot both win.
+// Returns the decided value (ours, or the one another workgroup set first).
+// (Each failed swap means another workgroup wrote this launch's decision, so
+// the loop ends after at most one retry.)
+__device__ __forceinline__ uint64_t fused_decide(uint64_t *out, uint64_t nonce, uint64_t what) {
+  uint64_t x = ld_sc1(out);
+  for (;;) {
+    if ((x & ~7ull) == nonce) return x;
+    uint64_t seen = x;
+    if (__hip_atomic_compare_exchange_strong(out, &seen, nonce | what, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return nonce | what;
+    x = seen;
+  }
+}
+
 // Grid barrier k (1, 2) of the launch with nonce N: every wave's stores
 // complete, workgroup c publishes N + k (+ 1 with `flag`, at k = 2) in
 // arrive[c], and wave 0 polls all nblk words (sc1, bounded) until each holds
@@ -518,11 +539,15 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
 // flag -- phase 2's "a bucket ran out", carried by the arrival words rather
 // than by one word every workgroup would store to (write-through stores to
 // one address are served one after another: 10 us for 256 of them) -- else
-// 0; or -1: the launch aborted.  A workgroup whose wait exceeds
-// f.spin_ticks, or that sees another's abort word (N | 4), publishes its own
-// abort word and the status, and its caller returns at once: once any
-// workgroup has given up, every barrier still waiting ends in an abort, and
-// a workgroup that arrives later (it was not resident) sees the abort words.
+// 0; or -1: the launch aborted.
+// Outcome through the decision word (fused_decide): a workgroup whose wait
+// exceeds f.spin_ticks proposes "aborted"; at barrier 2 a workgroup that saw
+// every arrival proposes "passed".  Whichever came first holds for all: a
+// workgroup that saw "aborted" returns -1 (the status word set), one whose
+// own wait ran out after the commit was decided keeps polling (every arrival
+// is there) and commits with the others.  Barrier 1 never decides "passed"
+// (nothing is committed there), so an abort at barrier 1 always wins, and a
+// workgroup that was not resident yet sees it when it arrives.
 __device__ __forceinline__ int fused_barrier(const PermitFused &f, uint32_t c, uint64_t k,
                                              bool flag = false) {
   __shared__ int res;
@@ -531,31 +556,47 @@ __device__ __forceinline__ int fused_barrier(const PermitFused &f, uint32_t c, u
   if (threadIdx.x < 64) {
     if (threadIdx.x == 0) st_sc1(f.arrive + c, f.nonce + k + (flag ? 1u : 0u));
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool passed = false;   // barrier 2's commit decided (by any workgroup)
+    int r = 0;
     for (;;) {
-      bool ok = true, fl = false, ab = false;
+      const uint64_t d = ld_sc1(f.out);
+      const bool ours = (d & ~7ull) == f.nonce;
+      if (ours && (d & 4ull)) {
+        r = -1;
+        break;
+      }
+      passed = passed || (ours && (d & 2ull));
+      bool ok = true, fl = false;
       for (uint32_t i = threadIdx.x; i < f.nblk; i += 64) {
         const uint64_t x = ld_sc1(f.arrive + i);
-        const bool ours = (x & ~7ull) == f.nonce;
-        ok = ok && ours && (x & 3ull) >= k;
-        fl = fl || (ours && (x & 3ull) == 3ull);
-        ab = ab || (ours && (x & 4ull) != 0);
+        const bool mine = (x & ~7ull) == f.nonce;
+        ok = ok && mine && (x & 3ull) >= k;
+        fl = fl || (mine && (x & 3ull) == 3ull);
       }
-      const bool give_up = __any(ab) || __builtin_amdgcn_s_memrealtime() - t0 > f.spin_ticks;
-      if (!give_up && __all(ok)) {
-        if (threadIdx.x == 0) res = 0;
-        __builtin_amdgcn_wave_barrier();
-        if (__any(fl) && threadIdx.x == 0) res = 1;
-        break;
-      }
-      if (give_up) {
-        if (threadIdx.x == 0) {
-          st_sc1(f.arrive + c, f.nonce | 4u);
-          st_sc1(f.out + 1, f.nonce | 1u);
-          res = -1;
+      if (__all(ok)) {
+        uint64_t dec = f.nonce | 2u;
+        if (k == 2 && !passed) {
+          if (threadIdx.x == 0) dec = fused_decide(f.out, f.nonce, 2u);
+          dec = __shfl(dec, 0);
         }
+        r = (dec & 4ull) ? -1 : (__any(fl) ? 1 : 0);
         break;
+      }
+      if (!passed && __builtin_amdgcn_s_memrealtime() - t0 > f.spin_ticks) {
+        uint64_t dec = 0;
+        if (threadIdx.x == 0) dec = fused_decide(f.out, f.nonce, 4u);
+        dec = __shfl(dec, 0);
+        if (dec & 4ull) {
+          r = -1;
+          break;
+        }
+        passed = true;   // the commit won: wait for the arrivals it saw
       }
       __builtin_amdgcn_s_sleep(1);
+    }
+    if (threadIdx.x == 0) {
+      if (r < 0) st_sc1(f.out + 1, f.nonce | 1u);
+      res = r;
     }
   }
   __syncthreads();
@@ -795,12 +836,27 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
       put_word(rel, spec_word(v));
     }
   };
+  // An aborted launch fails closed: every subject frame of the segment is
+  // denied (0), the others stay "not a subject" (2) -- no frame is admitted
+  // without a token, as the reference's ip_permitted never does
+  // (iphash/iphash.c:164-196) -- while the tokens stay as they were.
+  auto put_fail = [&]() {
+#pragma unroll
+    for (int v = 0; v < FKV; ++v) {
+      const uint32_t rel = (uint32_t)v * FT * 4 + 4 * tid;
+      if (rel >= nrel) break;
+      put_word(rel, spec_word(v) & 0x02020202u);
+    }
+  };
   FSTAMP(2);
 #ifdef PPTK_PERMIT_SPEC_EARLY   // (A/B: the speculative verdicts before the table loads)
   put_spec();
 #endif
   fused_stall(f, c, 1);
-  if (fused_barrier(f, c, 1) < 0) return;   // aborted: nothing written but scratch
+  if (fused_barrier(f, c, 1) < 0) {   // aborted: no token touched, subjects denied
+    put_fail();
+    return;
+  }
   FSTAMP(3);
 
   // ---- phase 2: per bucket down its column ---------------------------------
@@ -965,7 +1021,10 @@ __global__ __launch_bounds__(FT) void permit_fused(PermitArgs a, PermitFused f) 
   __syncthreads();
   fused_stall(f, c, 2);
   const int b2 = fused_barrier(f, c, 2, out_l != 0);
-  if (b2 < 0) return;   // aborted: the tokens stay as they were
+  if (b2 < 0) {   // aborted: the tokens stay as they were, subjects denied
+    put_fail();
+    return;
+  }
   FSTAMP(5);
   // every workgroup is past phase 2: commit this one's token counts
   if (tid < 64) {
@@ -1631,11 +1690,35 @@ uint64_t nonce_of(uint64_t k) { return nonce_base() + 8 * k; }
 std::mutex g_status_mu;
 std::unordered_map<const void *, std::pair<uint64_t, uint64_t>> g_status;   // first, last k
 
+// At most this many scratch buffers are tracked: a caller that never queries
+// the status (or allocates a fresh scratch per call) does not grow the map
+// without bound; the entry whose last launch is oldest goes first (a later
+// status query on it reports 0).
+constexpr size_t kMaxStatus = 1024;
+
+void note_launch(const void *scratch, uint64_t k) {
+  std::lock_guard<std::mutex> sl(g_status_mu);
+  auto it = g_status.find(scratch);
+  if (it != g_status.end()) {
+    it->second.second = k;
+    return;
+  }
+  if (g_status.size() >= kMaxStatus) {
+    auto old = g_status.begin();
+    for (auto j = g_status.begin(); j != g_status.end(); ++j)
+      if (j->second.second < old->second.second) old = j;
+    g_status.erase(old);
+  }
+  g_status.emplace(scratch, std::make_pair(k, k));
+}
+
 // The previous fused launch of each device, which the next one on another
 // stream waits for: two fused grids running at once could split the CUs
 // between them and each wait at its barrier for workgroups that cannot
 // become resident.  An event per device, the stop event of
-// every fused launch once the device has seen them from two streams.
+// every fused launch (hipExtLaunchKernelGGL's own, 2.2 us per call), so a
+// launch from a new stream only waits for that event -- never for the whole
+// device, which would also wait for other streams' gathers and batches.
 // (A/B builds: PPTK_PERMIT_ORDER=0, no order)
 #ifndef PPTK_PERMIT_ORDER
 #define PPTK_PERMIT_ORDER 1
@@ -1644,8 +1727,7 @@ struct FusedOrder {
   std::mutex mu;
   hipEvent_t ev = nullptr;
   hipStream_t last = nullptr;
-  bool any = false;     // a fused launch was made on this device
-  bool multi = false;   // ... from more than one stream: launches record ev
+  bool any = false;     // a fused launch was made on this device (ev records its end)
 };
 FusedOrder g_order[64];
 
@@ -1726,26 +1808,13 @@ hipError_t launch_permit(const PermitArgs &a, void *scratch, hipStream_t st) {
                                                     hipEventDisableSystemFence) != hipSuccess &&
         (e = hipEventCreateWithFlags(&o.ev, hipEventDisableTiming)) != hipSuccess)
       return e;
-    if (PPTK_PERMIT_ORDER && o.any && o.last != st) {
-      // The first time a second stream shows up, the launches so far carry
-      // no event (a process that issues every call on one stream never pays
-      // for one): wait for the device once, then order by event from here on.
-      if (!o.multi) {
-        if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
-        o.multi = true;
-      } else if ((e = hipStreamWaitEvent(st, o.ev, 0)) != hipSuccess) {
-        return e;
-      }
-    }
+    if (PPTK_PERMIT_ORDER && o.any && o.last != st &&
+        (e = hipStreamWaitEvent(st, o.ev, 0)) != hipSuccess)
+      return e;
     const uint64_t k = g_nonce_ctr.fetch_add(1);
     f.nonce = nonce_of(k);
-    {
-      std::lock_guard<std::mutex> sl(g_status_mu);
-      auto it = g_status.find(scratch);
-      if (it == g_status.end()) g_status.emplace(scratch, std::make_pair(k, k));
-      else it->second.second = k;
-    }
-    if (PPTK_PERMIT_ORDER && o.multi) {
+    note_launch(scratch, k);
+    if (PPTK_PERMIT_ORDER) {
       // the order event as the launch's own stop event (2.2 us per call;
       // a separate hipEventRecord behind the kernel cost 3.6)
       hipExtLaunchKernelGGL(permit_fused<true>, dim3(g.nblk), dim3(FT), 0, st, nullptr, o.ev, 0,

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-from .records import REC_DTYPE
+from .records import REC32_DTYPE, REC_DTYPE
 
 LIB_PATH = os.environ.get("PPTK_RX_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "libpptkrx.so")   # env: A/B builds
@@ -170,7 +170,8 @@ assert ctypes.sizeof(LdpPacket) == 24
 assert ctypes.sizeof(RxOpts) == 40
 
 EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
-           "pptk_rx_batch", "pptk_rx_batch_submit", "pptk_rx_batch_complete",
+           "pptk_rx_batch", "pptk_rx_batch32", "pptk_rx_batch_submit", "pptk_rx_batch_submit32",
+           "pptk_rx_batch_complete",
            "pptk_rx_batch_pending", "pptk_rx_batch_device", "pptk_rx_bin_scratch_bytes",
            "pptk_rx_bin_device", "pptk_rx_batch_device_mixed", "pptk_rx_version", "pptk_rx_set_tuning",
            "pptk_rx_variant_count", "pptk_rx_last_variant", "pptk_rx_register_ring", "pptk_rx_unregister_ring",
@@ -216,6 +217,10 @@ def lib(path=None):
         L.pptk_rx_ctx_destroy.restype = None
         L.pptk_rx_batch.argtypes = [vp, vp, ctypes.c_int, vp]
         L.pptk_rx_batch.restype = ctypes.c_int
+        if hasattr(L, "pptk_rx_batch32"):   # (absent from older A/B builds)
+            for f in ("pptk_rx_batch32", "pptk_rx_batch_submit32"):
+                getattr(L, f).argtypes = [vp, vp, ctypes.c_int, vp]
+                getattr(L, f).restype = ctypes.c_int
         L.pptk_rx_batch_device.argtypes = [vp, ctypes.POINTER(RxDevBatch), vp]
         L.pptk_rx_batch_device.restype = ctypes.c_int
         L.pptk_rx_bin_scratch_bytes.argtypes = [ctypes.c_uint64]
@@ -714,8 +719,9 @@ class RxContext:
         """pptk_rx_stream_split: (rx stream, collective stream) as torch
         streams on this context's device, the collective's holding coll_cus
         CUs (a multiple of 32 on an MI355X) and the batches' the rest; the
-        context sizes its grids for the rest until stream_join().  The HIP
-        streams live until the process exits (see stream_join)."""
+        context sizes its grids for the rest until stream_join().  Call it
+        before creating the communicator (its channel cap follows coll_cus).
+        The HIP streams belong to the context and are destroyed with it."""
         import torch
         a, b = ctypes.c_void_p(), ctypes.c_void_p()
         rc = self._L.pptk_rx_stream_split(self._ctx, coll_cus, ctypes.byref(a), ctypes.byref(b))
@@ -726,12 +732,8 @@ class RxContext:
                 torch.cuda.ExternalStream(b.value, device=dev))
 
     def stream_join(self):
-        """Undo stream_split: the whole chip for this context's grids again.
-        The split's HIP streams are not destroyed here: torch events recorded
-        on them may outlive this call, and a gather stream must outlive the
-        communicator (destroyed first, later device-wide waits or the
-        teardown hung now and then: DESIGN.md section 8), so they live until
-        the process exits."""
+        """Undo stream_split: the whole chip for this context's grids again
+        (the split's streams stay the context's until close())."""
         if not hasattr(self._L, "pptk_rx_stream_split"):
             return
         self._L.pptk_rx_stream_split(self._ctx, 0, None, None)
@@ -760,32 +762,36 @@ class RxContext:
         if rc != 0:
             raise OSError(-rc, "pptk_rx_unregister_ring failed")
 
-    def batch_host(self, pkts, out=None):
-        """pptk_rx_batch over a ctypes array of LdpPacket; returns records
-        (into `out`, a REC_DTYPE array of len(pkts), when given: an rx loop
-        reuses its record array, so its pages are not faulted in per call)."""
+    def batch_host(self, pkts, out=None, compact=False):
+        """pptk_rx_batch (compact: pptk_rx_batch32, 32-byte records) over a
+        ctypes array of LdpPacket; returns records (into `out`, a REC_DTYPE /
+        REC32_DTYPE array of len(pkts), when given: an rx loop reuses its
+        record array, so its pages are not faulted in per call)."""
         n = len(pkts)
+        dt = REC32_DTYPE if compact else REC_DTYPE
         if out is not None:
-            assert out.dtype == REC_DTYPE and out.shape == (n,) and out.flags["C_CONTIGUOUS"]
+            assert out.dtype == dt and out.shape == (n,) and out.flags["C_CONTIGUOUS"]
             recs = out
         else:
-            recs = np.zeros(n, dtype=REC_DTYPE)
-        rc = self._L.pptk_rx_batch(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n,
-                                 ctypes.c_void_p(recs.ctypes.data))
+            recs = np.zeros(n, dtype=dt)
+        fn = self._L.pptk_rx_batch32 if compact else self._L.pptk_rx_batch
+        rc = fn(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n, ctypes.c_void_p(recs.ctypes.data))
         if rc != 0:
-            raise OSError(-rc, f"pptk_rx_batch failed ({rc})")
+            raise OSError(-rc, f"pptk_rx_batch{'32' if compact else ''} failed ({rc})")
         return recs
 
     def submit_host(self, pkts, out):
-        """pptk_rx_batch_submit: enqueue one batch (len(pkts) <= max_batch);
-        `pkts`, the frames they point at and `out` (a REC_DTYPE array of
-        len(pkts)) must stay alive and untouched until complete_host() has
-        returned this batch.  Raises OSError(EBUSY) with
-        PPTK_RX_MAX_INFLIGHT batches outstanding."""
+        """pptk_rx_batch_submit (pptk_rx_batch_submit32 when `out` is a
+        REC32_DTYPE array): enqueue one batch (len(pkts) <= max_batch);
+        `pkts`, the frames they point at and `out` (len(pkts) records) must
+        stay alive and untouched until complete_host() has returned this
+        batch.  Raises OSError(EBUSY) with PPTK_RX_MAX_INFLIGHT batches
+        outstanding."""
         n = len(pkts)
-        assert out.dtype == REC_DTYPE and out.shape == (n,) and out.flags["C_CONTIGUOUS"]
-        rc = self._L.pptk_rx_batch_submit(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n,
-                                          ctypes.c_void_p(out.ctypes.data))
+        compact = out.dtype == REC32_DTYPE
+        assert (compact or out.dtype == REC_DTYPE) and out.shape == (n,) and out.flags["C_CONTIGUOUS"]
+        fn = self._L.pptk_rx_batch_submit32 if compact else self._L.pptk_rx_batch_submit
+        rc = fn(self._ctx, ctypes.cast(pkts, ctypes.c_void_p), n, ctypes.c_void_p(out.ctypes.data))
         if rc != 0:
             raise OSError(-rc, f"pptk_rx_batch_submit failed ({rc})")
         # the library holds pointers into both until the batch completes:

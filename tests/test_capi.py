@@ -616,3 +616,24 @@ def test_ctypes_structs_match_the_header(tmp_path):
         assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
         for fname, _ in py._fields_:
             assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
+
+
+def test_comm_config_caps_channels_only_when_split():
+    """The communicator configuration the library builds (rx_comm.hip
+    comm_config, through the test library's hook; no GPU): non-blocking
+    always; ncclConfig_t.maxCTAs = the CUs pptk_rx_stream_split left the
+    collective when the context is split, RCCL's default (unset) when not.
+    bench.py sets no NCCL_* variable for this any more."""
+    from conftest import HOOKS_LIB
+    L = ctypes.CDLL(HOOKS_LIB)
+    f = L.pptk_rx_test_comm_config
+    f.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_int)] * 3
+    undef = -(1 << 31)                                  # NCCL_CONFIG_UNDEF_INT
+    for cus, want_max in ((0, undef), (32, 32), (64, 64), (128, 128)):
+        b, mn, mx = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        assert f(cus, ctypes.byref(b), ctypes.byref(mn), ctypes.byref(mx)) == 0
+        assert (b.value, mn.value, mx.value) == (0, undef, want_max), cus
+    assert "NCCL_MAX_NCHANNELS" not in open(os.path.join(ROOT, "bench.py")).read()
+    # the product library has no such hook
+    assert not hasattr(ctypes.CDLL(os.path.join(ROOT, "pptk_amd", "libpptkrx.so")),
+                       "pptk_rx_test_comm_config")

@@ -107,16 +107,22 @@ def test_rx_multigpu_allgather_bit_exact(tmp_path):
 
 @pytest.mark.gpu
 def test_rx_multigpu_split_overlap_bit_exact(tmp_path):
-    """RX_MULTIGPU_SPLIT=32: the gathers on their own stream beside the next
-    batch, the chip's CUs split between the two (pptk_rx_stream_split),
-    batch r waiting for gather r - 2; four rounds, bit-exact as above."""
+    """split_cus 32 (4th argument; no environment knob, no RCCL variable):
+    the gathers on their own stream beside the next batch, the chip's CUs
+    split between the two (pptk_rx_stream_split, made before the
+    communicator, which the library then caps at 32 channels), batch r
+    waiting for gather r - 2; four rounds, bit-exact as above.  The streams
+    are the context's: the example's pptk_rx_stream_destroy of the gather
+    stream before pptk_rx_ctx_destroy -- the order that hung in round 5 --
+    returns EBUSY, and the context's own teardown (communicator first, then
+    its streams) ends the process cleanly."""
     p = str(tmp_path / "s.rxq")
     n = write_rxq(p)
-    env = dict(os.environ, RX_MULTIGPU_SPLIT="32", RX_MULTIGPU_TRACE="1",
-               RX_MULTIGPU_TIMEOUT_MS="20000")
+    env = dict(os.environ, RX_MULTIGPU_TRACE="1", RX_MULTIGPU_TIMEOUT_MS="20000")
+    env.pop("NCCL_MAX_NCHANNELS", None)
     exe = build(tmp_path, "rx_multigpu", hip=True)
     with open(tmp_path / "out", "w+") as fo, open(tmp_path / "err", "w+") as fe:
-        pr = subprocess.Popen([exe, p, "1", "4"], stdout=fo, stderr=fe, env=env)
+        pr = subprocess.Popen([exe, p, "1", "4", "32"], stdout=fo, stderr=fe, env=env)
         try:
             rc = pr.wait(timeout=90)
         except subprocess.TimeoutExpired:
@@ -128,6 +134,7 @@ def test_rx_multigpu_split_overlap_bit_exact(tmp_path):
         out, err = fo.read(), fe.read()
     assert rc == 0, (rc, out, err)
     assert f"{n} frames, 0 mismatches" in out
+    assert "before the context: -16 (EBUSY" in out, out
 
 
 @pytest.mark.gpu

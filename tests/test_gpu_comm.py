@@ -466,3 +466,101 @@ def test_gather_alloc_n_rank_slice_probe(dev):
         assert np.array_equal(got[2 * per:2 * per + n], want), k
         assert (got[:2 * per] == 0).all() and (got[2 * per + n:] == 0).all()
     ctx.close()
+
+
+def _channels_logged(split_cus):
+    """Child process: one-rank communicator on a context split (or not) with
+    RCCL's INFO log on; the largest channel count its "Channel xx/NN" lines
+    name (None if it names none)."""
+    import os
+    import re
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from pptk_amd.rx import RxContext, comm_uid\n"
+        "ctx = RxContext(0, bytes(range(1, 17)))\n"
+        "if %d: ctx.stream_split(%d)\n"
+        "ctx.comm_create(1, 0, comm_uid())\n"
+        "ctx.close()\n"
+        "print('child ok')\n") % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                  split_cus, split_cus)
+    env = dict(os.environ, NCCL_DEBUG="INFO")
+    env.pop("NCCL_MAX_NCHANNELS", None)
+    env.pop("NCCL_MAX_CTAS", None)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=120, env=env)
+    assert out.returncode == 0 and "child ok" in out.stdout, out.stderr[-2000:]
+    counts = [int(m.group(1)) for m in re.finditer(r"Channel \d+/(\d+)", out.stdout + out.stderr)]
+    return max(counts) if counts else None
+
+
+def test_split_streams_owned_by_context_and_channel_cap(dev):
+    """pptk_rx_stream_split before the communicator: the context owns the two
+    streams (a second split to the same count returns them; a split to
+    another count once a communicator exists is EBUSY), the gather runs on
+    the collective stream beside the batches' stream bit-exact,
+    pptk_rx_stream_destroy of either stream before the context is EBUSY --
+    the 'wrong' destroy order that hung in round 5 is refused, not queued --
+    and the context's teardown (communicator, then its streams) returns
+    promptly; afterwards the destroy of the retired handle is a no-op 0."""
+    import time
+    from pptk_amd.rx import comm_uid
+    z = load_golden("cmix")
+    ctx = _ctx(z)
+    L = ctx._L
+    rx, coll = ctx.stream_split(32)
+    rx2, coll2 = ctx.stream_split(32)
+    assert (rx2.cuda_stream, coll2.cuda_stream) == (rx.cuda_stream, coll.cuda_stream)
+    ctx.comm_create(1, 0, comm_uid())
+    with pytest.raises(OSError) as e:                   # the cap is fixed now
+        ctx.stream_split(64)
+    assert e.value.errno == 16
+    ctx.stream_join()                                   # grids on the whole chip: allowed
+    rx3, coll3 = ctx.stream_split(32)                   # the same pair again
+    assert coll3.cuda_stream == coll.cuda_stream
+    from pptk_amd.shard import GatherBuffer
+    n = len(z["off"])
+    gb = GatherBuffer(n, 1, 0, dev)
+    frames = torch.from_numpy(z["buf"]).to(dev)
+    off = torch.from_numpy(z["off"].view(np.int64)).to(dev)
+    lens = torch.from_numpy(z["len"].view(np.int16)).to(dev)
+    torch.cuda.synchronize()
+    ctx.batch_device(frames, n, off=off, lens=lens, max_len=int(z["len"].max()),
+                     hash_out=gb.local[:n], stream=rx)
+    ev = torch.cuda.Event()
+    ev.record(rx)
+    coll.wait_event(ev)
+    ctx.allgather_hash(gb.local, gb.per, gb.out, stream=coll)
+    assert ctx.comm_sync(coll) == 0
+    got = gb.out.cpu().numpy().view(np.uint64)[:n]
+    assert np.array_equal(got, as_records(z["recs"])["flow_hash"])
+    for s in (coll, rx):                                # the context's: refused
+        assert L.pptk_rx_stream_destroy(ctypes.c_void_p(s.cuda_stream)) == -16
+    handles = (coll.cuda_stream, rx.cuda_stream)
+    t0 = time.monotonic()
+    ctx.close()                                         # communicator, then the streams
+    assert time.monotonic() - t0 < 30
+    for h in handles:                                   # destroyed by the context
+        assert L.pptk_rx_stream_destroy(ctypes.c_void_p(h)) == 0
+    # without a communicator a split may change its CU count (new pair)
+    c2 = _ctx(z)
+    c2.stream_split(32)
+    _, b = c2.stream_split(64)
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ctypes.c_uint32 * (ncu // 32))()
+    assert hip.hipExtStreamGetCUMask(ctypes.c_void_p(b.cuda_stream), len(words), words) == 0
+    assert sum(bin(w).count("1") for w in words) == 64
+    c2.close()
+
+
+def test_split_caps_rccl_channels(dev):
+    """RCCL's own log of a communicator created on a split context names no
+    channel count above the 32 CUs left to the collective (maxCTAs).  The
+    unsplit count is printed beside it for the record."""
+    capped = _channels_logged(32)
+    free = _channels_logged(0)
+    print(f"RCCL channels: split 32 -> {capped}, unsplit -> {free}")
+    if capped is not None:
+        assert capped <= 32

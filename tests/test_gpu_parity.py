@@ -1201,3 +1201,55 @@ def test_dense_hash_misaligned_and_ragged(name, stride, compact, dev):
         assert np.array_equal(got[1:n + 1].view(np.uint64), want), VARIANTS[ctx.last_variant()]
         assert got[0] == -7 and (got[n + 1:] == -7).all()
     ctx.close()
+
+
+@pytest.mark.parametrize("max_batch,threads", [(97, 1), (4096, 4), (65536, 8)])
+@pytest.mark.parametrize("mode", ["staged", "ring", "ring_recs"])
+@pytest.mark.parametrize("name", ["edge", "fuzz", "cmix", "c64", "c1500"])
+def test_host_batch_compact_records(name, mode, max_batch, threads, dev):
+    """pptk_rx_batch32 (compact 32-byte records host to host): staged frames,
+    frames in a registered ring, and records written in place into a
+    registered array; small chunks (direct: the kernel reads the pinned
+    staging and writes pinned records) and large ones (DMA both ways); every
+    record equals to_rec32 of the reference-made golden record, and the bytes
+    around an in-place array are untouched.  Then the pipelined form
+    (pptk_rx_batch_submit32) interleaved with 64-byte submissions in one
+    queue: each completes into its own record size."""
+    from pptk_amd.records import REC32_DTYPE, REC_DTYPE, to_rec32
+    from pptk_amd.rx import RxContext, ldp_packets
+    z = load_golden(name)
+    n = len(z["off"])
+    b4, b6, hs = (int(x) for x in z["iphash"])
+    ctx = RxContext(0, z["key"].tobytes(), b4, b6, hs, max_batch=max_batch, max_frame=65535,
+                    gather_threads=threads)
+    ring = _pages(z["buf"].size + 4096)
+    ring[:z["buf"].size] = z["buf"]
+    pkts = ldp_packets(ring, z["off"], z["len"])
+    want32 = to_rec32(z["recs"])
+    region = _pages((n + 16) * 32)
+    region[:] = 0x5A
+    out = region[8 * 32:(8 + n) * 32].view(REC32_DTYPE)
+    if mode != "staged":
+        ctx.register_ring(ring)
+    if mode == "ring_recs":
+        ctx.register_ring(region)
+    for _ in range(2):
+        out[:] = np.zeros(1, dtype=REC32_DTYPE)
+        got = ctx.batch_host(pkts, out=out, compact=True)
+        d = diff_records(got, want32, dtype=REC32_DTYPE)
+        assert not d, d
+        assert (region[:8 * 32] == 0x5A).all() and (region[(8 + n) * 32:] == 0x5A).all()
+    k = min(n, max_batch, 500)
+    o32 = [np.zeros(k, REC32_DTYPE) for _ in range(2)]
+    o64 = [np.zeros(k, REC_DTYPE) for _ in range(2)]
+    for j in range(2):
+        ctx.submit_host(_packet_slice(pkts, 0, k), o32[j])
+        ctx.submit_host(_packet_slice(pkts, 0, k), o64[j])
+    for _ in range(4):
+        assert ctx.complete_host() == k
+    for j in range(2):
+        d = diff_records(o32[j], want32[:k], dtype=REC32_DTYPE)
+        assert not d, d
+        d = diff_records(o64[j], z["recs"][:k])
+        assert not d, d
+    ctx.close()

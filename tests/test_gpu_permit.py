@@ -438,8 +438,10 @@ def test_permit_fused_abort_leaves_tokens_and_reports(dev, monkeypatch, stall_at
     """Fault injection (the test build of the library, PPTK_RX_TEST_HOOKS):
     one workgroup of the fused launch is held 600 ms before grid barrier
     `stall_at` while the others' barrier gives up after 200 ms.  The launch
-    aborts: pptk_rx_permit_status reports -ETIMEDOUT and the token array is
-    exactly as before the call (the commit comes after the last barrier).
+    aborts: pptk_rx_permit_status reports -ETIMEDOUT, the token array is
+    exactly as before the call (the commit comes after the last barrier) and
+    the launch fails closed (every subject frame's verdict 0, the reference's
+    iphash/iphash.c:164-196 never admits without a token).
     The same call repeated without the stall gives the frame-by-frame
     verdicts and tokens, and status 0."""
     from conftest import HOOKS_LIB
@@ -457,9 +459,11 @@ def test_permit_fused_abort_leaves_tokens_and_reports(dev, monkeypatch, stall_at
     monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_MS", "600")
     monkeypatch.setenv("PPTK_RX_TEST_PERMIT_SPIN_MS", "200")
     monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_AT", str(stall_at))
-    ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
+    v = ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
     assert ctx.permit_status(scratch) == -ETIMEDOUT
     assert np.array_equal(tok.cpu().numpy().view(np.uint32), tok_h)
+    # fails closed: every subject frame denied, the others "not a subject"
+    assert np.array_equal(v.cpu().numpy(), np.where(k >= 0, 0, 2).astype(np.uint8))
     for name in ("PPTK_RX_TEST_PERMIT_STALL_MS", "PPTK_RX_TEST_PERMIT_SPIN_MS",
                  "PPTK_RX_TEST_PERMIT_STALL_AT"):
         monkeypatch.delenv(name)
@@ -468,4 +472,55 @@ def test_permit_fused_abort_leaves_tokens_and_reports(dev, monkeypatch, stall_at
     assert ctx.permit_status(scratch) == 0
     assert np.array_equal(v.cpu().numpy(), v_want)
     assert np.array_equal(tok.cpu().numpy().view(np.uint32), t_want)
+    ctx.close()
+
+
+@pytest.mark.parametrize("spin_ms", [20, 21])
+def test_permit_fused_commit_decision_is_agreed(dev, monkeypatch, spin_ms):
+    """the last workgroup is held before barrier 2 (the commit
+    point) for as long as the others wait there (20 ms against 20 / 21 ms),
+    so its arrival lands right around their deadline, on both sides of it
+    over the repeats.  Whatever each launch decides, all workgroups act on
+    the one decision word: either status 0 with the frame-by-frame verdicts
+    and tokens (chained through the launches), or -ETIMEDOUT with the tokens
+    exactly as before that launch and every subject denied -- never some
+    buckets committed and others not."""
+    from conftest import HOOKS_LIB
+    from pptk_amd.rx import RxContext
+    if _PATH[0] == "passes":
+        pytest.skip("the four-launch path has no grid barrier")
+    n, hs = 1 << 20, 1 << 16
+    k, tok_h, keys_h = _keys_case(n, hs, 98)
+    ctx = RxContext(0, bytes(range(1, 17)), 24, 48, hs, lib_path=HOOKS_LIB)
+    keys = torch.from_numpy(keys_h.view(np.int32)).to(dev)
+    tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
+    scratch = torch.empty(ctx._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8,
+                          device=dev)
+    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_MS", "20")
+    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_SPIN_MS", str(spin_ms))
+    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_AT", "2")
+    t_cur = tok_h.copy()
+    outcomes = []
+    denied = np.where(k >= 0, 0, 2).astype(np.uint8)
+    cap = np.uint32(2 * n // hs)
+    for _ in range(16):
+        v = ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
+        st = ctx.permit_status(scratch)
+        got_t = tok.cpu().numpy().view(np.uint32)
+        got_v = v.cpu().numpy()
+        if st == 0:
+            v_want, t_next = _np_permit(k, hs, t_cur)
+            assert np.array_equal(got_v, v_want)
+            assert np.array_equal(got_t, t_next)
+            t_cur = t_next
+        else:
+            assert st == -ETIMEDOUT
+            assert np.array_equal(got_t, t_cur)
+            assert np.array_equal(got_v, denied)
+        outcomes.append(st)
+        # a refill, so later launches still hold buckets that run out and some that do not
+        t_cur = np.minimum(t_cur + np.uint32(3), cap).astype(np.uint32)
+        tok.copy_(torch.from_numpy(t_cur.view(np.int32).copy()).to(dev))
+    print(f"spin {spin_ms} ms: {outcomes.count(0)} committed, "
+          f"{outcomes.count(-ETIMEDOUT)} aborted of {len(outcomes)}")
     ctx.close()
