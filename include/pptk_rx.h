@@ -764,6 +764,16 @@ int pptk_rx_gather_free(struct pptk_rx_gather *gather);
 /* Library / build identification for the loaders. */
 const char *pptk_rx_version(void);
 
+/* The layout revision of the structs in this header (pptk_rx_opts,
+ * pptk_rx_dev_batch, pptk_rx_ring_spec, ...).  It changes whenever one of
+ * them changes size or meaning (round 5 added pptk_rx_ring_spec.budget_bytes
+ * and .reserved; round 6 is the first revision with this check): a caller
+ * compares pptk_rx_abi() with the PPTK_RX_ABI it was compiled against before
+ * passing any struct, so a caller built against an older header is detected
+ * instead of read past its structs' end. */
+#define PPTK_RX_ABI 6
+int pptk_rx_abi(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -257,7 +257,9 @@ static uint64_t le64(const uint8_t *p) {
 
 extern "C" {
 
-const char *pptk_rx_version(void) { return "pptk_amd rx 0.1 gfx950"; }
+const char *pptk_rx_version(void) { return "pptk_amd rx 0.6 gfx950"; }
+
+int pptk_rx_abi(void) { return PPTK_RX_ABI; }
 
 void pptk_rx_opts_default(struct pptk_rx_opts *o) {
   if (!o) return;
@@ -394,9 +396,10 @@ static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
   constexpr uint32_t rx_bits = kTuneMask & ~(uint32_t)PPTK_RX_TUNE_PERMIT_PASSES;
   if (c->forced_flags >= 0) return (uint32_t)c->forced_flags & rx_bits;
   // (an environment word holding only the rate limiter's bit leaves the
-  // memory policy automatic, as pptk_rx_set_tuning does)
+  // memory policy automatic, as pptk_rx_set_tuning does; any other word,
+  // 0 included, forces the policy it names)
   const long tune = env_tune();
-  if (tune >= 0 && ((uint32_t)tune & rx_bits)) return (uint32_t)tune & rx_bits;
+  if (tune >= 0 && tune != PPTK_RX_TUNE_PERMIT_PASSES) return (uint32_t)tune & rx_bits;
   const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2 ||
                      variant == RX_L4;
   return (small || gather) ? PPTK_RX_TUNE_NT_STORES

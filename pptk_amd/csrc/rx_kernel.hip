@@ -297,7 +297,8 @@ __device__ __forceinline__ uint32_t sum_chunk(u32x4 c, int o, int rs, int re, ui
 // whole -- no byte masking at either end, so every lane runs the same four
 // dot2 ops whatever its frame's length.  The chunk holding the frame's last
 // byte therefore also adds the bytes [len, end of that chunk), which the
-// owning lane subtracts once per frame (tail_past_end).  `o` = frame offset.
+// same round takes off again (tail_past_end on the copy of that chunk the
+// team's last lane holds, see load_round).  `o` = frame offset.
 //
 // MASKED instead masks the bytes past the end inside the chunk (no
 // correction needed): the choice for fixed-stride batches, whose frames all
@@ -330,16 +331,18 @@ __device__ __forceinline__ int last_chunk_off(int m, int len) {
 
 // What sum_chunk_from over-counted for this frame: the bytes past its end
 // in its last chunk `tc`, if that chunk was summed (it starts at or after
-// the team start ts); absolute pairing, like the team sums.
+// the team start ts); absolute pairing, like the team sums.  Branch-free
+// (every lane of a round computes it): the keep-masks of the two 8-byte
+// halves are one 64-bit shift each.
 __device__ __forceinline__ uint32_t tail_past_end(u32x4 tc, int m, int len, int ts) {
-  const int e = (m + len) & 15;   // first byte past the end inside the chunk
-  if (len <= 0 || e == 0 || last_chunk_off(m, len) < ts)
-    return 0;
-  uint32_t t = 0;
-#pragma unroll
-  for (int d = 0; d < 4; ++d)
-    t = dot16(tc[d] & bmask(min(max(e - 4 * d, 0), 4), 4), t);
-  return t;
+  const uint32_t e8 = 8u * (uint32_t)((m + len) & 15);   // first bit past the end
+  const uint64_t lo = e8 >= 64u ? 0ull : ~0ull << (e8 & 63u);
+  const uint64_t hi = e8 <= 64u ? ~0ull : ~0ull << ((e8 - 64u) & 63u);
+  uint32_t t = dot16(tc.x & (uint32_t)lo, 0u);
+  t = dot16(tc.y & (uint32_t)(lo >> 32), t);
+  t = dot16(tc.z & (uint32_t)hi, t);
+  t = dot16(tc.w & (uint32_t)(hi >> 32), t);
+  return (len > 0 && e8 != 0u && last_chunk_off(m, len) >= ts) ? t : 0u;
 }
 
 // First chunk boundary (frame offset) at or after byte 18 of a frame whose
@@ -595,8 +598,7 @@ __device__ __forceinline__ u32x4 frag_words(const FrameView &v, const Parse &p) 
 // frame bytes [team_start_of(v.m), len), flow hash, bucket hash, and (tx
 // batches) the checksum stores.  DESIGN.md "Record semantics" steps 1-9.
 __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &v, uint32_t len,
-                                             uint64_t base, uint32_t my_sum, u32x4 tailc,
-                                             LaneRec &o) {
+                                             uint64_t base, uint32_t my_sum, LaneRec &o) {
   const int m = v.m;
   const Parse p = parse_frame(v, len);
   if (a.frag)
@@ -654,11 +656,9 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
       ps = dot16(s1, ps); ps = dot16(s2, ps); ps = dot16(s3, ps);
       ps = dot16(d0, ps); ps = dot16(d1, ps); ps = dot16(d2, ps); ps = dot16(d3, ps);
       ps += bswap16(proto) + bswap16(l4len);   // > 0: proto is 6 or 17
-      // region [rs, re) = [ts, L16) - [ts, rs) - [re, len) - [len, L16), mod
-      // 0xffff, where the team sum covered [ts, L16): L16 = the end of the
-      // chunk holding the last byte
-      uint32_t rsum = fold16(my_sum) + (0xffffu - fold16(tail_past_end(tailc, m, (int)len, ts)));
-      rsum += 0xffffu - fold16(s_tr);
+      // region [rs, re) = [ts, len) - [ts, rs) - [re, len), mod 0xffff,
+      // where the team sum covered exactly [ts, len)
+      uint32_t rsum = fold16(my_sum) + (0xffffu - fold16(s_tr));
       if (re < len)
         rsum += 0xffffu - fold16(sum_abs(v, (int)re, (int)len));
       rsum = fold16(rsum);
@@ -1079,13 +1079,6 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // is loaded here, the dependent offset/length of tile + 2 nwaves (whose
     // index arrived during the previous tile) before the last round group.
     const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
-    // the chunk holding the last byte of this lane's frame (for the
-    // over-count correction of the unmasked team sums); issued before this
-    // tile's rounds so that waiting for it never drains them
-    u32x4 tailc = (u32x4){0u, 0u, 0u, 0u};   // (masked sums: nothing to correct)
-    if constexpr (GATHER)
-      tailc = *(const u32x4 *)(a.frames + ((dc.base + (uint64_t)max(dc.len, 1u) - 1u) &
-                                           ~(uint64_t)15));
     // ---- streaming rounds: team g sums frame g*T + r over [team_start, len).
     // Fixed-slot ring of D + 1 rounds: round r lives in slot r % (D + 1); a
     // group of D + 1 rounds is unrolled so every slot index is a constant and
@@ -1129,10 +1122,21 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
           const int c = s * T + j;
           acc = sum_chunk_from<!GATHER>(cb.v[s], 16 * c - m, ts, (int)cb.pl, acc);
         }
-        if (!UNROLL && nch > S * T) {  // frames longer than the staged chunks
+        if (!UNROLL && nch > S * T) {  // frames longer than the staged chunks (masked)
           const u32x4 *c0 = (const u32x4 *)(a.frames + (cb.pb - (uint64_t)m));
           for (int c = S * T + j; c < nch; c += T)
-            acc = sum_chunk_from<!GATHER>(ldc<NT>(c0 + c), 16 * c - m, ts, (int)cb.pl, acc);
+            acc = sum_chunk_from<true>(ldc<NT>(c0 + c), 16 * c - m, ts, (int)cb.pl, acc);
+        }
+        if constexpr (GATHER) {
+          // The unmasked sums added the bytes past the frame's end in its
+          // last chunk.  The team's last lane holds that chunk in its last
+          // slot whenever the frame fits the round (its loads are clamped to
+          // the last chunk, load_round), so it takes them off here, in the
+          // round that streamed them: no second read of the chunk, no
+          // per-frame correction later.  (A lane's partial may wrap below
+          // zero; the team's u32 total cannot: it includes those bytes.)
+          const uint32_t corr = tail_past_end(cb.v[S - 1], m, (int)cb.pl, ts);
+          acc -= (j == T - 1 && nch <= S * T) ? corr : 0u;
         }
         acc = team_sum<T>(acc);
         if (j == r)
@@ -1178,15 +1182,15 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
         const int nch = (ma + (int)dc.len + 15) >> 4;
         if (nch > S * T) {
           const u32x4 *c0 = (const u32x4 *)(a.frames + (dc.base - (uint64_t)ma));
-          for (int c = S * T; c < nch; ++c)
-            my_sum = settle(sum_chunk_from<!GATHER>(ldc<NT>(c0 + c), 16 * c - ma, 0, (int)dc.len,
-                                                    my_sum));
+          for (int c = S * T; c < nch; ++c)   // (masked: the last one ends the frame)
+            my_sum = settle(sum_chunk_from<true>(ldc<NT>(c0 + c), 16 * c - ma, 0, (int)dc.len,
+                                                 my_sum));
         }
       }
       const FrameView v = {wimg + lane * IMG_STRIDE, (const GLB_AS uint8_t *)a.frames + dc.base, m,
                            16 * IMGC - m};
       LaneRec o;
-      lane_generic(a, v, dc.len, dc.base, my_sum, tailc, o);
+      lane_generic(a, v, dc.len, dc.base, my_sum, o);
       if (a.txside)
         a.txside[dc.idx] = o.tx;   // two-pass tx: 8 B per frame, coalesced in batch order
       // park the record in LDS (every lane's image reads are behind us in
@@ -1403,10 +1407,6 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
 
   while (tile < tend) {
     const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
-    u32x4 tailc = (u32x4){0u, 0u, 0u, 0u};
-    if constexpr (GATHER)
-      tailc = *(const u32x4 *)(a.frames + ((dc.base + (uint64_t)max(dc.len, 1u) - 1u) &
-                                           ~(uint64_t)15));
     // the next tile's schedule, into the other list (the previous tile's,
     // whose rounds are all consumed)
     const MSched sn = m_schedule(dn, lane, lst[cur ^ 1]);
@@ -1461,6 +1461,14 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
             acc = sum_chunk_from<true>(cb.v[i], 16 * ((i << tl) + j) - m, ts, pl, acc);
         }
         acc = m_team_sum(acc, tl);
+        if constexpr (GATHER) {
+          // the bytes past the frame's end in its last chunk, which the
+          // unmasked sums added: the team's last lane (which holds the team
+          // total) holds that chunk in its last slot when the frame fits the
+          // round (loads clamped to the last chunk, m_load_round)
+          const uint32_t corr = tail_past_end(cb.v[M_S - 1], m, pl, ts);
+          acc -= ((m + pl + 15) >> 4) <= (M_S << tl) ? corr : 0u;
+        }
         if (real && j == (1 << tl) - 1) *(LDS_AS uint32_t *)(img + M_SUM) = acc;
       }
     };
@@ -1484,14 +1492,14 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
       const int nch = (m + (int)dc.len + 15) >> 4;
       if (nch > 16 * M_S) {   // longer than a 16-lane round holds (jumbo): rare
         const u32x4 *c0 = (const u32x4 *)(a.frames + (dc.base - (uint64_t)m));
-        for (int c = 16 * M_S; c < nch; ++c)
-          my_sum = settle(sum_chunk_from<!GATHER>(ldc<NT>(c0 + c), 16 * c - m, 0, (int)dc.len,
-                                                  my_sum));
+        for (int c = 16 * M_S; c < nch; ++c)   // (masked: the last one ends the frame)
+          my_sum = settle(sum_chunk_from<true>(ldc<NT>(c0 + c), 16 * c - m, 0, (int)dc.len,
+                                               my_sum));
       }
       const FrameView v = {wimg + lane * IMG_STRIDE, (const GLB_AS uint8_t *)a.frames + dc.base, m,
                            16 * IMG_CHUNKS - m};
       LaneRec o;
-      lane_generic(a, v, dc.len, dc.base, my_sum, tailc, o);
+      lane_generic(a, v, dc.len, dc.base, my_sum, o);
       if (a.txside)
         a.txside[dc.idx] = o.tx;
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
@@ -1552,12 +1560,10 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
       for (int s = 0; s < 4; ++s)
         img[s] = (u32x4){d[4 * s], d[4 * s + 1], d[4 * s + 2], d[4 * s + 3]};
       // team-round equivalent: the sum of [team_start_of(0) = 32, len)
-      uint32_t ms = sum_chunk_from(img[2], 32, 32, (int)len, 0u);
-      ms = sum_chunk_from(img[3], 48, 32, (int)len, ms);
+      uint32_t ms = sum_chunk_from<true>(img[2], 32, 32, (int)len, 0u);
+      ms = sum_chunk_from<true>(img[3], 48, 32, (int)len, ms);
       const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + i * a.stride, 0, 64};
-      const uint32_t lc = len ? (len - 1u) >> 4 : 0u;   // chunk holding the last byte
-      const u32x4 tailc = lc == 0 ? c[0] : lc == 1 ? c[1] : lc == 2 ? c[2] : c[3];
-      lane_generic(a, v, len, i * a.stride, ms, tailc, o);
+      lane_generic(a, v, len, i * a.stride, ms, o);
     }
     emit_record(a, o, (uint32_t)i, (LDS_AS u32x4 *)slot, true);
   }

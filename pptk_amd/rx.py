@@ -186,7 +186,7 @@ EXPORTS = ("pptk_rx_opts_default", "pptk_rx_ctx_create", "pptk_rx_ctx_destroy",
            "pptk_rx_comm_create_all", "pptk_rx_comm_destroy", "pptk_rx_comm_info",
            "pptk_rx_comm_abort", "pptk_rx_comm_sync",
            "pptk_rx_shard_range", "pptk_rx_allgather_hash", "pptk_rx_stream_split",
-           "pptk_rx_stream_destroy",
+           "pptk_rx_stream_destroy", "pptk_rx_abi",
            # kept per-packet APIs (ipcksum.h, hashseed.h)
            "ip_cksum_feed", "ip_hdr_cksum_calc", "tcp_cksum_calc", "udp_cksum_calc",
            "tcp6_cksum_calc", "udp6_cksum_calc", "hash_seed_init",
@@ -198,6 +198,7 @@ VARIANTS = ("T4S1", "T4S2", "T16S2", "T16S6", "T32S3", "T64S2", "T16S7L", "T32S4
 RX_L4 = VARIANTS.index("L4")
 
 _libs = {}
+ABI = 6   # include/pptk_rx.h PPTK_RX_ABI
 
 
 def lib(path=None):
@@ -209,6 +210,11 @@ def lib(path=None):
             raise ImportError(f"{path} not built: run `make` or __graft_entry__.build()")
         L = ctypes.CDLL(path)
         vp = ctypes.c_void_p
+        # the struct layouts below are PPTK_RX_ABI's (older A/B builds lack
+        # the symbol and are taken as they are)
+        if hasattr(L, "pptk_rx_abi") and L.pptk_rx_abi() != ABI:
+            raise ImportError(f"{path}: struct layout revision {L.pptk_rx_abi()}, "
+                              f"this binding expects {ABI}")
         L.pptk_rx_opts_default.argtypes = [ctypes.POINTER(RxOpts)]
         L.pptk_rx_opts_default.restype = None
         L.pptk_rx_ctx_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(RxOpts)]

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round 6: the in-round tail correction (no second read of each frame's last
+# chunk): parity, then in-process A/B against the round-5 kernel, the PMC
+# read bytes of CMIX, and a write-phase period sweep on CMIX.
+cd $GRAFT_REPO_ROOT
+source scripts/gpu_steps.sh
+export TMPDIR=/tmp
+O=gpurun_out/r06b
+mkdir -p $O
+PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+step parity 900 $PT -m gpu tests/test_gpu_parity.py tests/test_gpu_frag.py tests/test_gpu_tx.py \
+  tests/test_gpu_rewrite.py tests/test_gpu_mss.py || exit $?
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
+export AB_LIBS=r05=tools/ab_r06/libpptkrx_r05.so AB_PLACE=1 AB_ROUNDS=7
+for cfg in cmix c1500 imix jmix c64; do
+  step ab_$cfg 300 python -u tools/ab.py $cfg -1:-1 r05:-1:-1 || exit $?
+done
+unset AB_LIBS AB_PLACE
+export AB_ROUNDS=2 AB_REPS=3
+step pmc_cmix_new 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rx_kernel -d $O/pmc_new \
+  -o run --output-format csv -- python3 tools/ab.py cmix -1:-1 || exit $?
+export AB_LIBS=r05=tools/ab_r06/libpptkrx_r05.so
+step pmc_cmix_r05 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex rx_kernel -d $O/pmc_r05 \
+  -o run --output-format csv -- python3 tools/ab.py cmix r05:-1:-1 || exit $?
+# write-phase period sweep on CMIX (experiment build: PPTK_RX_PHASE_TICKS
+# forces the period, 100 MHz ticks; the product's estimate beside it)
+export AB_LIBS=exp=tools/ab_r06/libpptkrx_exp.so AB_PLACE=1 AB_ROUNDS=5 AB_REPS=5
+for t in 0 1000 1360 1700 2000 2500 3200; do
+  PPTK_RX_PHASE_TICKS=$t step sweep_cmix_$t 240 python -u tools/ab.py cmix -1:-1 exp:-1:-1 || exit $?
+done

@@ -637,3 +637,12 @@ def test_comm_config_caps_channels_only_when_split():
     # the product library has no such hook
     assert not hasattr(ctypes.CDLL(os.path.join(ROOT, "pptk_amd", "libpptkrx.so")),
                        "pptk_rx_test_comm_config")
+
+
+def test_abi_revision_matches_header(lib):
+    """pptk_rx_abi() == the header's PPTK_RX_ABI == the Python binding's:
+    a caller can detect a library whose structs differ from its header."""
+    from pptk_amd import rx as R
+    txt = open(os.path.join(INCLUDE, "pptk_rx.h")).read()
+    hdr = int(re.search(r"#define PPTK_RX_ABI (\d+)", txt).group(1))
+    assert lib.pptk_rx_abi() == hdr == R.ABI
