@@ -28,3 +28,9 @@ export AB_LIBS=exp=tools/ab_r06/libpptkrx_exp.so AB_PLACE=1 AB_ROUNDS=5 AB_REPS=
 for t in 0 1000 1360 1700 2000 2500 3200; do
   PPTK_RX_PHASE_TICKS=$t step sweep_cmix_$t 240 python -u tools/ab.py cmix -1:-1 exp:-1:-1 || exit $?
 done
+# last (a hang here ends the call): the round-5 teardown order replayed with
+# the HIP runtime's API log, then the library's order
+gcc -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude tools/split_hang_repro.c -Lpptk_amd \
+  -lpptkrx -Wl,-rpath,$PWD/pptk_amd -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -o $O/repro || exit 1
+AMD_LOG_LEVEL=3 step repro_old 60 $O/repro old 4 || exit $?
+AMD_LOG_LEVEL=3 step repro_new 60 $O/repro new 4 || exit $?
