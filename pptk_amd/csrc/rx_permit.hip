@@ -1739,12 +1739,15 @@ void test_hooks(PermitFused &f) {
     const char *e = getenv(name);
     return e ? atol(e) : dflt;
   };
-  const long stall_ms = knob("PPTK_RX_TEST_PERMIT_STALL_MS", 0);
+  // (milliseconds, or microseconds through the _US forms, which win)
+  const long stall_us = knob("PPTK_RX_TEST_PERMIT_STALL_US",
+                             knob("PPTK_RX_TEST_PERMIT_STALL_MS", 0) * 1000);
   const long stall_at = knob("PPTK_RX_TEST_PERMIT_STALL_AT", 1);
-  const long spin_ms = knob("PPTK_RX_TEST_PERMIT_SPIN_MS", 0);
-  if (spin_ms > 0) f.spin_ticks = (uint64_t)spin_ms * 100000ull;
-  if (stall_ms > 0) {
-    f.stall_ticks = (uint64_t)std::min(stall_ms, 10000l) * 100000ull;
+  const long spin_us = knob("PPTK_RX_TEST_PERMIT_SPIN_US",
+                            knob("PPTK_RX_TEST_PERMIT_SPIN_MS", 0) * 1000);
+  if (spin_us > 0) f.spin_ticks = (uint64_t)spin_us * 100ull;
+  if (stall_us > 0) {
+    f.stall_ticks = (uint64_t)std::min(stall_us, 10000000l) * 100ull;
     f.stall_at = (uint32_t)stall_at;
   }
 #else

@@ -8,8 +8,8 @@ export TMPDIR=/tmp
 O=gpurun_out/r06b
 mkdir -p $O
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
-step parity 900 $PT -m gpu tests/test_gpu_parity.py tests/test_gpu_frag.py tests/test_gpu_tx.py \
-  tests/test_gpu_rewrite.py tests/test_gpu_mss.py || exit $?
+step permit 300 $PT -s "tests/test_gpu_permit.py::test_permit_fused_commit_decision_is_agreed" \
+  "tests/test_gpu_permit.py::test_permit_fused_abort_leaves_tokens_and_reports" || exit $?
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
 export AB_LIBS=r05=tools/ab_r06/libpptkrx_r05.so AB_PLACE=1 AB_ROUNDS=7
 for cfg in cmix c1500 imix jmix c64; do

@@ -475,16 +475,17 @@ def test_permit_fused_abort_leaves_tokens_and_reports(dev, monkeypatch, stall_at
     ctx.close()
 
 
-@pytest.mark.parametrize("spin_ms", [20, 21])
-def test_permit_fused_commit_decision_is_agreed(dev, monkeypatch, spin_ms):
+def test_permit_fused_commit_decision_is_agreed(dev, monkeypatch):
     """the last workgroup is held before barrier 2 (the commit
-    point) for as long as the others wait there (20 ms against 20 / 21 ms),
-    so its arrival lands right around their deadline, on both sides of it
-    over the repeats.  Whatever each launch decides, all workgroups act on
-    the one decision word: either status 0 with the frame-by-frame verdicts
-    and tokens (chained through the launches), or -ETIMEDOUT with the tokens
-    exactly as before that launch and every subject denied -- never some
-    buckets committed and others not."""
+    point) for 20 ms while the others wait there for 20 ms + delta, delta
+    stepping through -200 .. +600 us in 20-us steps (41 launches), so the
+    held workgroup's arrival lands before, at and after their deadlines:
+    across the sweep the outcome flips from abort to commit, and the
+    launches at the flip race the decision.  Whatever each launch decides,
+    all workgroups act on the one decision word: either status 0 with the
+    frame-by-frame verdicts and tokens (chained through the launches), or
+    -ETIMEDOUT with the tokens exactly as before that launch and every
+    subject denied -- never some buckets committed and others not."""
     from conftest import HOOKS_LIB
     from pptk_amd.rx import RxContext
     if _PATH[0] == "passes":
@@ -496,31 +497,30 @@ def test_permit_fused_commit_decision_is_agreed(dev, monkeypatch, spin_ms):
     tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
     scratch = torch.empty(ctx._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8,
                           device=dev)
-    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_MS", "20")
-    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_SPIN_MS", str(spin_ms))
+    monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_US", "20000")
     monkeypatch.setenv("PPTK_RX_TEST_PERMIT_STALL_AT", "2")
     t_cur = tok_h.copy()
     outcomes = []
     denied = np.where(k >= 0, 0, 2).astype(np.uint8)
     cap = np.uint32(2 * n // hs)
-    for _ in range(16):
+    for delta in range(-200, 601, 20):
+        monkeypatch.setenv("PPTK_RX_TEST_PERMIT_SPIN_US", str(20000 + delta))
         v = ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
         st = ctx.permit_status(scratch)
         got_t = tok.cpu().numpy().view(np.uint32)
         got_v = v.cpu().numpy()
         if st == 0:
             v_want, t_next = _np_permit(k, hs, t_cur)
-            assert np.array_equal(got_v, v_want)
-            assert np.array_equal(got_t, t_next)
+            assert np.array_equal(got_v, v_want), delta
+            assert np.array_equal(got_t, t_next), delta
             t_cur = t_next
         else:
             assert st == -ETIMEDOUT
-            assert np.array_equal(got_t, t_cur)
-            assert np.array_equal(got_v, denied)
-        outcomes.append(st)
+            assert np.array_equal(got_t, t_cur), delta
+            assert np.array_equal(got_v, denied), delta
+        outcomes.append((delta, "C" if st == 0 else "A"))
         # a refill, so later launches still hold buckets that run out and some that do not
         t_cur = np.minimum(t_cur + np.uint32(3), cap).astype(np.uint32)
         tok.copy_(torch.from_numpy(t_cur.view(np.int32).copy()).to(dev))
-    print(f"spin {spin_ms} ms: {outcomes.count(0)} committed, "
-          f"{outcomes.count(-ETIMEDOUT)} aborted of {len(outcomes)}")
+    print("delta us -> outcome: " + " ".join(f"{d}{o}" for d, o in outcomes))
     ctx.close()
