@@ -478,8 +478,9 @@ def test_permit_fused_abort_leaves_tokens_and_reports(dev, monkeypatch, stall_at
 def test_permit_fused_commit_decision_is_agreed(dev, monkeypatch):
     """the last workgroup is held before barrier 2 (the commit
     point) for 20 ms while the others wait there for 20 ms + delta, delta
-    stepping through -200 .. +600 us in 20-us steps (41 launches), so the
-    held workgroup's arrival lands before, at and after their deadlines:
+    stepping through -40 .. +60 us in 2-us steps (51 launches; the outcome
+    flipped between +0 and +20 us in a coarser sweep), so the held
+    workgroup's arrival lands before, at and after their deadlines:
     across the sweep the outcome flips from abort to commit, and the
     launches at the flip race the decision.  Whatever each launch decides,
     all workgroups act on the one decision word: either status 0 with the
@@ -503,7 +504,7 @@ def test_permit_fused_commit_decision_is_agreed(dev, monkeypatch):
     outcomes = []
     denied = np.where(k >= 0, 0, 2).astype(np.uint8)
     cap = np.uint32(2 * n // hs)
-    for delta in range(-200, 601, 20):
+    for delta in range(-40, 61, 2):
         monkeypatch.setenv("PPTK_RX_TEST_PERMIT_SPIN_US", str(20000 + delta))
         v = ctx.permit_keys_device(keys, 4, tok, scratch=scratch)
         st = ctx.permit_status(scratch)
