@@ -49,6 +49,15 @@ constexpr int IMG_CHUNKS = 8;     // 16-byte chunks parked in LDS per frame
 // in-process A/B) -- the per-frame phase is hidden behind the streaming --
 // so 144 stays.
 constexpr int IMG_STRIDE = PPTK_RX_IMG_STRIDE;
+// Offset-described batches: where the team parks a frame's last chunk in the
+// frame's slot (rx_kernel); PPTK_RX_TAIL_LDS=0 (A/B) corrects in the round.
+#ifndef PPTK_RX_TAIL_LDS
+#define PPTK_RX_TAIL_LDS 1
+#endif
+constexpr bool TAIL_LDS = PPTK_RX_TAIL_LDS;
+constexpr int TAIL_OFF = 128;
+static_assert(!TAIL_LDS || (IMG_STRIDE >= TAIL_OFF + 16 && IMG_STRIDE % 16 == 0),
+              "the parked tail chunk lives past the 128-byte image");
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -597,8 +606,13 @@ __device__ __forceinline__ u32x4 frag_words(const FrameView &v, const Parse &p) 
 // parse, IPv4 header checksum, L4 checksum from the team sum `my_sum` of the
 // frame bytes [team_start_of(v.m), len), flow hash, bucket hash, and (tx
 // batches) the checksum stores.  DESIGN.md "Record semantics" steps 1-9.
+// `my_sum` = the team sum of the frame bytes [team_start_of(v.m), end of the
+// chunk holding the last byte) when `tailc` is that last chunk (the bytes
+// past the end are taken off here), or of exactly [team_start, len) when
+// `tailc` is zero.
 __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &v, uint32_t len,
-                                             uint64_t base, uint32_t my_sum, LaneRec &o) {
+                                             uint64_t base, uint32_t my_sum, u32x4 tailc,
+                                             LaneRec &o) {
   const int m = v.m;
   const Parse p = parse_frame(v, len);
   if (a.frag)
@@ -656,9 +670,11 @@ __device__ __forceinline__ void lane_generic(const RxKArgs &a, const FrameView &
       ps = dot16(s1, ps); ps = dot16(s2, ps); ps = dot16(s3, ps);
       ps = dot16(d0, ps); ps = dot16(d1, ps); ps = dot16(d2, ps); ps = dot16(d3, ps);
       ps += bswap16(proto) + bswap16(l4len);   // > 0: proto is 6 or 17
-      // region [rs, re) = [ts, len) - [ts, rs) - [re, len), mod 0xffff,
-      // where the team sum covered exactly [ts, len)
-      uint32_t rsum = fold16(my_sum) + (0xffffu - fold16(s_tr));
+      // region [rs, re) = [ts, L) - [len, L) - [ts, rs) - [re, len), mod
+      // 0xffff, where the team sum covered [ts, L): L = len, or the end of
+      // the chunk holding the last byte (tailc: tail_past_end is [len, L))
+      uint32_t rsum = fold16(my_sum) + (0xffffu - fold16(tail_past_end(tailc, m, (int)len, ts)));
+      rsum += 0xffffu - fold16(s_tr);
       if (re < len)
         rsum += 0xffffu - fold16(sum_abs(v, (int)re, (int)len));
       rsum = fold16(rsum);
@@ -1131,12 +1147,18 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
           // The unmasked sums added the bytes past the frame's end in its
           // last chunk.  The team's last lane holds that chunk in its last
           // slot whenever the frame fits the round (its loads are clamped to
-          // the last chunk, load_round), so it takes them off here, in the
-          // round that streamed them: no second read of the chunk, no
-          // per-frame correction later.  (A lane's partial may wrap below
-          // zero; the team's u32 total cannot: it includes those bytes.)
-          const uint32_t corr = tail_past_end(cb.v[S - 1], m, (int)cb.pl, ts);
-          acc -= (j == T - 1 && nch <= S * T) ? corr : 0u;
+          // the last chunk, load_round): it parks it in the frame's image
+          // slot (bytes 128..143), where the owning lane takes those bytes
+          // off in the lane phase -- no second read of the chunk from
+          // memory, one LDS store per round.  (TAIL_LDS 0, A/B: the same
+          // correction here, every lane computing it, every round; a lane's
+          // partial may wrap below zero, the team's u32 total cannot.)
+          if constexpr (TAIL_LDS) {
+            if (j == T - 1) *(LDS_AS u32x4 *)(img + TAIL_OFF) = cb.v[S - 1];
+          } else {
+            const uint32_t corr = tail_past_end(cb.v[S - 1], m, (int)cb.pl, ts);
+            acc -= (j == T - 1 && nch <= S * T) ? corr : 0u;
+          }
         }
         acc = team_sum<T>(acc);
         if (j == r)
@@ -1177,9 +1199,17 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // tune bit 4 (diagnostics only, output invalid): skip the lane phase
     if (dc.idx != 0xffffffffu && !(kDiag && (a.tune & 16u))) {
       const int m = (int)(dc.base & 15);
+      const int ma = (int)(dc.base & ALM);
+      const int nch = (ma + (int)dc.len + 15) >> 4;
+      // the frame's last chunk as its team parked it (frames that fit the
+      // round; longer ones were summed masked)
+      u32x4 tailc = (u32x4){0u, 0u, 0u, 0u};
+      if constexpr (GATHER && TAIL_LDS) {
+        const u32x4 t = *(const LDS_AS u32x4 *)(wimg + lane * IMG_STRIDE + TAIL_OFF);
+        const bool fits = nch <= S * T;
+        tailc = (u32x4){fits ? t.x : 0u, fits ? t.y : 0u, fits ? t.z : 0u, fits ? t.w : 0u};
+      }
       if (UNROLL) {  // unrolled variants: chunks past the staged S*T, summed here (rare)
-        const int ma = (int)(dc.base & ALM);
-        const int nch = (ma + (int)dc.len + 15) >> 4;
         if (nch > S * T) {
           const u32x4 *c0 = (const u32x4 *)(a.frames + (dc.base - (uint64_t)ma));
           for (int c = S * T; c < nch; ++c)   // (masked: the last one ends the frame)
@@ -1190,7 +1220,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
       const FrameView v = {wimg + lane * IMG_STRIDE, (const GLB_AS uint8_t *)a.frames + dc.base, m,
                            16 * IMGC - m};
       LaneRec o;
-      lane_generic(a, v, dc.len, dc.base, my_sum, o);
+      lane_generic(a, v, dc.len, dc.base, my_sum, tailc, o);
       if (a.txside)
         a.txside[dc.idx] = o.tx;   // two-pass tx: 8 B per frame, coalesced in batch order
       // park the record in LDS (every lane's image reads are behind us in
@@ -1499,7 +1529,7 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
       const FrameView v = {wimg + lane * IMG_STRIDE, (const GLB_AS uint8_t *)a.frames + dc.base, m,
                            16 * IMG_CHUNKS - m};
       LaneRec o;
-      lane_generic(a, v, dc.len, dc.base, my_sum, o);
+      lane_generic(a, v, dc.len, dc.base, my_sum, (u32x4){0u, 0u, 0u, 0u}, o);
       if (a.txside)
         a.txside[dc.idx] = o.tx;
       emit_record(a, o, dc.idx, (LDS_AS u32x4 *)wimg + lane * 5, stage);
@@ -1563,7 +1593,7 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
       uint32_t ms = sum_chunk_from<true>(img[2], 32, 32, (int)len, 0u);
       ms = sum_chunk_from<true>(img[3], 48, 32, (int)len, ms);
       const FrameView v = {slot, (const GLB_AS uint8_t *)a.frames + i * a.stride, 0, 64};
-      lane_generic(a, v, len, i * a.stride, ms, o);
+      lane_generic(a, v, len, i * a.stride, ms, (u32x4){0u, 0u, 0u, 0u}, o);
     }
     emit_record(a, o, (uint32_t)i, (LDS_AS u32x4 *)slot, true);
   }
