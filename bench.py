@@ -1157,7 +1157,7 @@ def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", "c1500", 1 << 20, False, False),
     from pptk_amd.rx import RxContext, ldp_packets
     from harness.synth import make_batch
     threads, _ = _cpu_topology()
-    gt = max(1, min(8, threads))
+    gt = max(1, min(16, threads))
     ceil = pcie_ceiling(dev)
     out = {"pcie_h2d_gbs": ceil, "gather_threads": gt}
     for key, cfg, n, reg, compact in cfgs:

@@ -36,6 +36,12 @@ struct PartDesc {
   size_t bytes = 0, base = 0;
   size_t lo = SIZE_MAX, hi = 0, fbytes = 0;
   uint32_t maxlen = 0;
+  // uniform frames: every frame of the part sz0 bytes, at p0 + k * stride
+  // (k = its index in the part); cleared at the first frame that is not
+  bool uni = true;
+  uint32_t sz0 = 0;
+  const uint8_t *p0 = nullptr;
+  int64_t stride = 0;
 };
 
 // One half of the host-batch double buffer: pinned staging, device copies,
@@ -1212,6 +1218,14 @@ static double ring_dma_density() {
   return v / 100.0;
 }
 
+// Uniform chunks (every frame one length, ring frames at one stride) run as
+// fixed-stride batches without descriptors (enqueue_chunk).  PPTK_RX_UNIFORM=0
+// turns that off (A/B).
+static bool uniform_chunks() {
+  static const long v = EXP_KNOB("PPTK_RX_UNIFORM", 1);
+  return v != 0;
+}
+
 // Copy one frame into 16-byte-aligned pinned staging with non-temporal
 // stores: the lines go to memory without being read for ownership first
 // and without staying dirty in the host caches, where the copy engine's
@@ -1284,18 +1298,33 @@ static int retire(RxSlot &sl, WorkerPool *pool) {
 // The registered ring holding every frame of pkts[0, num), so that frame
 // bytes can be read in place (the kernel reads whole 16-byte chunks, so each
 // frame's chunk-rounded end must lie inside the ring too); NULL otherwise.
-static const RxRing *ring_of(const pptk_rx_ctx *c, const struct ldp_packet *pkts, int num) {
+// (Large calls check their frames on the worker pool: a serial pass over 4 M
+// descriptors cost a C64 call more than its frame copies.)
+static const RxRing *ring_of(const pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
+                             WorkerPool *pool) {
   if (c->rings.empty() || num <= 0) return nullptr;
   const uint8_t *p0 = (const uint8_t *)pkts[0].data;
   for (const RxRing &r : c->rings) {
     if (p0 < r.host || p0 >= r.host + r.bytes) continue;
-    for (int i = 0; i < num; ++i) {
-      const uint8_t *p = (const uint8_t *)pkts[i].data;
-      if (!p || p < r.host) return nullptr;
-      const size_t off = (size_t)(p - r.host);
-      if (((off + pkts[i].sz + 15) & ~(size_t)15) > r.bytes) return nullptr;
-    }
-    return &r;
+    auto inside = [&r, pkts](size_t i0, size_t i1) {
+      for (size_t i = i0; i < i1; ++i) {
+        const uint8_t *p = (const uint8_t *)pkts[i].data;
+        if (!p || p < r.host) return false;
+        const size_t off = (size_t)(p - r.host);
+        if (((off + pkts[i].sz + 15) & ~(size_t)15) > r.bytes) return false;
+      }
+      return true;
+    };
+    constexpr size_t kPart = 1u << 16;
+    if (!pool || (size_t)num < 2 * kPart) return inside(0, (size_t)num) ? &r : nullptr;
+    const size_t parts = ((size_t)num + kPart - 1) / kPart;
+    std::atomic<bool> ok{true};
+    pool->parallel_for(parts, [&](size_t t) {
+      if (ok.load(std::memory_order_relaxed) &&
+          !inside(t * kPart, std::min((size_t)num, (t + 1) * kPart)))
+        ok.store(false, std::memory_order_relaxed);
+    });
+    return ok.load() ? &r : nullptr;
   }
   return nullptr;
 }
@@ -1377,10 +1406,18 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
   auto describe = [&sl, cp, ring, maxf, nt, &stage](size_t i0, size_t i1, size_t base,
                                                     bool gather, PartDesc &d) {
     size_t pos = base;
+    if (i1 > i0) {
+      d.p0 = (const uint8_t *)cp[i0].data;
+      d.sz0 = cp[i0].sz;
+      d.stride = i1 - i0 > 1 ? (const uint8_t *)cp[i0 + 1].data - d.p0 : 0;
+      d.uni = d.p0 != nullptr && d.sz0 <= maxf;
+    }
     for (size_t i = i0; i < i1; ++i) {
       const struct ldp_packet &pk = cp[i];
       const bool ok = pk.data && pk.sz <= maxf;
       const uint32_t sz = ok ? pk.sz : 0u;
+      d.uni = d.uni && pk.sz == d.sz0 &&
+              (const uint8_t *)pk.data == d.p0 + (int64_t)(i - i0) * d.stride;
       sl.h_len[i] = (uint16_t)sz;
       if (ring) {
         const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
@@ -1455,6 +1492,29 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
     fbytes += d.fbytes;
     maxlen = std::max(maxlen, d.maxlen);
   }
+  // Uniform chunk: every frame the same length (and, for a registered ring,
+  // at one fixed stride from the first): it runs as a fixed-stride batch --
+  // no descriptor is read by the kernel (in a staged chunk the frames sit at
+  // 16-byte-rounded offsets, i.e. at a fixed stride already), and frames of
+  // at most 64 bytes take the lane kernel.  A C64 chunk then moves its frames
+  // and its records over PCIe and nothing else.
+  bool uni_len = !parts.empty(), uni_ptr = uni_len;
+  int64_t stride = 0;
+  {
+    const PartDesc &f = parts[0];
+    stride = f.stride;
+    for (size_t t = 0; t < parts.size() && uni_len; ++t) {
+      const PartDesc &d = parts[t];
+      const size_t i0 = cnt * t / parts.size();
+      uni_len = d.uni && d.sz0 == f.sz0;
+      // (each part's own stride, and its first frame where the first
+      // part's stride puts it; one-frame parts have no stride of their own)
+      uni_ptr = uni_ptr && uni_len && (d.stride == stride || cnt * (t + 1) / parts.size() - i0 == 1) &&
+                d.p0 == f.p0 + (int64_t)i0 * stride;
+    }
+    if (cnt == 1) uni_ptr = false;
+  }
+  const uint32_t ulen = parts.empty() ? 0u : parts[0].sz0;
   // a dense ring chunk goes down as one span; the kernel sees the span's
   // buffer shifted down by `lo`, so the ring offsets stay as they are
   const bool ring_dma = ring && hi > lo && hi - lo > direct_max_bytes() &&
@@ -1485,6 +1545,20 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
   b.d_len = pcie ? sl.hd_len : sl.d_len;
   b.max_len = maxlen;
   b.n = cnt;
+  if (uniform_chunks() && cnt > 1 && uni_len && (!ring || (uni_ptr && stride > 0))) {
+    // fixed stride: staged frames at i * round16(len); ring frames at the
+    // first frame's place + i * stride
+    b.d_off = nullptr;
+    b.d_len = nullptr;
+    b.fixed_len = ulen;
+    if (ring) {
+      b.d_frames += (size_t)(parts[0].p0 - ring->host);
+      b.stride = (uint64_t)stride;
+    } else {
+      b.stride = (ulen + 15u) & ~15u;
+      if (b.stride == 0) b.stride = 16;
+    }
+  }
   // records: into the caller's array itself when it is registered
   void *d_out = rreg ? (void *)(rreg->dev + ((const uint8_t *)out - rreg->host))
                 : pcie ? (void *)sl.hd_recs
@@ -1534,10 +1608,10 @@ static int host_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int 
   if (c->async_n) return -EBUSY;   // the submissions own the slots
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
-  const RxRing *ring = ring_of(c, pkts, num);
+  WorkerPool *pool = pool_of(c);
+  const RxRing *ring = ring_of(c, pkts, num, pool);
   const RxRing *rreg = records_region(c, recs, (size_t)num * rec_bytes);
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
-  WorkerPool *pool = pool_of(c);
   int rc = 0;
   // Multi-buffered: while chunk k runs on one slot's stream (H2D, kernel,
   // D2H), the host gathers the next chunks into the other slots.
@@ -1577,7 +1651,7 @@ static int host_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int
   if (c->async_n >= PPTK_RX_MAX_INFLIGHT) return -EBUSY;
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
-  const RxRing *ring = ring_of(c, pkts, num);
+  const RxRing *ring = ring_of(c, pkts, num, pool_of(c));
   const RxRing *rreg = records_region(c, recs, (size_t)num * rec_bytes);
   // the slots rotate in submission order (FIFO), so consecutive
   // submissions run on different streams and may overlap on the GPU
