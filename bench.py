@@ -1255,7 +1255,7 @@ def gather_bench(ctx, gb, ws, dev, steps, stream=None):
 
 # the newest round's committed PMC summary (tools/pmc_summary.py)
 PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json")
-                                for r in ("r05", "r04", "r03", "r02", "r01")) if os.path.exists(p)),
+                                for r in ("r06", "r05", "r04", "r03", "r02", "r01")) if os.path.exists(p)),
                    os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"))
 
 
