@@ -641,7 +641,7 @@ def compact_line(full, detail_path=None):
     if e2e:
         line["e2e"] = ({k: ({kk: v.get(kk) for kk in ("mpkts", "path", "frame_gbs", "of_pcie")}
                             if isinstance(v, dict) else v)
-                        for k, v in e2e.items() if k != "gather_threads"})
+                        for k, v in e2e.items() if k not in ("gather_threads", "numa")})
     ops = {}
     pm = full.get("permit") or {}
     for key, sub in (("permit_records_ms", pm), ("permit_keys_ms", pm.get("keys")),
@@ -1134,9 +1134,33 @@ def pcie_ceiling(dev, mb=96, reps=20):
     return round((mb << 20) * reps / (time.perf_counter() - t0) / 1e9, 2)
 
 
+def gpu_numa(dev):
+    """The GPU's NUMA node (sysfs, by PCI bus id) and the CPUs of that node
+    this process may run on: {"node": N, "cpus": [...]}, or None when the
+    box does not say."""
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read().strip())
+        if node < 0:
+            return None
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = set()
+            for part in f.read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                cpus.update(range(int(lo), int(hi or lo) + 1))
+        mine = sorted(cpus & os.sched_getaffinity(0))
+        return {"node": node, "bdf": bdf, "cpus": mine} if mine else None
+    except (OSError, AttributeError, ValueError):
+        return None
+
+
 def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", "c1500", 1 << 20, False, False),
                                       ("c64", "c64", 1 << 22, True, False),
-                                      ("c64_rec32", "c64", 1 << 22, True, True))):
+                                      ("c64_rec32", "c64", 1 << 22, True, True)),
+              numa_local=True):
     """End to end, host to host (the north star's "rate
     including pinned hipMemcpyAsync to and from the GPU"): pptk_rx_batch on
     borrowed ldp_packet frames in host memory (reference rx loop
@@ -1152,18 +1176,42 @@ def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", "c1500", 1 << 20, False, False),
     Every mode is checked bit-exact against a device-resident launch of the
     same frames before it is timed.  Reported: the faster path, Mpkt/s,
     frame GB/s and its fraction of this box's pinned H2D copy rate."""
+    threads, _ = _cpu_topology()
+    gt = max(1, min(16, threads))
+    # An rx loop runs on the CPUs next to its NIC and GPU, and its ring lives
+    # in their memory (netmap allocates it once, ldp/ldpnetmap.c:163-185).
+    # numa_local: this process (so the library's gather threads, created per
+    # context below, and the first touch of the ring and record arrays) on the
+    # GPU's NUMA node for the measurement -- unpinned, the ring's pages land
+    # wherever the main thread happens to run, and a ring on the far socket
+    # made the C64 ring path swing between runs (716 vs 588 Mpkt/s with 32-byte
+    # records, profiles/r06/e2e/).
+    numa = gpu_numa(dev) if numa_local else None
+    old_aff = os.sched_getaffinity(0)
+    if numa:
+        os.sched_setaffinity(0, numa["cpus"])
+    try:
+        out = {"pcie_h2d_gbs": pcie_ceiling(dev), "gather_threads": gt,
+               "numa": None if not numa else {"node": numa["node"], "cpus": len(numa["cpus"])}}
+        _e2e_configs(dev, seconds, cfgs, gt, out)
+    finally:
+        if numa:
+            os.sched_setaffinity(0, old_aff)
+    return out
+
+
+def _e2e_configs(dev, seconds, cfgs, gt, out):
     import torch
     from pptk_amd.records import REC32_DTYPE, REC_DTYPE, diff_records
     from pptk_amd.rx import RxContext, ldp_packets
     from harness.synth import make_batch
-    threads, _ = _cpu_topology()
-    gt = max(1, min(16, threads))
-    ceil = pcie_ceiling(dev)
-    out = {"pcie_h2d_gbs": ceil, "gather_threads": gt}
+    ceil = out["pcie_h2d_gbs"]
     for key, cfg, n, reg, compact in cfgs:
         b = make_batch(cfg, n, dev)
         stride, flen = b["stride"], b["fixed_len"]
-        ring = b["frames"][: n * stride + 64].cpu().numpy()      # the host "ring"
+        # the host "ring", first touched here (on the CPUs just chosen)
+        ring = np.zeros(n * stride + 64, dtype=np.uint8)
+        torch.from_numpy(ring).copy_(b["frames"][: n * stride + 64])
         ctx = RxContext(0, KEY, max_batch=65536, max_frame=1518, gather_threads=gt)
         ref = ctx.batch_device(b["frames"], n, stride=stride, fixed_len=flen, compact=compact)
         dt = REC32_DTYPE if compact else REC_DTYPE
@@ -1200,7 +1248,6 @@ def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", "c1500", 1 << 20, False, False),
                     "staged_mpkts": res["staged"], "ring_mpkts": res["ring"]}
         del ring, pkts, outbuf, want
         torch.cuda.empty_cache()
-    return out
 
 
 def forced_ms(ctx, b, recs, n, variant, steps, warmup=3):
