@@ -231,6 +231,22 @@ PLACE_RECORDS = 8         # record-buffer candidates
 SCRUB_BYTES_PER_S = 20e9
 
 
+_SCRUB_UNTIL = [0.0]   # when the scrub of everything freed so far should be over
+
+
+def note_freed(nbytes, at):
+    _SCRUB_UNTIL[0] = max(_SCRUB_UNTIL[0], at + nbytes / SCRUB_BYTES_PER_S)
+
+
+def wait_scrub(cap_s=20.0):
+    """Sleep until the driver's scrub of what this process freed is over
+    (at SCRUB_BYTES_PER_S, at most cap_s); returns the seconds slept."""
+    left = min(cap_s, _SCRUB_UNTIL[0] - time.perf_counter())
+    if left > 0:
+        time.sleep(left)
+    return round(max(0.0, left), 2)
+
+
 def release(dev):
     """Return the caching allocator's free blocks to the driver; returns
     (bytes released, when), the input of the scrub wait."""
@@ -238,7 +254,9 @@ def release(dev):
     torch.cuda.synchronize(dev)
     before = torch.cuda.memory_reserved(dev)
     torch.cuda.empty_cache()
-    return max(0, before - torch.cuda.memory_reserved(dev)), time.perf_counter()
+    freed, at = max(0, before - torch.cuda.memory_reserved(dev)), time.perf_counter()
+    note_freed(freed, at)
+    return freed, at
 
 
 def _spaced(dev, count, nbytes, spacer, hold):
@@ -320,6 +338,7 @@ def ring_buffers(ctx, b, n, dev, compact, probe_hash=False):
     freed, at = release(dev)          # the batch as generated, now copied into the ring
     report["freed_bytes"] += freed
     report["_freed_at"] = at
+    note_freed(report["freed_bytes"], at)
     return ring.recs, report
 
 
@@ -340,6 +359,7 @@ def placed_gather(ctx, b, recs, kw, n_total, ws, rank, dev):
     gbs = [GatherBuffer(n_total, ws, rank, dev, out=g.out[k]) for k in range(2)]
     rep = dict(g.report)
     rep["_freed_at"] = time.perf_counter()
+    note_freed(rep.get("freed_bytes", 0), rep["_freed_at"])
     return gbs, rep
 
 
@@ -641,7 +661,7 @@ def compact_line(full, detail_path=None):
     if e2e:
         line["e2e"] = ({k: ({kk: v.get(kk) for kk in ("mpkts", "path", "frame_gbs", "of_pcie")}
                             if isinstance(v, dict) else v)
-                        for k, v in e2e.items() if k not in ("gather_threads", "numa")})
+                        for k, v in e2e.items() if k not in ("gather_threads", "numa", "scrub_wait_s")})
     ops = {}
     pm = full.get("permit") or {}
     for key, sub in (("permit_records_ms", pm), ("permit_keys_ms", pm.get("keys")),
@@ -978,7 +998,7 @@ def rewrite_bench(ctx, n, dev, rank, steps, warmup):
     ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
     ach = b["bytes"] / (ms * 1e-3) / 1e9
     del b
-    torch.cuda.empty_cache()
+    release(dev)
     return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "kernel_ms": round(ms, 4),
             "workload": "C64 frames, TTL-1 + src/dst/ports rewritten in place, "
                         "checksums updated incrementally (RFC 1624)",
@@ -1022,7 +1042,7 @@ def mss_bench(ctx, n, dev, steps, warmup, stride=80):
     ms = float(np.median([a.elapsed_time(z) for a, z in ev]))
     ach = n * len(f) / (ms * 1e-3) / 1e9
     del frames, st
-    torch.cuda.empty_cache()
+    release(dev)
     return {"value": round(n / ms / 1e3, 1), "unit": "Mpkts/s", "kernel_ms": round(ms, 4),
             "workload": f"{n} IPv4 SYNs ({len(f)} B, MSS/SACK-perm/TS/NOP/WS options) in "
                         f"{stride}-byte slots, MSS clamped in place with checksum update",
@@ -1115,7 +1135,7 @@ def permit_bench(n, dev, ws, rank, steps, warmup, hash_size=1 << 16,
                                    "batch (~half the frames denied: resolve pass in every block)",
                                    c, "keys_denying")
     del recs, keys, verdict, scratch
-    torch.cuda.empty_cache()
+    release(dev)
     return out
 
 
@@ -1186,12 +1206,18 @@ def e2e_bench(dev, seconds=2.0, cfgs=(("c1500", "c1500", 1 << 20, False, False),
     # wherever the main thread happens to run, and a ring on the far socket
     # made the C64 ring path swing between runs (716 vs 588 Mpkt/s with 32-byte
     # records, profiles/r06/e2e/).
+    # After the device-resident configs the driver is still scrubbing the
+    # tens of GB their placement probes and buffers freed; beside that scrub
+    # the C64 paths measured 20-25 % slower (588 / 518 against 716 / 683
+    # Mpkt/s ring / staged with 32-byte records, profiles/r06/e2e/), so the
+    # measurement starts after it.
+    scrub_s = wait_scrub()
     numa = gpu_numa(dev) if numa_local else None
     old_aff = os.sched_getaffinity(0)
     if numa:
         os.sched_setaffinity(0, numa["cpus"])
     try:
-        out = {"pcie_h2d_gbs": pcie_ceiling(dev), "gather_threads": gt,
+        out = {"pcie_h2d_gbs": pcie_ceiling(dev), "gather_threads": gt, "scrub_wait_s": scrub_s,
                "numa": None if not numa else {"node": numa["node"], "cpus": len(numa["cpus"])}}
         _e2e_configs(dev, seconds, cfgs, gt, out)
     finally:
@@ -1247,7 +1273,7 @@ def _e2e_configs(dev, seconds, cfgs, gt, out):
                     "records": ("registered" if reg else "copied") + (" 32 B" if compact else " 64 B"),
                     "staged_mpkts": res["staged"], "ring_mpkts": res["ring"]}
         del ring, pkts, outbuf, want
-        torch.cuda.empty_cache()
+        release(dev)
 
 
 def forced_ms(ctx, b, recs, n, variant, steps, warmup=3):
@@ -1559,7 +1585,7 @@ def main():
     full_check = prim.get("full_batch_check")
     sample_check = prim.get("oracle_sample")
     del prim["_batch"], prim["_recs"]
-    torch.cuda.empty_cache()
+    release(dev)
 
     secondary = {}
     if not args.no_secondary and args.only is None:
@@ -1592,7 +1618,7 @@ def main():
                 secondary[cfg]["cpu_baseline"] = cpu_baseline_small(
                     r["_batch"], seconds=max(1.0, args.cpu_seconds / 2.5))
             del r["_batch"], r["_recs"]
-            torch.cuda.empty_cache()
+            release(dev)
 
     permit = rewrite = mss = None
     if not args.no_secondary and args.only is None:

@@ -5,7 +5,7 @@
 cd $GRAFT_REPO_ROOT
 source scripts/gpu_steps.sh
 export TMPDIR=/tmp
-O=gpurun_out/r06final
+O=gpurun_out/${R06_OUT:-r06final}
 mkdir -p $O
 step gpu 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread || exit $?
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
