@@ -42,6 +42,7 @@ struct PartDesc {
   uint32_t sz0 = 0;
   const uint8_t *p0 = nullptr;
   int64_t stride = 0;
+  bool outside = false;   // a frame not (wholly) inside the candidate ring
 };
 
 // One half of the host-batch double buffer: pinned staging, device copies,
@@ -1298,34 +1299,16 @@ static int retire(RxSlot &sl, WorkerPool *pool) {
 // The registered ring holding every frame of pkts[0, num), so that frame
 // bytes can be read in place (the kernel reads whole 16-byte chunks, so each
 // frame's chunk-rounded end must lie inside the ring too); NULL otherwise.
-// (Large calls check their frames on the worker pool: a serial pass over 4 M
-// descriptors cost a C64 call more than its frame copies.)
-static const RxRing *ring_of(const pptk_rx_ctx *c, const struct ldp_packet *pkts, int num,
-                             WorkerPool *pool) {
+// The registered ring holding the call's first frame, the candidate for
+// reading the frames in place; every chunk checks its own frames against it
+// in its descriptor pass (enqueue_chunk) and is staged instead when one lies
+// outside.  (A serial pass over all frames here, before the first chunk,
+// had cost a 4 M-frame C64 call as much as its frame copies.)
+static const RxRing *ring_of(const pptk_rx_ctx *c, const struct ldp_packet *pkts, int num) {
   if (c->rings.empty() || num <= 0) return nullptr;
   const uint8_t *p0 = (const uint8_t *)pkts[0].data;
-  for (const RxRing &r : c->rings) {
-    if (p0 < r.host || p0 >= r.host + r.bytes) continue;
-    auto inside = [&r, pkts](size_t i0, size_t i1) {
-      for (size_t i = i0; i < i1; ++i) {
-        const uint8_t *p = (const uint8_t *)pkts[i].data;
-        if (!p || p < r.host) return false;
-        const size_t off = (size_t)(p - r.host);
-        if (((off + pkts[i].sz + 15) & ~(size_t)15) > r.bytes) return false;
-      }
-      return true;
-    };
-    constexpr size_t kPart = 1u << 16;
-    if (!pool || (size_t)num < 2 * kPart) return inside(0, (size_t)num) ? &r : nullptr;
-    const size_t parts = ((size_t)num + kPart - 1) / kPart;
-    std::atomic<bool> ok{true};
-    pool->parallel_for(parts, [&](size_t t) {
-      if (ok.load(std::memory_order_relaxed) &&
-          !inside(t * kPart, std::min((size_t)num, (t + 1) * kPart)))
-        ok.store(false, std::memory_order_relaxed);
-    });
-    return ok.load() ? &r : nullptr;
-  }
+  for (const RxRing &r : c->rings)
+    if (p0 >= r.host && p0 < r.host + r.bytes) return &r;
   return nullptr;
 }
 
@@ -1383,6 +1366,8 @@ static int chunk_failed(RxSlot &sl, int rc) {
 // nothing waited for.  retire() waits for it and hands the records to `out`.
 // In a registered ring the kernel reads the frames in place over PCIe (or
 // the span goes down by DMA) and only the 10-byte descriptors are written.
+static size_t chunk_bytes(const pptk_rx_ctx *c);
+
 static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp, size_t cnt,
                          void *out, size_t rec_bytes, const RxRing *ring,
                          const RxRing *rreg, WorkerPool *pool) {
@@ -1403,8 +1388,10 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
   // one part: lengths (+ ring offsets / span) and, for staged chunks, the
   // staging bytes it needs; with `base` given, also the staging offsets
   // and the gather
+  // (write = false: a ring chunk's first pass -- the span, the checks, the
+  // uniformity -- with nothing written; a uniform ring chunk needs no more)
   auto describe = [&sl, cp, ring, maxf, nt, &stage](size_t i0, size_t i1, size_t base,
-                                                    bool gather, PartDesc &d) {
+                                                    bool gather, PartDesc &d, bool write = true) {
     size_t pos = base;
     if (i1 > i0) {
       d.p0 = (const uint8_t *)cp[i0].data;
@@ -1418,10 +1405,15 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
       const uint32_t sz = ok ? pk.sz : 0u;
       d.uni = d.uni && pk.sz == d.sz0 &&
               (const uint8_t *)pk.data == d.p0 + (int64_t)(i - i0) * d.stride;
-      sl.h_len[i] = (uint16_t)sz;
+      if (write) sl.h_len[i] = (uint16_t)sz;
       if (ring) {
-        const uint64_t o = pk.data ? (uint64_t)((const uint8_t *)pk.data - ring->host) : 0u;
-        sl.h_off[i] = o;
+        const uint8_t *pd = (const uint8_t *)pk.data;
+        // (every frame's chunk-rounded end inside the registered region)
+        d.outside = d.outside || (pd && (pd < ring->host ||
+                                         (((size_t)(pd - ring->host) + pk.sz + 15) & ~(size_t)15) >
+                                             ring->bytes));
+        const uint64_t o = pd ? (uint64_t)(pd - ring->host) : 0u;
+        if (write) sl.h_off[i] = o;
         d.lo = std::min<size_t>(d.lo, o);
         // (the frame's chunk-rounded END, clamped to the region: a span
         // copy must not read past the registered memory; the kernel's reads
@@ -1458,12 +1450,35 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
   nparts = std::max<size_t>(1, std::min<size_t>(nparts, std::min<size_t>(8 * pool_size(pool), cnt)));
   std::vector<PartDesc> &parts = sl.parts;
   parts.assign(nparts, PartDesc{});
-  if (nparts == 1) {
+  if (!staged) {
+    // first pass: nothing written; a frame outside the ring stages the
+    // chunk, a uniform chunk needs no descriptors at all
+    auto pass = [&](bool write) {
+      if (nparts == 1)
+        describe(0, cnt, 0, false, parts[0], write);
+      else
+        pool->parallel_for(nparts, [&](size_t t) {
+          parts[t] = PartDesc{};
+          describe(cnt * t / nparts, cnt * (t + 1) / nparts, 0, false, parts[t], write);
+        });
+    };
+    pass(false);
+    bool outside = false, uni = uniform_chunks() && cnt > 1;
+    for (const PartDesc &d : parts) outside = outside || d.outside;
+    if (outside) {   // staged instead (the slot is idle: size its staging)
+      const int rc = ensure_slot(c, sl, std::max<size_t>(c->opts.max_batch, 1), chunk_bytes(c));
+      return rc ? rc : enqueue_chunk(c, sl, cp, cnt, out, rec_bytes, nullptr, rreg, pool);
+    }
+    for (size_t t = 0; t < parts.size() && uni; ++t)
+      uni = parts[t].uni && parts[t].sz0 == parts[0].sz0 && parts[t].stride == parts[0].stride &&
+            parts[t].stride > 0 &&
+            parts[t].p0 == parts[0].p0 + (int64_t)(cnt * t / parts.size()) * parts[0].stride;
+    if (!uni) {
+      for (PartDesc &d : parts) d = PartDesc{};
+      pass(true);
+    }
+  } else if (nparts == 1) {
     describe(0, cnt, 0, staged, parts[0]);
-  } else if (!staged) {
-    pool->parallel_for(nparts, [&](size_t t) {
-      describe(cnt * t / nparts, cnt * (t + 1) / nparts, 0, false, parts[t]);
-    });
   } else {
     if (sl.run_cap < nparts) {
       sl.run.reset(new std::atomic<size_t>[nparts]);
@@ -1609,7 +1624,7 @@ static int host_batch(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int 
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
   WorkerPool *pool = pool_of(c);
-  const RxRing *ring = ring_of(c, pkts, num, pool);
+  const RxRing *ring = ring_of(c, pkts, num);
   const RxRing *rreg = records_region(c, recs, (size_t)num * rec_bytes);
   const size_t chunk = std::max<size_t>(c->opts.max_batch, 1);
   int rc = 0;
@@ -1651,7 +1666,7 @@ static int host_submit(struct pptk_rx_ctx *c, const struct ldp_packet *pkts, int
   if (c->async_n >= PPTK_RX_MAX_INFLIGHT) return -EBUSY;
   DeviceScope dg(c->device);
   if (!dg.ok) return -EIO;
-  const RxRing *ring = ring_of(c, pkts, num, pool_of(c));
+  const RxRing *ring = ring_of(c, pkts, num);
   const RxRing *rreg = records_region(c, recs, (size_t)num * rec_bytes);
   // the slots rotate in submission order (FIFO), so consecutive
   // submissions run on different streams and may overlap on the GPU
