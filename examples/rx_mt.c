@@ -11,10 +11,12 @@
  * Every record is compared with the expected one from the set file, on
  * every lap.  With "pipe", each thread keeps two bursts in flight
  * (pptk_rx_batch_submit, then pptk_rx_batch_complete of the previous burst
- * before its deallocate_some).
+ * before its deallocate_some).  With "rec32" / "pipe32" the same with the
+ * 32-byte compact records (pptk_rx_batch32 / pptk_rx_batch_submit32),
+ * compared with the compact form of the expected records.
  *
  *   gcc -O2 -pthread -Iinclude examples/rx_mt.c -Lpptk_amd -lpptkrx -o rx_mt
- *   ./rx_mt frames.rxq [threads [laps [pipe]]]
+ *   ./rx_mt frames.rxq [threads [laps [pipe|rec32|pipe32]]]
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -28,7 +30,7 @@
 #define BURST 1000 /* ldp/ldprecvmt.c:23: struct ldp_packet pkt_tbl[1000] */
 
 struct rxq_thread {
-  int id, device, laps, pipe;
+  int id, device, laps, pipe, rec32;
   const struct rxq_set *set;
   uint32_t first, count;   /* this thread's queue */
   unsigned long pkts, mismatches;
@@ -42,12 +44,41 @@ static double now(void)
   return tv.tv_sec + tv.tv_usec * 1e-6;
 }
 
-/* records of the burst starting at queue position `head` against the set */
-static void check(struct rxq_thread *t, const struct pptk_rx_rec *recs, uint32_t head, int num)
+/* The compact record of a full one (include/pptk_rx.h: the same values, the
+ * IPv6 addresses left out). */
+static void to_rec32(const struct pptk_rx_rec *r, struct pptk_rx_rec32 *o)
 {
-  for (int i = 0; i < num; i++)
-    if (memcmp(&recs[i], &t->set->want[t->first + head + (uint32_t)i], sizeof(recs[i])) != 0)
+  memset(o, 0, sizeof(*o));
+  o->flow_hash = r->flow_hash;
+  if (!(r->flags & PPTK_RX_F_IPV6)) {
+    memcpy(&o->src4, r->src, 4);
+    memcpy(&o->dst4, r->dst, 4);
+  }
+  o->sport = r->sport;
+  o->dport = r->dport;
+  o->flags = r->flags;
+  o->proto = r->proto;
+  o->l3_off = r->l3_off;
+  o->l4_off = r->l4_off;
+  o->l4_len = r->l4_len;
+  o->src_bucket = r->src_bucket;
+}
+
+/* records of the burst starting at queue position `head` against the set
+ * (recs: struct pptk_rx_rec[], or struct pptk_rx_rec32[] with rec32) */
+static void check(struct rxq_thread *t, const void *recs, uint32_t head, int num)
+{
+  for (int i = 0; i < num; i++) {
+    const struct pptk_rx_rec *w = &t->set->want[t->first + head + (uint32_t)i];
+    if (t->rec32) {
+      struct pptk_rx_rec32 w32;
+      to_rec32(w, &w32);
+      if (memcmp((const struct pptk_rx_rec32 *)recs + i, &w32, sizeof(w32)) != 0)
+        t->mismatches++;
+    } else if (memcmp((const struct pptk_rx_rec *)recs + i, w, sizeof(*w)) != 0) {
       t->mismatches++;
+    }
+  }
   t->pkts += (unsigned long)num;
 }
 
@@ -85,12 +116,17 @@ static void *thrfn(void *arg)
         pkt_tbl[b][i].ancillary = k;
       }
       if (!t->pipe) {
-        if ((t->rc = pptk_rx_batch(ctx, pkt_tbl[b], num, recs[b])) != 0)
+        t->rc = t->rec32 ? pptk_rx_batch32(ctx, pkt_tbl[b], num, (struct pptk_rx_rec32 *)recs[b])
+                         : pptk_rx_batch(ctx, pkt_tbl[b], num, recs[b]);
+        if (t->rc != 0)
           break;
         check(t, recs[b], head, num);
         /* ldp_in_deallocate_some(intf->inq[id], pkt_tbl, num); */
       } else {
-        if ((t->rc = pptk_rx_batch_submit(ctx, pkt_tbl[b], num, recs[b])) != 0)
+        t->rc = t->rec32 ? pptk_rx_batch_submit32(ctx, pkt_tbl[b], num,
+                                                  (struct pptk_rx_rec32 *)recs[b])
+                         : pptk_rx_batch_submit(ctx, pkt_tbl[b], num, recs[b]);
+        if (t->rc != 0)
           break;
         burst_head[b] = head;
         burst_num[b] = num;
@@ -125,7 +161,9 @@ int main(int argc, char **argv)
 {
   struct rxq_set set;
   int nthr = argc > 2 ? atoi(argv[2]) : 4, laps = argc > 3 ? atoi(argv[3]) : 3;
-  int pipe = argc > 4 && strcmp(argv[4], "pipe") == 0;
+  const char *mode = argc > 4 ? argv[4] : "";
+  int pipe = !strcmp(mode, "pipe") || !strcmp(mode, "pipe32");
+  int rec32 = !strcmp(mode, "rec32") || !strcmp(mode, "pipe32");
   int ndev = pptk_rx_device_count();
   unsigned long pkts = 0, bad = 0;
   pthread_t pth[64];
@@ -134,7 +172,7 @@ int main(int argc, char **argv)
   int i, failed = 0;
 
   if (argc < 2 || rxq_load(argv[1], &set) != 0) {
-    fprintf(stderr, "usage: rx_mt frames.rxq [threads [laps [pipe]]]\n");
+    fprintf(stderr, "usage: rx_mt frames.rxq [threads [laps [pipe|rec32|pipe32]]]\n");
     return 1;
   }
   if (nthr < 1 || nthr > 64 || ndev < 1) {
@@ -144,7 +182,7 @@ int main(int argc, char **argv)
   t0 = now();
   for (i = 0; i < nthr; i++) {
     thr[i] = (struct rxq_thread){.id = i, .device = i % ndev, .laps = laps, .pipe = pipe,
-                                  .set = &set};
+                                  .rec32 = rec32, .set = &set};
     thr[i].first = (uint32_t)((uint64_t)set.h.n * (uint64_t)i / (uint64_t)nthr);
     thr[i].count = (uint32_t)((uint64_t)set.h.n * (uint64_t)(i + 1) / (uint64_t)nthr) - thr[i].first;
     pthread_create(&pth[i], NULL, thrfn, &thr[i]);
@@ -160,8 +198,9 @@ int main(int argc, char **argv)
     pkts += thr[i].pkts;
     bad += thr[i].mismatches;
   }
-  printf("rx_mt: %d threads%s, %lu frames, %.3f MPPS, %lu mismatches\n", nthr,
-         pipe ? " (pipelined)" : "", pkts, pkts / (now() - t0) / 1e6, bad);
+  printf("rx_mt: %d threads%s%s, %lu frames, %.3f MPPS, %lu mismatches\n", nthr,
+         pipe ? " (pipelined)" : "", rec32 ? " (32-byte records)" : "", pkts,
+         pkts / (now() - t0) / 1e6, bad);
   rxq_free(&set);
   return failed ? 1 : bad ? 2 : 0;
 }

@@ -78,19 +78,21 @@ def test_rxq_file_layout(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipe", [False, True])
+@pytest.mark.parametrize("mode", ["", "pipe", "rec32", "pipe32"])
 @pytest.mark.parametrize("threads", [1, 4, 8])
-def test_rx_mt_threads_bit_exact(tmp_path, threads, pipe):
+def test_rx_mt_threads_bit_exact(tmp_path, threads, mode):
     """N rx threads, each with its own context and queue, 2 laps, bursts
-    synchronous or two in flight per thread: every record equals the golden
-    record."""
+    synchronous or two in flight per thread, 64- or 32-byte records
+    (pptk_rx_batch32 / _submit32 from a C host): every record equals the
+    golden record (or its compact form)."""
     p = str(tmp_path / "s.rxq")
     n = write_rxq(p)
-    out = subprocess.run([build(tmp_path, "rx_mt"), p, str(threads), "2"] + (["pipe"] if pipe else []),
+    out = subprocess.run([build(tmp_path, "rx_mt"), p, str(threads), "2"] + ([mode] if mode else []),
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    mode = " (pipelined)" if pipe else ""
-    assert f"{threads} threads{mode}, {2 * n} frames" in out.stdout and "0 mismatches" in out.stdout
+    tag = (" (pipelined)" if mode.startswith("pipe") else "") + \
+        (" (32-byte records)" if mode.endswith("32") else "")
+    assert f"{threads} threads{tag}, {2 * n} frames" in out.stdout and "0 mismatches" in out.stdout
 
 
 @pytest.mark.gpu
