@@ -503,6 +503,8 @@ def test_entry_points_reject_bad_arguments(lib):
     assert lib.pptk_rx_ctx_create(ctypes.byref(out), ctypes.byref(bad)) == EINVAL
     assert lib.pptk_rx_batch(None, None, 1, None) == EINVAL
     assert lib.pptk_rx_batch_submit(None, None, 1, None) == EINVAL
+    assert lib.pptk_rx_batch32(None, None, 1, None) == EINVAL
+    assert lib.pptk_rx_batch_submit32(None, None, 1, None) == EINVAL
     assert lib.pptk_rx_batch_complete(None) == EINVAL
     assert lib.pptk_rx_batch_pending(None) == EINVAL
     b = RxDevBatch()
@@ -531,6 +533,8 @@ def test_entry_points_reject_bad_arguments(lib):
     assert lib.pptk_rx_allgather_hash(None, None, 1, None, None) == EINVAL
     assert lib.pptk_rx_stream_split(None, 32, None, None) == EINVAL
     assert lib.pptk_rx_stream_destroy(None) == EINVAL
+    assert lib.pptk_rx_stream_split(None, 0, None, None) == EINVAL
+    assert lib.pptk_rx_stream_split(None, -1, None, None) == EINVAL
     assert lib.pptk_rx_place_records(None, ctypes.byref(b), None, 1, 1, None, None, None) == EINVAL
     assert lib.pptk_rx_place_buffers(None, ctypes.byref(b), None, 1, None, 1, 1, None, None, None,
                                      None) == EINVAL
