@@ -25,7 +25,12 @@ def _full(n_gpus=1):
                              "ring_mpkts": 31.9},
                    "c64": {"mpkts": 448.12, "path": "ring", "frame_gbs": 28.68, "of_pcie": 0.506,
                            "frames": 4194304, "records": "registered", "staged_mpkts": 121.5,
-                           "ring_mpkts": 448.12}}
+                           "ring_mpkts": 448.12},
+                   "c64_rec32": {"mpkts": 776.2, "path": "ring", "frame_gbs": 49.68,
+                                 "of_pcie": 0.878, "frames": 4194304,
+                                 "records": "registered 32 B", "staged_mpkts": 589.16,
+                                 "ring_mpkts": 776.2},
+                   "scrub_wait_s": 0.07, "numa": {"node": 0, "cpus": 128}}
     if n_gpus > 1:
         full["n_gpus"] = n_gpus
         full["config"]["rccl_ranks"] = n_gpus
@@ -56,6 +61,8 @@ def test_line_fits_the_stored_tail_and_carries_every_config():
             assert all(isinstance(e[k], (int, float)) for k in ("mpkts", "kernel_ms", "frac")), cfg
         assert back["configs"]["cmix"]["m6_ms"] == 2.5123
         assert back["e2e"]["c1500"]["mpkts"] == 36.12
+        assert back["e2e"]["c64_rec32"]["of_pcie"] == 0.878   # the compact host path
+        assert "numa" not in back["e2e"] and "scrub_wait_s" not in back["e2e"]
         for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                   "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
                   "roofline", "cpu_baseline"):
