@@ -36,9 +36,11 @@ struct PartDesc {
   size_t bytes = 0, base = 0;
   size_t lo = SIZE_MAX, hi = 0, fbytes = 0;
   uint32_t maxlen = 0;
-  // uniform frames: every frame of the part sz0 bytes, at p0 + k * stride
-  // (k = its index in the part); cleared at the first frame that is not
-  bool uni = true;
+  // uniform frames: every frame of the part sz0 bytes (same), and at
+  // p0 + k * stride (uni; k = its index in the part); each cleared at the
+  // first frame that is not.  A staged chunk needs only `same` (the staging
+  // puts equal frames at one stride), a ring chunk both.
+  bool same = true, uni = true;
   uint32_t sz0 = 0;
   const uint8_t *p0 = nullptr;
   int64_t stride = 0;
@@ -1397,14 +1399,15 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
       d.p0 = (const uint8_t *)cp[i0].data;
       d.sz0 = cp[i0].sz;
       d.stride = i1 - i0 > 1 ? (const uint8_t *)cp[i0 + 1].data - d.p0 : 0;
-      d.uni = d.p0 != nullptr && d.sz0 <= maxf;
+      d.same = d.p0 != nullptr && d.sz0 <= maxf;
+      d.uni = d.same;
     }
     for (size_t i = i0; i < i1; ++i) {
       const struct ldp_packet &pk = cp[i];
       const bool ok = pk.data && pk.sz <= maxf;
       const uint32_t sz = ok ? pk.sz : 0u;
-      d.uni = d.uni && pk.sz == d.sz0 &&
-              (const uint8_t *)pk.data == d.p0 + (int64_t)(i - i0) * d.stride;
+      d.same = d.same && ok && pk.sz == d.sz0;
+      d.uni = d.uni && d.same && (const uint8_t *)pk.data == d.p0 + (int64_t)(i - i0) * d.stride;
       if (write) sl.h_len[i] = (uint16_t)sz;
       if (ring) {
         const uint8_t *pd = (const uint8_t *)pk.data;
@@ -1521,10 +1524,11 @@ static int enqueue_chunk(pptk_rx_ctx *c, RxSlot &sl, const struct ldp_packet *cp
     for (size_t t = 0; t < parts.size() && uni_len; ++t) {
       const PartDesc &d = parts[t];
       const size_t i0 = cnt * t / parts.size();
-      uni_len = d.uni && d.sz0 == f.sz0;
+      uni_len = d.same && d.sz0 == f.sz0;
       // (each part's own stride, and its first frame where the first
       // part's stride puts it; one-frame parts have no stride of their own)
-      uni_ptr = uni_ptr && uni_len && (d.stride == stride || cnt * (t + 1) / parts.size() - i0 == 1) &&
+      uni_ptr = uni_ptr && uni_len && d.uni &&
+                (d.stride == stride || cnt * (t + 1) / parts.size() - i0 == 1) &&
                 d.p0 == f.p0 + (int64_t)i0 * stride;
     }
     if (cnt == 1) uni_ptr = false;
