@@ -401,7 +401,7 @@ static long env_tune() {
   return tune;
 }
 
-static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
+static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather, bool coal = false) {
   constexpr uint32_t rx_bits = kTuneMask & ~(uint32_t)PPTK_RX_TUNE_PERMIT_PASSES;
   if (c->forced_flags >= 0) return (uint32_t)c->forced_flags & rx_bits;
   // (an environment word holding only the rate limiter's bit leaves the
@@ -409,8 +409,11 @@ static uint32_t pick_tune(const pptk_rx_ctx *c, int variant, bool gather) {
   // 0 included, forces the policy it names)
   const long tune = env_tune();
   if (tune >= 0 && tune != PPTK_RX_TUNE_PERMIT_PASSES) return (uint32_t)tune & rx_bits;
+  // (the lane kernel on a packed run of 64-byte slots reads its tiles as
+  // contiguous 1 KB runs, rx_kernel.hip lane_load: there non-temporal loads
+  // pay, C64 0.3815 -> 0.3723 ms; on its per-frame loads they cost 22 %)
   const bool small = variant == RX_T4S1 || variant == RX_T4S2 || variant == RX_T8S2 ||
-                     variant == RX_L4;
+                     (variant == RX_L4 && !coal);
   return (small || gather) ? PPTK_RX_TUNE_NT_STORES
                            : (PPTK_RX_TUNE_NT_STORES | PPTK_RX_TUNE_NT_LOADS);
 }
@@ -536,7 +539,8 @@ extern "C" int pptk_rx_wave_times(uint64_t *host, int max_waves) {
 
 static int launch_batch(pptk_rx_ctx *c, const pptk_rx_dev_batch *b, int variant, void *stream) {
   RxKArgs a = batch_args(c, b);
-  a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm);
+  a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm,
+                     variant == RX_L4 && lane_coalesced(b->stride, b->fixed_len));
   c->last_variant = variant;
   const int grid = grid_for(c, variant, b->n);
   a.phase_ticks = phase_ticks_for(b, variant, grid);

@@ -124,6 +124,16 @@ enum RxVariant {
   RX_NVARIANTS
 };
 
+// The lane kernel reads a batch packed at a 64-byte stride whose frames all
+// span four chunks as contiguous 4 KB tiles (rx_kernel.hip lane_load);
+// PPTK_RX_LANE_COAL=0 builds the per-frame loads only (A/B).
+#ifndef PPTK_RX_LANE_COAL
+#define PPTK_RX_LANE_COAL 1
+#endif
+__host__ __device__ inline bool lane_coalesced(uint64_t stride, uint32_t fixed_len) {
+  return PPTK_RX_LANE_COAL && stride == 64 && ((fixed_len + 15u) >> 4) == 4;
+}
+
 // Length groups of pptk_rx_batch_device_mixed: group g holds the frames with
 // len <= kGroupMaxLen[g] (and above the previous bound) and is streamed by
 // kGroupVariant[g], whose 16*T*S-byte shape covers len + 15 bytes of chunk

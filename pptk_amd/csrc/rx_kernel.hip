@@ -1556,22 +1556,54 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
 // turn, so no in-flight load destination is ever copied).
 constexpr int LSLOT = 80;   // LDS bytes per lane: 64-byte frame image, then the record
 
+// Coalesced tiles (PPTK_RX_LANE_COAL): when the frames are packed at a
+// 64-byte stride and every frame spans four chunks, the tile is one
+// contiguous 4 KB run and load s of lane q takes its chunk 64 s + q (each
+// instruction reads 1 KB contiguously, as the speed-of-light kernel does,
+// instead of 16 bytes of each of 64 frames); the chunks then go through the
+// LDS slots to the lane of their frame (lane_chunks).  With non-temporal
+// loads (the automatic policy for such batches): C64 0.3815 -> 0.3723 ms,
+// compact records 0.3178 -> 0.3151 (in-process A/B, profiles/r06/lane/);
+// with temporal loads it is slower (0.3885), as the per-frame loads are
+// with non-temporal ones (0.4662).
+
 template <bool NT>
 __device__ __forceinline__ void lane_load(const RxKArgs &a, uint64_t tile, int lane, uint32_t nch,
-                                          u32x4 c[4]) {
+                                          bool coal, u32x4 c[4]) {
   uint64_t i = tile * WAVE + lane;
   i = i < a.n ? i : a.n - 1;   // past-the-end lanes re-read the last frame (no record)
   const u32x4 *p = (const u32x4 *)(a.frames + i * a.stride);
+  const u32x4 *t = (const u32x4 *)a.frames;
+  const uint64_t last = 4 * a.n - 1;   // (coalesced: the batch's last chunk)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint64_t k = min(tile * (4 * WAVE) + (uint64_t)(s * WAVE + lane), last);
+    c[s] = ldc<NT>(coal ? t + k : p + min((uint32_t)s, nch ? nch - 1 : 0u));   // past the frame: masked at use
+  }
+}
+
+// The lane's own four chunks from a coalesced tile's loads: chunk 64 s + q
+// belongs to frame 16 s + q / 4, piece q % 4; parked in that frame's LDS slot
+// and read back by its lane.  (The 80-byte slot pitch keeps both the stores
+// and the 16-lane read groups free of bank conflicts.)
+__device__ __forceinline__ void lane_chunks(LDS_AS uint8_t *wimg, int lane, u32x4 c[4]) {
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int s = 0; s < 4; ++s)
-    c[s] = ldc<NT>(p + min((uint32_t)s, nch ? nch - 1 : 0u));   // past the frame: masked at use
+    *(LDS_AS u32x4 *)(wimg + (16 * s + (lane >> 2)) * LSLOT + (lane & 3) * 16) = c[s];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) c[s] = *(const LDS_AS u32x4 *)(wimg + lane * LSLOT + s * 16);
+  __builtin_amdgcn_wave_barrier();
 }
 
 template <bool NT>
 __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int lane, uint32_t nch,
-                                          const u32x4 c[4], LDS_AS uint8_t *wimg) {
+                                          bool coal, const u32x4 cl[4], LDS_AS uint8_t *wimg) {
   const uint64_t i = tile * WAVE + lane;
   LDS_AS uint8_t *slot = wimg + lane * LSLOT;
+  u32x4 c[4] = {cl[0], cl[1], cl[2], cl[3]};
+  if (coal) lane_chunks(wimg, lane, c);
   if (i < a.n && !(kDiag && (a.tune & 16u))) {
     const uint32_t len = a.fixed_len;
     uint32_t d[16];
@@ -1610,12 +1642,14 @@ __global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
   const uint64_t step = (uint64_t)gridDim.x * WPB;
   const uint32_t nch = (a.fixed_len + 15u) >> 4;   // 1..4, uniform
+  // (uniform: the batch is one contiguous run of 64-byte frame slots)
+  const bool coal = lane_coalesced(a.stride, a.fixed_len);
   uint64_t tile = (uint64_t)blockIdx.x * WPB + wv;
   u32x4 c0[4], c1[4];
-  lane_load<NT>(a, tile, lane, nch, c0);
+  lane_load<NT>(a, tile, lane, nch, coal, c0);
   while (tile < ntiles) {
-    lane_load<NT>(a, tile + step, lane, nch, c1);
-    lane_tile<NT>(a, tile, lane, nch, c0, wimg);
+    lane_load<NT>(a, tile + step, lane, nch, coal, c1);
+    lane_tile<NT>(a, tile, lane, nch, coal, c0, wimg);
     tile += step;
 #pragma unroll
     for (int s = 0; s < 4; ++s) c0[s] = c1[s];

@@ -669,6 +669,17 @@ def test_lane_kernel_large_batch(dev):
         assert (ctx.last_variant() == RX_L4) == lane
         d = diff_records(got.cpu().numpy().reshape(-1), want)
         assert not d, f"shift {shift}: {d}"
+    # the coalesced tile loads (64-byte stride, four chunks per frame) under
+    # every memory policy: temporal / non-temporal loads and stores
+    big[:buf.size] = torch.from_numpy(buf).to(dev)   # (the shifted runs moved it)
+    for flags in (0x0, 0x1, 0x20, 0x21):
+        ctx.set_tuning(RX_L4, flags)
+        got = ctx.batch_device(big, n, stride=64, fixed_len=64)
+        torch.cuda.synchronize()
+        assert ctx.last_variant() == RX_L4
+        d = diff_records(got.cpu().numpy().reshape(-1), want)
+        assert not d, f"flags {flags:#x}: {d}"
+    ctx.set_tuning(-1, -1)
 
 
 @pytest.mark.parametrize("cfg", ["c64", "c1500"])
