@@ -425,9 +425,25 @@ static int forced_variant(const pptk_rx_ctx *c) {
   return force >= 0 && force < RX_NVARIANTS ? (int)force : -1;
 }
 
-static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n) {
+// Blocks a launch may keep resident (the persistent grid).
+static uint64_t resident_blocks(const pptk_rx_ctx *c, int variant);
+
+// Grid of a launch: by default persistent (every block resident, its waves
+// striding over the tiles).  tpw > 0: enough blocks that each wave takes
+// about tpw tiles -- more than are resident, so the dispatcher hands out
+// the later blocks as earlier ones finish (tiles_per_wave).
+static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n, uint32_t tpw = 0) {
   const uint64_t ntiles = (n + 63) / 64;
   const uint64_t want_blocks = (ntiles + 3) / 4;
+  if (tpw > 0) {
+    const uint64_t blocks = (ntiles + 4ull * tpw - 1) / (4ull * tpw);
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks,
+                                                         std::max(blocks, resident_blocks(c, variant))));
+  }
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, resident_blocks(c, variant)));
+}
+
+static uint64_t resident_blocks(const pptk_rx_ctx *c, int variant) {
   static const long grid_mult = std::max(1l, EXP_KNOB("PPTK_RX_GRID_MULT", 1));
   // the CUs pptk_rx_stream_split left to the collective (the batches'
   // stream cannot use them); PPTK_RX_RESERVE_CUS: that many CUs' worth of
@@ -436,8 +452,29 @@ static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n) {
   static const int reserve_knob = (int)std::max(0l, EXP_KNOB("PPTK_RX_RESERVE_CUS", 0));
   const int reserve = std::max(reserve_knob, c->coll_cus);
   const uint64_t ncu = (uint64_t)std::max(1, c->ncu - std::min(reserve, c->ncu - 1));
-  const uint64_t cap = ncu * (uint64_t)c->bpc[variant] * (uint64_t)grid_mult;
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks, cap));
+  // (PPTK_RX_BPC: resident blocks per CU for every variant, A/B only)
+  static const long bpc_knob = EXP_KNOB("PPTK_RX_BPC", 0);
+  const uint64_t bpc = bpc_knob > 0 ? (uint64_t)bpc_knob : (uint64_t)c->bpc[variant];
+  return ncu * bpc * (uint64_t)grid_mult;
+}
+
+// Tiles per wave of an oversubscribed grid (grid_for), 0 = persistent.  The
+// lane kernel, and the streaming shapes on offset-described batches (tiles
+// of uneven duration), run faster when the dispatcher hands out blocks of a
+// few tiles per wave than when every wave owns a fixed share of the batch:
+// in-process A/B (profiles/r06/grid/), C64 0.3764 -> 0.3580 ms (8 tiles)
+// and 0.3972 -> 0.3615 (4), CMIX T16S6 2.5245 -> 2.4591 (8) and 2.5189 ->
+// 2.4509 (4), M6 on CMIX 2.5563 -> 2.4439 and on IMIX 1.3977 -> 1.3385 (8);
+// C1500 (fixed stride, T32S3) is unchanged and T16S6 on it is slower
+// (4.1465 -> 4.3680), so fixed-stride streaming stays persistent, as does
+// the jumbo shape T64S2 (JMIX 3.9191 -> 4.0169 with 4 tiles, equal with 8).
+static uint32_t tiles_per_wave(int variant, bool gather) {
+  static const long lane = EXP_KNOB("PPTK_RX_LANE_TPW", 4);
+  static const long strm = EXP_KNOB("PPTK_RX_GATHER_TPW", 8);
+  static const long jumbo = EXP_KNOB("PPTK_RX_JUMBO_TPW", 0);   // T64S2 (A/B)
+  if (variant == RX_L4) return (uint32_t)std::max(0l, lane);
+  if (!gather) return 0;
+  return (uint32_t)std::max(0l, variant == RX_T64S2 ? jumbo : strm);
 }
 
 static uint64_t gcd64(uint64_t a, uint64_t b) {
@@ -542,8 +579,11 @@ static int launch_batch(pptk_rx_ctx *c, const pptk_rx_dev_batch *b, int variant,
   a.tune = pick_tune(c, variant, b->d_off || b->d_len || b->d_perm,
                      variant == RX_L4 && lane_coalesced(b->stride, b->fixed_len));
   c->last_variant = variant;
-  const int grid = grid_for(c, variant, b->n);
-  a.phase_ticks = phase_ticks_for(b, variant, grid);
+  const bool gather = b->d_off || b->d_len || b->d_perm;
+  const int grid = grid_for(c, variant, b->n, tiles_per_wave(variant, gather));
+  // (the period follows the waves resident at once, not the whole grid)
+  a.phase_ticks = phase_ticks_for(
+      b, variant, (int)std::min<uint64_t>((uint64_t)grid, resident_blocks(c, variant)));
 #ifdef PPTK_RX_WAVE_TIMES
   if (!g_wave_times && hipMalloc(&g_wave_times, (size_t)65536 * 16) != hipSuccess) return -ENOMEM;
   if (grid * 4 > 65536) return -EINVAL;
