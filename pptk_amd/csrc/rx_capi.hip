@@ -434,9 +434,10 @@ static uint64_t resident_blocks(const pptk_rx_ctx *c, int variant);
 // the later blocks as earlier ones finish (tiles_per_wave).
 static int grid_for(const pptk_rx_ctx *c, int variant, uint64_t n, uint32_t tpw = 0) {
   const uint64_t ntiles = (n + 63) / 64;
-  const uint64_t want_blocks = (ntiles + 3) / 4;
+  const uint64_t want_blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
   if (tpw > 0) {
-    const uint64_t blocks = (ntiles + 4ull * tpw - 1) / (4ull * tpw);
+    const uint64_t per_block = (uint64_t)kWavesPerBlock * tpw;
+    const uint64_t blocks = (ntiles + per_block - 1) / per_block;
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(want_blocks,
                                                          std::max(blocks, resident_blocks(c, variant))));
   }
@@ -554,7 +555,7 @@ static uint32_t phase_ticks_for(const pptk_rx_dev_batch *b, int variant, int gri
   const uint64_t tile_bytes =
       64 * (b->d_off ? std::max<uint64_t>(64, maxlen / 2)
                      : std::min<uint64_t>(std::max<uint64_t>(b->stride, 64), 1u << 20));
-  const uint64_t waves = (uint64_t)grid * 4;
+  const uint64_t waves = (uint64_t)grid * kWavesPerBlock;
   const uint64_t ticks = tile_bytes * waves * 3 / 4 / 55000;   // 5.5 TB/s = 55 000 B per tick
   return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ticks, 100), 1000000);
 }
@@ -586,9 +587,9 @@ static int launch_batch(pptk_rx_ctx *c, const pptk_rx_dev_batch *b, int variant,
       b, variant, (int)std::min<uint64_t>((uint64_t)grid, resident_blocks(c, variant)));
 #ifdef PPTK_RX_WAVE_TIMES
   if (!g_wave_times && hipMalloc(&g_wave_times, (size_t)65536 * 16) != hipSuccess) return -ENOMEM;
-  if (grid * 4 > 65536) return -EINVAL;
+  if (grid * kWavesPerBlock > 65536) return -EINVAL;
   a.wave_times = g_wave_times;
-  g_wave_count = grid * 4;
+  g_wave_count = grid * kWavesPerBlock;
 #endif
   return hip_err(launch_rx(variant, a, grid, (hipStream_t)stream));
 }

@@ -124,6 +124,13 @@ enum RxVariant {
   RX_NVARIANTS
 };
 
+// Wavefronts per block of the receive kernels (every wave works on its own
+// tiles; no block-wide barrier).  PPTK_RX_WPB builds another size (A/B).
+#ifndef PPTK_RX_WPB
+#define PPTK_RX_WPB 4
+#endif
+constexpr int kWavesPerBlock = PPTK_RX_WPB;
+
 // The lane kernel reads a batch packed at a 64-byte stride whose frames all
 // span four chunks as contiguous 4 KB tiles (rx_kernel.hip lane_load);
 // PPTK_RX_LANE_COAL=0 builds the per-frame loads only (A/B).

@@ -36,7 +36,7 @@ namespace pptk {
 namespace {
 
 constexpr int WAVE = 64;
-constexpr int WPB = 4;            // waves per block (256 threads)
+constexpr int WPB = kWavesPerBlock;   // waves per block (4: 256 threads)
 constexpr int IMG_CHUNKS = 8;     // 16-byte chunks parked in LDS per frame
 #ifndef PPTK_RX_IMG_STRIDE
 #define PPTK_RX_IMG_STRIDE 144
