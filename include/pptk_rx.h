@@ -580,9 +580,11 @@ int pptk_rx_allgather_hash(struct pptk_rx_ctx *ctx, const uint64_t *d_hash, uint
  * gather that overlaps them (no reference counterpart: the reference has no
  * device; this belongs with the collective above).  RCCL's all-gather
  * kernel needs a whole CU per block on gfx950 (512 threads, 37 KB of LDS,
- * 248 VGPRs), and the persistent receive grid fills every CU, so at each
- * batch boundary one kernel takes CUs the other was sized for and the two
- * run one after the other.  *coll_stream (for
+ * 248 VGPRs), and the receive grid fills every CU (persistent for
+ * fixed-stride batches, oversubscribed for offset-described ones and the
+ * small-frame kernel), so at each batch boundary one kernel takes CUs the
+ * other was sized for and the two run one after the other (DESIGN.md
+ * section 8).  *coll_stream (for
  * pptk_rx_allgather_hash) may use `coll_cus` CUs -- the same number in
  * every shader engine of every XCC -- and *rx_stream (for the batches) the
  * rest; the context sizes its receive grids for the rest from now on, on
