@@ -459,6 +459,12 @@ static uint64_t resident_blocks(const pptk_rx_ctx *c, int variant) {
   return ncu * bpc * (uint64_t)grid_mult;
 }
 
+// An oversubscribed launch's grid with its tail region (RxKArgs::tail_block):
+// the last PPTK_RX_TAIL_PCT % of the tiles in blocks of PPTK_RX_TAIL_TPW
+// tiles per wave, dispatched last, so that the launch does not end on a few
+// long blocks (A/B knobs; 0 % = one region).
+static int plan_grid(const pptk_rx_ctx *c, int variant, uint64_t n, uint32_t tpw, RxKArgs &a);
+
 // Tiles per wave of an oversubscribed grid (grid_for), 0 = persistent.  The
 // lane kernel, and the streaming shapes on offset-described batches (tiles
 // of uneven duration), run faster when the dispatcher hands out blocks of a
@@ -476,6 +482,24 @@ static uint32_t tiles_per_wave(int variant, bool gather) {
   if (variant == RX_L4) return (uint32_t)std::max(0l, lane);
   if (!gather) return 0;
   return (uint32_t)std::max(0l, variant == RX_T64S2 ? jumbo : strm);
+}
+
+static int plan_grid(const pptk_rx_ctx *c, int variant, uint64_t n, uint32_t tpw, RxKArgs &a) {
+  a.tail_block = 0;
+  a.tail_tile = 0;
+  const int grid = grid_for(c, variant, n, tpw);
+  static const long pct = EXP_KNOB("PPTK_RX_TAIL_PCT", 0);
+  static const long ttpw = EXP_KNOB("PPTK_RX_TAIL_TPW", 1);
+  if (tpw == 0 || pct <= 0 || pct >= 100 || ttpw <= 0) return grid;
+  const uint64_t ntiles = (n + 63) / 64;
+  const uint64_t t2 = ntiles * (uint64_t)pct / 100, t1 = ntiles - t2;
+  const uint64_t w1 = (uint64_t)kWavesPerBlock * tpw, w2 = (uint64_t)kWavesPerBlock * (uint64_t)ttpw;
+  const uint64_t b1 = (t1 + w1 - 1) / w1, b2 = (t2 + w2 - 1) / w2;
+  // (a batch too small to fill the chip twice over keeps one region)
+  if (t2 == 0 || b1 < 2 * resident_blocks(c, variant) || b1 + b2 > 0x7fffffffull) return grid;
+  a.tail_block = (uint32_t)b1;
+  a.tail_tile = t1;
+  return (int)(b1 + b2);
 }
 
 static uint64_t gcd64(uint64_t a, uint64_t b) {
@@ -581,7 +605,7 @@ static int launch_batch(pptk_rx_ctx *c, const pptk_rx_dev_batch *b, int variant,
                      variant == RX_L4 && lane_coalesced(b->stride, b->fixed_len));
   c->last_variant = variant;
   const bool gather = b->d_off || b->d_len || b->d_perm;
-  const int grid = grid_for(c, variant, b->n, tiles_per_wave(variant, gather));
+  const int grid = plan_grid(c, variant, b->n, tiles_per_wave(variant, gather), a);
   // (the period follows the waves resident at once, not the whole grid)
   a.phase_ticks = phase_ticks_for(
       b, variant, (int)std::min<uint64_t>((uint64_t)grid, resident_blocks(c, variant)));

@@ -106,6 +106,11 @@ struct RxKArgs {
   // global write phases of the streaming shapes (rx_kernel.hip): the period
   // in s_memrealtime ticks (10 ns); 0 = each tile's records at its end
   uint32_t phase_ticks;
+  // oversubscribed grids (rx_capi.hip grid_for): blocks from tail_block on
+  // (0: none) take the tiles from tail_tile on, in fewer tiles per wave, so
+  // that the launch's last blocks are short
+  uint32_t tail_block;
+  uint64_t tail_tile;
 #ifdef PPTK_RX_WAVE_TIMES
   uint64_t *wave_times;   // probe build: per wave (start, end) of the last launch
 #endif

@@ -987,6 +987,32 @@ __device__ __forceinline__ void flush_stash(const RxKArgs &a, const LDS_AS u32x4
   }
 }
 
+// The tiles of wave `wv` of this block: first, first + step, ... below end.
+// Strided over the grid by default; with a tail region (RxKArgs::tail_block)
+// the blocks before it stride over the tiles before tail_tile and the ones
+// from it on over the rest; with tune bit 8 (experiment) a contiguous run.
+struct TileRange {
+  uint64_t first, step, end;
+};
+__device__ __forceinline__ TileRange wave_tiles(const RxKArgs &a, uint64_t ntiles, int wv) {
+  const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
+  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+  if (a.tune & 256u) {
+    const uint64_t per = (ntiles + nwaves - 1) / nwaves;
+    return {wid * per, 1, min(ntiles, (wid + 1) * per)};
+  }
+  if (a.tail_block == 0) return {wid, nwaves, ntiles};
+  if (blockIdx.x < a.tail_block) return {wid, (uint64_t)a.tail_block * WPB, min(a.tail_tile, ntiles)};
+  return {a.tail_tile + (uint64_t)(blockIdx.x - a.tail_block) * WPB + wv,
+          (uint64_t)(gridDim.x - a.tail_block) * WPB, ntiles};
+}
+// A tile to prefetch descriptors or frames for: past the wave's range it
+// is no tile (ntiles: past-the-end lanes, which read frame 0 / the batch's
+// last chunk from cache), not a tile of another region.
+__device__ __forceinline__ uint64_t pf_tile(const TileRange &r, uint64_t ntiles, uint64_t t) {
+  return t < r.end ? t : ntiles;
+}
+
 // Waves per SIMD the register allocator must leave room for: the streaming
 // variants keep D = 3 rounds of S chunks in registers (D * S * 4 VGPRs) and
 // need 2 waves/SIMD; the small-frame variants 4.
@@ -1060,23 +1086,20 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
   LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * IMG_STRIDE;
   LDS_AS u32x4 *stash = (LDS_AS u32x4 *)stash_lds + (PHASED ? wv * 4 * WAVE : 0);
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
-  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
-  // Tile order: strided over the grid (default), or, with tune bit 8
-  // (experiment), a contiguous block of tiles per wave, so that one wave's
-  // successive record flushes are adjacent in memory.
-  const bool blocked = a.tune & 256u;
-  const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
-  const uint64_t per = (ntiles + nwaves - 1) / nwaves;
-  const uint64_t step = blocked ? 1 : nwaves;
-  const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
+  // Tile order (wave_tiles): strided over the grid (default), or, with tune
+  // bit 8 (experiment), a contiguous block of tiles per wave, so that one
+  // wave's successive record flushes are adjacent in memory.
+  const TileRange tr = wave_tiles(a, ntiles, wv);
+  const uint64_t step = tr.step, tend = tr.end;
 
-  uint64_t tile = blocked ? wid * per : wid;
+  uint64_t tile = tr.first;
 #ifdef PPTK_RX_WAVE_TIMES
+  const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
   const uint64_t wt_start = __builtin_amdgcn_s_memrealtime();
 #endif
-  Desc dc = load_desc<GATHER>(a, tile, lane);
-  Desc dn = load_desc<GATHER>(a, tile + step, lane);
-  uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * step, lane);
+  Desc dc = load_desc<GATHER>(a, pf_tile(tr, ntiles, tile), lane);
+  Desc dn = load_desc<GATHER>(a, pf_tile(tr, ntiles, tile + step), lane);
+  uint32_t idx2 = desc_idx<GATHER>(a, pf_tile(tr, ntiles, tile + 2 * step), lane);
   // prologue: the first D rounds of the first tile, in slots 0 .. D-1
   Buf<S> b[D + 1];
   // (issued strictly in slot order: the loop-header wait is computed from
@@ -1094,7 +1117,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // to drain the chunk loads in flight: the index (perm) of tile + 3 nwaves
     // is loaded here, the dependent offset/length of tile + 2 nwaves (whose
     // index arrived during the previous tile) before the last round group.
-    const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
+    const uint32_t idx3 = desc_idx<GATHER>(a, pf_tile(tr, ntiles, tile + 3 * step), lane);
     // ---- streaming rounds: team g sums frame g*T + r over [team_start, len).
     // Fixed-slot ring of D + 1 rounds: round r lives in slot r % (D + 1); a
     // group of D + 1 rounds is unrolled so every slot index is a constant and
@@ -1189,7 +1212,7 @@ __global__ __launch_bounds__(WAVE * WPB, (min_waves<T, S, D>())) void rx_kernel(
     // the descriptors two tiles ahead are loaded BEFORE the last group issues
     // the next tile's first D rounds: the copies dc <- dn <- d2 at the tile
     // boundary then wait only for these loads, not for the rounds in flight
-    const Desc d2 = desc_fill<GATHER>(a, idx2, tile + 2 * step, lane);
+    const Desc d2 = desc_fill<GATHER>(a, idx2, pf_tile(tr, ntiles, tile + 2 * step), lane);
     __builtin_amdgcn_sched_barrier(0);
     group(T - (D + 1));
 
@@ -1415,17 +1438,13 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
   LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * IMG_STRIDE;
   LDS_AS uint8_t *lst[2] = {(LDS_AS uint8_t *)lists[wv][0], (LDS_AS uint8_t *)lists[wv][1]};
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
-  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
-  const bool blocked = a.tune & 256u;
-  const uint64_t wid = (uint64_t)blockIdx.x * WPB + wv;
-  const uint64_t per = (ntiles + nwaves - 1) / nwaves;
-  const uint64_t step = blocked ? 1 : nwaves;
-  const uint64_t tend = blocked ? min(ntiles, (wid + 1) * per) : ntiles;
+  const TileRange tr = wave_tiles(a, ntiles, wv);
+  const uint64_t step = tr.step, tend = tr.end;
 
-  uint64_t tile = blocked ? wid * per : wid;
-  Desc dc = load_desc<GATHER>(a, tile, lane);
-  Desc dn = load_desc<GATHER>(a, tile + step, lane);
-  uint32_t idx2 = desc_idx<GATHER>(a, tile + 2 * step, lane);
+  uint64_t tile = tr.first;
+  Desc dc = load_desc<GATHER>(a, pf_tile(tr, ntiles, tile), lane);
+  Desc dn = load_desc<GATHER>(a, pf_tile(tr, ntiles, tile + step), lane);
+  uint32_t idx2 = desc_idx<GATHER>(a, pf_tile(tr, ntiles, tile + 2 * step), lane);
   int cur = 0;
   MSched sc = m_schedule(dc, lane, lst[0]);
   MBuf b[M_D + 1];
@@ -1436,7 +1455,7 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
   }
 
   while (tile < tend) {
-    const uint32_t idx3 = desc_idx<GATHER>(a, tile + 3 * step, lane);
+    const uint32_t idx3 = desc_idx<GATHER>(a, pf_tile(tr, ntiles, tile + 3 * step), lane);
     // the next tile's schedule, into the other list (the previous tile's,
     // whose rounds are all consumed)
     const MSched sn = m_schedule(dn, lane, lst[cur ^ 1]);
@@ -1508,7 +1527,7 @@ __global__ __launch_bounds__(WAVE * WPB, PPTK_RX_M_WAVES) void rx_kernel_mixed(R
       group(r0, std::false_type{});
       r0 += M_D + 1;
     } while (r0 < P - (M_D + 1));
-    const Desc d2 = desc_fill<GATHER>(a, idx2, tile + 2 * step, lane);
+    const Desc d2 = desc_fill<GATHER>(a, idx2, pf_tile(tr, ntiles, tile + 2 * step), lane);
     __builtin_amdgcn_sched_barrier(0);
     group(P - (M_D + 1), std::true_type{});
 
@@ -1640,15 +1659,16 @@ __global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
   const int wv = threadIdx.x / WAVE;
   LDS_AS uint8_t *wimg = (LDS_AS uint8_t *)lds + wv * WAVE * LSLOT;
   const uint64_t ntiles = (a.n + WAVE - 1) / WAVE;
-  const uint64_t step = (uint64_t)gridDim.x * WPB;
+  const TileRange tr = wave_tiles(a, ntiles, wv);
+  const uint64_t step = tr.step;
   const uint32_t nch = (a.fixed_len + 15u) >> 4;   // 1..4, uniform
   // (uniform: the batch is one contiguous run of 64-byte frame slots)
   const bool coal = lane_coalesced(a.stride, a.fixed_len);
-  uint64_t tile = (uint64_t)blockIdx.x * WPB + wv;
+  uint64_t tile = tr.first;
   u32x4 c0[4], c1[4];
-  lane_load<NT>(a, tile, lane, nch, coal, c0);
-  while (tile < ntiles) {
-    lane_load<NT>(a, tile + step, lane, nch, coal, c1);
+  lane_load<NT>(a, pf_tile(tr, ntiles, tile), lane, nch, coal, c0);
+  while (tile < tr.end) {
+    lane_load<NT>(a, pf_tile(tr, ntiles, tile + step), lane, nch, coal, c1);
     lane_tile<NT>(a, tile, lane, nch, coal, c0, wimg);
     tile += step;
 #pragma unroll

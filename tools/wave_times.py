@@ -1,4 +1,5 @@
-"""PROBE TOOLING: when does each wave of the persistent rx grid finish?
+"""PROBE TOOLING: when does each wave of the rx grid (persistent or
+oversubscribed) start and finish?
 Needs the probe build (`make abvariant NAME=wt DEFS=-DPPTK_RX_WAVE_TIMES`,
 copied to tools/ab_libs/wt.so, run with PPTK_RX_LIB=tools/ab_libs/wt.so):
 every wave writes its start and end clock (s_memrealtime, 100 MHz).  For
@@ -51,7 +52,17 @@ def main():
             t0 = t[:, 0].min()
             st, en = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0     # us
             grp = (np.arange(nw) // 4) % 8
+            # concurrency over time: how many waves run at once, and how
+            # long the launch runs with fewer than 90 % of the peak
+            ev = np.concatenate([np.stack([st, np.ones(nw)], 1), np.stack([en, -np.ones(nw)], 1)])
+            ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+            act = np.cumsum(ev[:, 1])
+            peak = float(act.max())
+            hi = ev[act >= 0.9 * peak, 0]
             out.append({
+                "waves": int(nw), "peak_active": peak,
+                "util": float((en - st).sum() / (peak * en.max())),
+                "tail_below90_us": float(en.max() - hi.max()) if len(hi) else None,
                 "span_us": float(en.max()), "start_spread_us": float(st.max()),
                 "end_pct_us": {p: float(np.percentile(en, p)) for p in (0, 10, 50, 90, 99, 100)},
                 "tail_frac": float((en.max() - np.median(en)) / en.max()),
