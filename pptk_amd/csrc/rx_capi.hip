@@ -479,8 +479,9 @@ static uint32_t tiles_per_wave(int variant, bool gather) {
   static const long lane = EXP_KNOB("PPTK_RX_LANE_TPW", 4);
   static const long strm = EXP_KNOB("PPTK_RX_GATHER_TPW", 8);
   static const long jumbo = EXP_KNOB("PPTK_RX_JUMBO_TPW", 0);   // T64S2 (A/B)
+  static const long fixed = EXP_KNOB("PPTK_RX_FIXED_TPW", 0);   // fixed stride (A/B)
   if (variant == RX_L4) return (uint32_t)std::max(0l, lane);
-  if (!gather) return 0;
+  if (!gather) return (uint32_t)std::max(0l, fixed);
   return (uint32_t)std::max(0l, variant == RX_T64S2 ? jumbo : strm);
 }
 
