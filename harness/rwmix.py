@@ -47,7 +47,11 @@ def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
     actual span after its descriptors -- and writing wb record bytes per
     tile; the non-temporal shapes also with the rx kernel's global write
     phases (period ~0.75 of a tile's duration at 5.5 TB/s, as
-    rx_capi.hip phase_ticks_for sets it).  Returns (ms, setting)."""
+    rx_capi.hip phase_ticks_for sets it).  The grids go past what fits at
+    once (32 and 128 blocks per CU: ~8 and ~2 tiles per wave for 16 M
+    frames), as the rx kernels' oversubscribed grids do (DESIGN.md §7
+    "Round 6: grids"); their phase period follows the 8 blocks per CU that
+    are resident.  Returns (ms, setting)."""
     import torch
     L = _lib()
     dev = inp.device
@@ -69,8 +73,8 @@ def sol_ms(inp, n, out, wb, rb=0, off=None, lens=None, reps=6):
     for mode in (0, 1, 4, 5, 9, 13):
         m = (mode & 7) | (2 if gather else 0)
         phased = bool(mode & 8)
-        for mult in (2, 4, 8):
-            period = max(100, int(tile_bytes * ncu * mult * 4 * 3 / 4 / 55000))
+        for mult in (2, 4, 8, 32, 128):
+            period = max(100, int(tile_bytes * ncu * min(mult, 8) * 4 * 3 / 4 / 55000))
             ts = []
             for k in range(reps + 2):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
