@@ -848,6 +848,56 @@ def test_mixed_shape_kernel_full_size(cfg, dev):
     ctx.close()
 
 
+@pytest.mark.parametrize("cfg", ["c64", "cmix", "imix"])
+def test_full_size_windows_vs_oracle(cfg, oracle_lib, dev):
+    """BASELINE sizes (16 M frames) on the product's own choices -- the lane
+    kernel's coalesced tiles at 4 tiles per wave (C64), the streaming shapes
+    and M6 on the oversubscribed grid at 8 (CMIX, IMIX) -- checked bit-exact
+    against the CPU oracle on 24 windows of 2 048 consecutive frames spread
+    over the batch (first, last and random tiles), records and compact
+    records."""
+    from oracle.oracle import make_opts
+    from pptk_amd.rx import RxContext
+    from harness.synth import make_batch
+    n = 1 << 24
+    b = make_batch(cfg, n, dev)
+    key = bytes(range(1, 17))
+    ctx = RxContext(0, key)
+    fixed = "off" not in b
+    kw = (dict(stride=b["stride"], fixed_len=b["fixed_len"]) if fixed else
+          dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]))
+    got = ctx.batch_device(b["frames"], n, **kw)
+    got32 = ctx.batch_device(b["frames"], n, compact=True, **kw)
+    torch.cuda.synchronize()
+    w = 2048
+    rng = np.random.default_rng(11)
+    starts = sorted({0, n - w, *(int(x) * 64 for x in rng.integers(0, (n - w) // 64, 22))})
+    if fixed:
+        off_all = None
+    else:
+        off_all = b["off"].cpu().numpy().view(np.uint64)
+        len_all = b["lens"].cpu().numpy().view(np.uint16)
+    opts = make_opts(key)
+    for s0 in starts:
+        if fixed:
+            lo, hi = s0 * b["stride"], (s0 + w) * b["stride"]
+            off = np.arange(w, dtype=np.uint64) * np.uint64(b["stride"])
+            lens = np.full(w, b["fixed_len"], np.uint16)
+        else:
+            lo = int(off_all[s0]) & ~15
+            hi = int(off_all[s0 + w - 1]) + int(len_all[s0 + w - 1])
+            off = off_all[s0:s0 + w] - np.uint64(lo)
+            lens = len_all[s0:s0 + w]
+        host = b["frames"][lo:hi + 16].cpu().numpy()
+        want = oracle_lib.rx_batch(host, off, lens, opts=opts, nthreads=8)
+        d = diff_records(got[s0:s0 + w].cpu().numpy().reshape(-1), want)
+        assert not d, f"{cfg} frames {s0}..{s0 + w}: {d}"
+        d = diff_records(got32[s0:s0 + w].cpu().numpy().reshape(-1), to_rec32(want),
+                         dtype=REC32_DTYPE)
+        assert not d, f"{cfg} compact, frames {s0}..{s0 + w}: {d}"
+    ctx.close()
+
+
 @pytest.mark.parametrize("layout", ["fixed", "offsets"])
 def test_autotune_keeps_records(layout, dev):
     """pptk_rx_autotune picks one of the interchangeable shapes for a
