@@ -433,6 +433,57 @@ def test_permit_keys_two_contexts_two_streams_at_once(dev):
     assert took < 1.5, took
 
 
+def test_permit_beside_oversubscribed_batches(dev):
+    """The rate limiter on one stream while another context's receive
+    batches run on another: offset-described (CMIX) and C64 batches launch
+    more blocks than fit (rx_capi.hip grid_for), so the dispatcher hands CUs
+    back and forth between the two kernels instead of one waiting for the
+    other to end.  The fused launch needs all its workgroups resident at
+    once; it must still get them well inside its 2 s bound: no abort
+    (status 0), verdicts and tokens equal to the frame-by-frame semantics,
+    and the batches' records equal to the same batches run alone."""
+    import time
+    from pptk_amd.rx import RxContext
+    from harness.synth import make_batch
+    n, hs, reps = 1 << 22, 1 << 16, 6
+    k, tok_h, keys_h = _keys_case(n, hs, 93)
+    want_v, t = [], tok_h
+    for _ in range(reps):
+        v, t = _np_permit(k, hs, t)
+        want_v.append(v)
+    pctx = _ctx({"key": np.arange(1, 17, dtype=np.uint8), "iphash": np.array([24, 48, hs])})
+    rctx = RxContext(0, bytes(range(1, 17)))
+    batches = [make_batch(cfg, 1 << 22, dev) for cfg in ("cmix", "c64")]
+    kws = [dict(off=b["off"], lens=b["lens"], max_len=b["max_len"]) if "off" in b else
+           dict(stride=b["stride"], fixed_len=b["fixed_len"]) for b in batches]
+    alone = [rctx.batch_device(b["frames"], 1 << 22, **kw) for b, kw in zip(batches, kws)]
+    torch.cuda.synchronize()
+    s_rx, s_pm = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    keys = torch.from_numpy(keys_h.view(np.int32)).to(dev)
+    tok = torch.from_numpy(tok_h.view(np.int32).copy()).to(dev)
+    scratch = torch.empty(pctx._L.pptk_rx_permit_scratch_bytes(n, hs), dtype=torch.uint8,
+                          device=dev)
+    verdicts = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(reps)]
+    outs = [[torch.empty_like(a) for a in alone] for _ in range(reps)]
+    torch.cuda.synchronize()
+    t0 = time.monotonic()
+    for r in range(reps):
+        for b, kw, o in zip(batches, kws, outs[r]):
+            rctx.batch_device(b["frames"], 1 << 22, recs=o, stream=s_rx, **kw)
+        pctx.permit_keys_device(keys, 4, tok, verdict=verdicts[r], scratch=scratch, stream=s_pm)
+    torch.cuda.synchronize()
+    took = time.monotonic() - t0
+    assert pctx.permit_status(scratch, stream=s_pm) == 0
+    for r in range(reps):
+        assert np.array_equal(verdicts[r].cpu().numpy(), want_v[r]), r
+        for a, o in zip(alone, outs[r]):
+            assert torch.equal(a, o), r
+    assert np.array_equal(tok.cpu().numpy().view(np.uint32), t)
+    assert took < 1.5, took
+    rctx.close()
+    pctx.close()
+
+
 @pytest.mark.parametrize("stall_at", [1, 2])
 def test_permit_fused_abort_leaves_tokens_and_reports(dev, monkeypatch, stall_at):
     """Fault injection (the test build of the library, PPTK_RX_TEST_HOOKS):
