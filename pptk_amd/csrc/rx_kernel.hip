@@ -1652,8 +1652,17 @@ __device__ __forceinline__ void lane_tile(const RxKArgs &a, uint64_t tile, int l
     flush_records(a, wimg, tile, lane, 0u, false);
 }
 
+// (A/B: PPTK_RX_LANE_WAVES waves per SIMD the registers must allow;
+// PPTK_RX_LANE_PREFETCH 0 loads each tile at its start instead of one tile
+// ahead, for more waves in the same registers)
+#ifndef PPTK_RX_LANE_WAVES
+#define PPTK_RX_LANE_WAVES 4
+#endif
+#ifndef PPTK_RX_LANE_PREFETCH
+#define PPTK_RX_LANE_PREFETCH 1
+#endif
 template <bool NT>
-__global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
+__global__ __launch_bounds__(WAVE * WPB, PPTK_RX_LANE_WAVES) void rx_kernel_lane(RxKArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * WAVE * LSLOT];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
@@ -1665,6 +1674,7 @@ __global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
   // (uniform: the batch is one contiguous run of 64-byte frame slots)
   const bool coal = lane_coalesced(a.stride, a.fixed_len);
   uint64_t tile = tr.first;
+#if PPTK_RX_LANE_PREFETCH
   u32x4 c0[4], c1[4];
   lane_load<NT>(a, pf_tile(tr, ntiles, tile), lane, nch, coal, c0);
   while (tile < tr.end) {
@@ -1674,6 +1684,14 @@ __global__ __launch_bounds__(WAVE * WPB, 4) void rx_kernel_lane(RxKArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) c0[s] = c1[s];
   }
+#else
+  while (tile < tr.end) {
+    u32x4 c0[4];
+    lane_load<NT>(a, tile, lane, nch, coal, c0);
+    lane_tile<NT>(a, tile, lane, nch, coal, c0, wimg);
+    tile += step;
+  }
+#endif
 }
 
 // Header rewrite with incremental checksum updates (pptk_tx_rewrite_device,
